@@ -1,0 +1,252 @@
+"""Benchmark of the KGE negative-sample scoring step on MI355X.
+
+Metric (BASELINE.json): scored (pos+neg) triples/s, WN18RR InterHT d=1000 n_neg=256, 1/2/4/8 GPU.
+One step = the forward of supervisor.py:17-18 on one batch, i.e. TFKGEModel.call for the batch's
+negative mode (head/tail alternating, model.py:148-199) and for mode 3 (single, model.py:127-146):
+  * fused gather + InterHT score of B*N negatives   -> [B, N]   (kernel score_fwd_kernel)
+  * self-adversarial reduction                      -> [B, 1]   (neg_reduce_kernel)
+  * fused gather + score of the B positives         -> [B, 1]   (score_fwd_kernel, single)
+  * logsigmoid of the positives                     -> [B, 1]   (log_sigmoid_kernel)
+Scored triples per step = B*N + B (the reference's redundant branches, Q2, are not counted).
+
+Multi-GPU: one process per GPU (torchrun); each rank scores its own batch with its own replica
+of the table (weak scaling, no collective in the data path); timing = max over ranks.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import customknowledgegraphembedding_amd as kge  # noqa: E402
+from customknowledgegraphembedding_amd import ops  # noqa: E402
+from customknowledgegraphembedding_amd._lib import FN_IDS  # noqa: E402
+
+METRIC = "scored (pos+neg) triples/sec, WN18RR InterHT d=1000 n_neg=256, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    # BASELINE.json configs[1]: the metric's config
+    "c2": dict(name="WN18RR InterHT d=1000 -de -tr gamma=24 n_neg=256 bz=512", fn="InterHT",
+               nentity=40943, nrelation=11, hidden_dim=1000, gamma=24.0, de=True, tr=True, dr=False,
+               B=512, N=256),
+    # configs[2]
+    "c3": dict(name="FB15k-237 RotatE d=1000 -de gamma=9 n_neg=256 bz=512", fn="RotatE",
+               nentity=14541, nrelation=237, hidden_dim=1000, gamma=9.0, de=True, tr=False, dr=False,
+               B=512, N=256),
+    # configs[3] (single-GPU replica form)
+    "c4": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512", fn="DistMult",
+               nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False, dr=False,
+               B=512, N=1024),
+}
+
+
+def dims(w):
+    d = w["hidden_dim"]
+    ent = 2 * d if w["de"] else d
+    if w["tr"]:
+        rel = 3 * d
+    elif w["dr"]:
+        rel = 2 * d
+    else:
+        rel = d
+    D = ent // 2 if w["fn"] in ("ComplEx", "RotatE", "InterHT") else ent
+    rel_used = rel // 3 if w["fn"] == "InterHT" else rel
+    return ent, rel, D, rel_used
+
+
+def algorithmic_bytes(w):
+    """per negative launch = B*N*(4*ent_dim + 8 idx + 4 score) + the shared query
+    side B*(4*ent_dim + 4*rel_used + 24); per positive launch B*(8*ent_dim + 4*rel_used + 28)."""
+    ent, _, _, rel_used = dims(w)
+    B, N = w["B"], w["N"]
+    neg = B * N * (4 * ent + 8 + 4) + B * (4 * ent + 4 * rel_used + 24)
+    pos = B * (8 * ent + 4 * rel_used + 28)
+    return neg, pos
+
+
+def make_inputs(w, rank, device, n_batches=8):
+    ent_dim, rel_dim, D, _ = dims(w)
+    from customknowledgegraphembedding_amd.model import TFKGEModel
+    m = TFKGEModel(w["fn"], w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"],
+                   double_entity_embedding=w["de"], double_relation_embedding=w["dr"],
+                   triple_relation_embedding=w["tr"], device=device, seed=0)
+    E, R, B, N = w["nentity"], w["nrelation"], w["B"], w["N"]
+    batches = []
+    for i in range(n_batches):
+        g = np.random.RandomState(1 + 1000 * rank + i)
+        pos = np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1)
+        neg = np.random.RandomState(2 + 1000 * rank + i).randint(E, size=(B, N))
+        batches.append((torch.from_numpy(pos).to(device), torch.from_numpy(neg).to(device)))
+    return m, batches
+
+
+def run_step(m, pos, neg, mode, fn, ev=None):
+    """Forward of supervisor.py:17-18 with the raw HIP ops (no autograd bookkeeping)."""
+    ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
+    if ev is not None:
+        ev[0].record()
+    s = ops.score_indexed_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
+    if ev is not None:
+        ev[1].record()
+    n_red = ops.neg_reduce_raw(s, 1.0, True)
+    p = ops.score_indexed_raw(fn, 3, ent, rel, m._rel_off, pos, None, m._D, m._gamma_f, m._range_f)
+    p_ls = ops.log_sigmoid_raw(p)
+    return n_red, p_ls
+
+
+def cpu_baseline(w, budget_s=15.0, rows=64):
+    """The oracle's torch-CPU fp32 restatement of the reference graph (model.py:114-235 with all
+    three branches per call, Q2; two calls per step as supervisor.py:17-18) on a bounded sample:
+    `rows` batch rows x N negatives of the same workload. Returns a dict for the JSON line."""
+    from oracle import kge_oracle as O
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    cores = max(1, min(cores, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(cores)
+    ent_dim, rel_dim, D, _ = dims(w)
+    ent, rel, rng = O.make_tables(w["nentity"], w["nrelation"], ent_dim, rel_dim, w["gamma"],
+                                  w["hidden_dim"], seed=0, dtype=torch.float32)
+    g = np.random.RandomState(1)
+    E, R, N = w["nentity"], w["nrelation"], w["N"]
+    pos = torch.from_numpy(np.stack([g.randint(E, size=rows), g.randint(R, size=rows), g.randint(E, size=rows)], 1))
+    neg = torch.from_numpy(np.random.RandomState(2).randint(E, size=(rows, N)))
+    mod = 0.5 * rng
+
+    def faithful(mode):
+        with torch.no_grad():
+            O.tf_call(w["fn"], ent, rel, pos, neg, mode, w["gamma"], rng, mod)
+            O.tf_call(w["fn"], ent, rel, pos, neg, 3, w["gamma"], rng, mod)
+
+    def useful(mode):
+        with torch.no_grad():
+            O.tf_call_useful(w["fn"], ent, rel, pos, neg, mode, w["gamma"], rng, mod)
+            O.tf_call_useful(w["fn"], ent, rel, pos, neg, 3, w["gamma"], rng, mod)
+
+    res = {}
+    for tag, f in (("faithful", faithful), ("useful", useful)):
+        f(0)  # warm-up
+        times = []
+        t_end = time.perf_counter() + budget_s / 2
+        i = 0
+        while (len(times) < 3 or time.perf_counter() < t_end) and len(times) < 50:
+            t0 = time.perf_counter()
+            f(i % 2)
+            times.append(time.perf_counter() - t0)
+            i += 1
+        res[tag] = (statistics.median(times), len(times))
+    triples = rows * N + rows
+    try:
+        cpu_model = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
+    except Exception:  # noqa: BLE001
+        cpu_model = "unknown"
+    return {
+        "value": triples / res["faithful"][0],
+        "unit": "triples/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": (f"{rows} batch rows x {N} negatives of {w['name']}: oracle torch-CPU fp32 restatement of "
+                   f"the reference TF graph (2 calls/step, all 3 branches each, Q2), median of "
+                   f"{res['faithful'][1]} steps"),
+        "useful_only_value": triples / res["useful"][0],
+        "cpu_model": cpu_model,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    w = WORKLOADS[a.workload]
+    fn = FN_IDS[w["fn"]]
+    m, batches = make_inputs(w, rank, device)
+    B, N = w["B"], w["N"]
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+
+    for i in range(a.warmup):
+        pos, neg = batches[i % len(batches)]
+        run_step(m, pos, neg, i % 2, fn)
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        pos, neg = batches[i % len(batches)]
+        run_step(m, pos, neg, i % 2, fn, evs[i])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    neg_bytes, pos_bytes = algorithmic_bytes(w)
+    kern_avg_s = statistics.mean(kern_ms) / 1e3
+    achieved = neg_bytes / kern_avg_s / 1e9
+    triples = (B * N + B) * a.steps * world
+    value = triples / elapsed
+    line = {
+        "metric": METRIC if a.workload == "c2" else f"scored (pos+neg) triples/sec, {w['name']}",
+        "value": value,
+        "unit": "triples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: U(-(gamma+2)/d,(gamma+2)/d) tables (seed 0), uniform random (h,r,t) positives and "
+                "negatives, 8 distinct batches resident in HBM, mode alternating head/tail",
+        "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N, "hidden_dim": w["hidden_dim"],
+                   "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "score_fwd_kernel (negatives)", "kernel_avg_us": kern_avg_s * 1e6,
+                     "algorithmic_bytes_per_launch": neg_bytes},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(w, a.cpu_budget)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,103 @@
+"""ctypes binding of libkge_hip.so (the C-ABI declared in include/kge_hip.h).
+
+This is the Python-side stub a maintainer of the reference would add next to
+tensorflow_codes/model.py. There is deliberately NO fallback: if the
+shared library is missing or fails to load, every scoring call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("KGE_HIP_LIB", os.path.join(_HERE, "libkge_hip.so"))
+
+# enum kge_fn (include/kge_hip.h)
+FN_IDS = {
+    "TransE": 0,
+    "DistMult": 1,
+    "ComplEx": 2,
+    "RotatE": 3,
+    "InterHT": 4,
+    "pRotatE": 5,
+}
+# enum kge_mode — the TF reference's integer mode codes (model.py:124,203; supervisor.py:18)
+HEAD_BATCH, TAIL_BATCH, SINGLE = 0, 1, 3
+
+_c_i64 = ctypes.c_int64
+_c_f = ctypes.c_float
+_c_p = ctypes.c_void_p
+_c_i = ctypes.c_int
+
+# exported symbol -> (restype, argtypes)
+SIGNATURES = {
+    "kge_abi_version": (_c_i, []),
+    "kge_last_error": (ctypes.c_char_p, []),
+    "kge_max_dim": (_c_i64, [_c_i]),
+    "kge_score_indexed": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_i64, _c_p],
+    ),
+    "kge_score_dense": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64,
+         _c_f, _c_f, _c_f, _c_p, _c_i64, _c_p],
+    ),
+    "kge_score_dense_bwd": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64,
+         _c_f, _c_f, _c_f, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p],
+    ),
+    "kge_neg_reduce": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_f, _c_i, _c_p, _c_p]),
+    "kge_neg_reduce_bwd": (
+        _c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_f, _c_i, _c_i, _c_p, _c_p, _c_i64, _c_p]),
+    "kge_log_sigmoid": (_c_i, [_c_p, _c_i64, _c_p, _c_p]),
+    "kge_log_sigmoid_bwd": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p]),
+    "kge_score_bwd_workspace_size": (_c_i64, [_c_i, _c_i, _c_i64, _c_i64, _c_i64]),
+    "kge_score_indexed_bwd": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p],
+    ),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class KGEHipError(RuntimeError):
+    """A libkge_hip.so entry point returned a non-zero status (message from kge_last_error)."""
+
+
+def load(path: str | None = None):
+    """Load libkge_hip.so once. torch is imported first so that the library binds to the HIP
+    runtime torch already loaded (same SONAME libamdhip64.so.7) and shares its streams."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        import torch  # noqa: F401  (HIP runtime first)
+
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise KGEHipError(
+                f"libkge_hip.so not found at {p}: build it with `make -C {_HERE}` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.kge_abi_version() != 1:
+            raise KGEHipError(f"ABI version mismatch: {lib.kge_abi_version()} != 1")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().kge_last_error().decode(errors="replace")
+        raise KGEHipError(f"{what} failed (rc={rc}): {msg}")

@@ -1,0 +1,243 @@
+"""KGE models on PyTorch-ROCm tensors whose scoring runs in libkge_hip.so.
+
+Two drop-in classes share the tables and the fused HIP scoring path:
+
+* ``TFKGEModel`` mirrors ``tensorflow_codes/model.py:47-235`` — constructor flags (including the
+  dead ``-dr`` flag, Q5), ``model_func`` plugin dict, and ``call(((pos, neg), mode))`` returning
+  ``[B, 1]``: ``logsigmoid(score)`` for mode 3 (model.py:145) and the self-adversarial reduction
+  ``sum softmax(s) * logsigmoid(-s)`` for the negative modes (model.py:168-171,195-198; Q1, Q3, Q4).
+* ``KGEModel`` mirrors the upstream PyTorch ``KnowledgeGraphEmbedding/codes/model.py``
+  (absent from the snapshot; restated from its published code): ``forward(sample, mode)`` returns
+  raw scores ``[B, 1|N]`` and the static ``train_step`` / ``test_step`` drive training / eval.
+
+Deliberate deviation from the TF graph: ``call`` evaluates only the branch the mode
+selects instead of all three blended with 0/1 masks. Outputs are identical except that the
+reference would turn a NaN/Inf in an unused branch into a NaN output (0 * NaN); we do not.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import FN_IDS, HEAD_BATCH, SINGLE, TAIL_BATCH
+
+SPLIT_ENTITY = {"ComplEx", "RotatE", "InterHT"}
+
+
+def _dims_for(model_name, entity_dim, relation_dim):
+    """Per-half width D and relation offset for a score function, validating the table widths the
+    way the reference's broadcasting would (it raises on a mismatch)."""
+    if model_name in ("TransE", "DistMult", "pRotatE"):
+        if entity_dim != relation_dim:
+            raise ValueError(f"{model_name} needs entity_dim == relation_dim, got {entity_dim} / {relation_dim}")
+        return entity_dim, 0
+    if model_name == "ComplEx":
+        if entity_dim % 2 or relation_dim != entity_dim:
+            raise ValueError("ComplEx needs double entity and double relation embeddings")
+        return entity_dim // 2, 0
+    if model_name == "RotatE":
+        if entity_dim % 2 or relation_dim * 2 != entity_dim:
+            raise ValueError("RotatE needs a double entity embedding and a single relation embedding")
+        return entity_dim // 2, 0
+    if model_name == "InterHT":
+        # model.py:208-210: entity split in 2, relation split in 3, middle third used (Q6)
+        if entity_dim % 2 or relation_dim % 3 or entity_dim // 2 != relation_dim // 3:
+            raise ValueError("InterHT needs -de and -tr (entity 2d, relation 3d)")
+        return entity_dim // 2, entity_dim // 2
+    if model_name == "TranSparse":
+        raise NotImplementedError("TranSparse (model.py:226-235) has no HIP kernel yet")
+    raise ValueError(f"model {model_name} not supported")
+
+
+class _KGEBase(nn.Module):
+    """Tables + the fused scoring entry shared by both model classes."""
+
+    def _init_tables(self, nentity, nrelation, entity_dim, relation_dim, init_range, device, seed):
+        g = torch.Generator().manual_seed(int(seed))
+        ent = torch.empty(nentity, entity_dim).uniform_(-init_range, init_range, generator=g)
+        rel = torch.empty(nrelation, relation_dim).uniform_(-init_range, init_range, generator=g)
+        self.entity_embedding = nn.Parameter(ent.to(device))
+        self.relation_embedding = nn.Parameter(rel.to(device))
+
+    def _make_model_func(self):
+        def plugin(name):
+            fn = FN_IDS[name]
+
+            def model_func(head, relation, tail, mode, *extra):
+                m = ops.mode_id(mode)
+                ew = head.shape[-1]
+                D = ew // 2 if name in SPLIT_ENTITY else ew
+                rel_off = D if name == "InterHT" else 0
+                mod = float(self.modulus.reshape(-1)[0]) if name == "pRotatE" else 0.0
+                return ops.score_dense(fn, m, head, relation, tail, D, self._gamma_f, self._range_f,
+                                       rel_off=rel_off, modulus=mod)
+
+            model_func.__name__ = name
+            return model_func
+
+        return {name: plugin(name) for name in FN_IDS}
+
+    # fused gather + score (no [B, N, d] tensor is ever built)
+    def score(self, mode, positive_sample, negative_sample=None):
+        fn = FN_IDS[self.model_name]
+        modulus = self.modulus if self.model_name == "pRotatE" else None
+        return ops.score_indexed(fn, mode, self.entity_embedding, self.relation_embedding,
+                                 positive_sample, negative_sample, self._D, self._gamma_f,
+                                 self._range_f, rel_off=self._rel_off, modulus=modulus)
+
+    def extra_repr(self):
+        return (f"model_name={self.model_name}, nentity={self.nentity}, nrelation={self.nrelation}, "
+                f"entity_dim={self.entity_dim}, relation_dim={self.relation_dim}, gamma={self._gamma_f}")
+
+
+class TFKGEModel(_KGEBase):
+    """Drop-in for ``TFKGEModel`` (tensorflow_codes/model.py:47-235)."""
+
+    def __init__(self, model_name, nentity, nrelation, hidden_dim, gamma,
+                 double_entity_embedding=False, double_relation_embedding=False,
+                 triple_relation_embedding=False, device=None, seed=0, **kwargs):
+        super().__init__()
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        self.model_name = model_name
+        self.nentity = nentity
+        self.nrelation = nrelation
+        self.hidden_dim = hidden_dim
+        self.epsilon = 2.0  # model.py:58
+        g32 = torch.tensor([gamma], dtype=torch.float32)
+        self.gamma = nn.Parameter(g32.clone(), requires_grad=False)  # model.py:60
+        # model.py:62-63: (gamma.numpy() + epsilon) / hidden_dim, evaluated in float32
+        rng = (g32 + torch.tensor(self.epsilon, dtype=torch.float32)) / hidden_dim
+        self.embedding_range = nn.Parameter(rng.clone(), requires_grad=False)
+
+        # model.py:65-78 — Q5: the -dr result is overwritten by the -tr branch, so -dr is dead.
+        # ComplEx cannot be built at all without a double relation, so there (only) -dr is honoured.
+        relation_dim = hidden_dim * 2 if double_relation_embedding else hidden_dim
+        entity_dim = hidden_dim * 2 if double_entity_embedding else hidden_dim
+        if triple_relation_embedding:
+            relation_dim = hidden_dim * 3
+        elif not (model_name == "ComplEx" and double_relation_embedding):
+            relation_dim = hidden_dim
+        self.entity_dim, self.relation_dim = entity_dim, relation_dim
+
+        # model.py:86-91 (Q8): U(-(gamma+2)/d, (gamma+2)/d) for both tables (torch RNG, seeded)
+        self._init_tables(nentity, nrelation, entity_dim, relation_dim, float(rng[0]), device, seed)
+        if model_name == "InterHT":
+            self.u = 1  # model.py:94-95 (the kernel hard-codes u = 1)
+        if model_name == "pRotatE":
+            self.modulus = nn.Parameter(torch.tensor([[0.5 * float(rng[0])]], device=device))
+        self._gamma_f = float(g32[0])
+        self._range_f = float(rng[0])
+        self._D, self._rel_off = _dims_for(model_name, entity_dim, relation_dim)
+        self.model_func = self._make_model_func()  # model.py:109-112
+
+    def forward(self, sample, training=True, **kwargs):
+        """``call(((positive_sample, negative_sample), mode))`` -> [B, 1] (model.py:114-205)."""
+        (positive_sample, negative_sample), mode = sample
+        m = ops.mode_id(mode)
+        if m == SINGLE:  # positive_call -> single_mode (model.py:117-146)
+            return ops.log_sigmoid(self.score(SINGLE, positive_sample))
+        # negative_call (model.py:121-125): head_batch_mode if mode == 0 else tail_batch_mode
+        s = self.score(m, positive_sample, negative_sample)
+        return ops.neg_reduce(s, temperature=1.0, adversarial=True, detach=False).unsqueeze(1)
+
+    call = forward
+
+
+class KGEModel(_KGEBase):
+    """Drop-in for the upstream PyTorch ``KGEModel`` (KnowledgeGraphEmbedding/codes/model.py)."""
+
+    def __init__(self, model_name, nentity, nrelation, hidden_dim, gamma,
+                 double_entity_embedding=False, double_relation_embedding=False,
+                 device=None, seed=0):
+        super().__init__()
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        self.model_name = model_name
+        self.nentity = nentity
+        self.nrelation = nrelation
+        self.hidden_dim = hidden_dim
+        self.epsilon = 2.0
+        self.gamma = nn.Parameter(torch.Tensor([gamma]), requires_grad=False)
+        self.embedding_range = nn.Parameter(
+            torch.Tensor([(self.gamma.item() + self.epsilon) / hidden_dim]), requires_grad=False)
+        self.entity_dim = hidden_dim * 2 if double_entity_embedding else hidden_dim
+        self.relation_dim = hidden_dim * 2 if double_relation_embedding else hidden_dim
+        if model_name not in ("TransE", "DistMult", "ComplEx", "RotatE", "pRotatE", "InterHT"):
+            raise ValueError("model %s not supported" % model_name)
+        if model_name == "RotatE" and (not double_entity_embedding or double_relation_embedding):
+            raise ValueError("RotatE should use --double_entity_embedding")
+        if model_name == "ComplEx" and (not double_entity_embedding or not double_relation_embedding):
+            raise ValueError("ComplEx should use --double_entity_embedding and --double_relation_embedding")
+        rng = self.embedding_range.item()
+        self._init_tables(nentity, nrelation, self.entity_dim, self.relation_dim, rng, device, seed)
+        if model_name == "pRotatE":
+            self.modulus = nn.Parameter(torch.Tensor([[0.5 * rng]]).to(device))
+        self._gamma_f = float(self.gamma.item())
+        self._range_f = float(self.embedding_range.item())
+        self._D, self._rel_off = _dims_for(model_name, self.entity_dim, self.relation_dim)
+        self.model_func = self._make_model_func()
+
+    def forward(self, sample, mode="single"):
+        if mode == "single":
+            return self.score(SINGLE, sample)
+        if mode == "head-batch":
+            tail_part, head_part = sample
+            return self.score(HEAD_BATCH, tail_part, head_part)
+        if mode == "tail-batch":
+            head_part, tail_part = sample
+            return self.score(TAIL_BATCH, head_part, tail_part)
+        raise ValueError("mode %s not supported" % mode)
+
+    @staticmethod
+    def train_step(model, optimizer, train_iterator, args):
+        """Upstream ``KGEModel.train_step``: one optimisation step on one batch; returns the log."""
+        model.train()
+        optimizer.zero_grad()
+        positive_sample, negative_sample, subsampling_weight, mode = next(train_iterator)
+        dev = model.entity_embedding.device
+        positive_sample = positive_sample.to(dev, non_blocking=True)
+        negative_sample = negative_sample.to(dev, non_blocking=True)
+        subsampling_weight = subsampling_weight.to(dev, non_blocking=True).reshape(-1)
+
+        negative_score = model((positive_sample, negative_sample), mode=mode)
+        if args.negative_adversarial_sampling:
+            # self-adversarial weights are detached upstream
+            negative_score = ops.neg_reduce(negative_score, args.adversarial_temperature,
+                                            adversarial=True, detach=True)
+        else:
+            negative_score = ops.neg_reduce(negative_score, 1.0, adversarial=False)
+        positive_score = ops.log_sigmoid(model(positive_sample)).squeeze(dim=1)
+
+        if args.uni_weight:
+            positive_sample_loss = -positive_score.mean()
+            negative_sample_loss = -negative_score.mean()
+        else:
+            positive_sample_loss = -(subsampling_weight * positive_score).sum() / subsampling_weight.sum()
+            negative_sample_loss = -(subsampling_weight * negative_score).sum() / subsampling_weight.sum()
+        loss = (positive_sample_loss + negative_sample_loss) / 2
+        if args.regularization != 0.0:
+            regularization = args.regularization * (
+                model.entity_embedding.norm(p=3) ** 3 + model.relation_embedding.norm(p=3).norm(p=3) ** 3)
+            loss = loss + regularization
+            regularization_log = {"regularization": regularization.item()}
+        else:
+            regularization_log = {}
+        loss.backward()
+        optimizer.step()
+        log = {
+            **regularization_log,
+            "positive_sample_loss": positive_sample_loss.item(),
+            "negative_sample_loss": negative_sample_loss.item(),
+            "loss": loss.item(),
+        }
+        return log
+
+
+def default_hidden_range(gamma, hidden_dim, epsilon=2.0):
+    """(gamma + epsilon) / hidden_dim (model.py:62,86)."""
+    return (gamma + epsilon) / hidden_dim
+
+
+__all__ = ["TFKGEModel", "KGEModel", "default_hidden_range"]

@@ -1,0 +1,160 @@
+/*
+ * kge_hip.h — C-ABI of libkge_hip.so, the MI355X (gfx950) knowledge-graph-embedding scoring path.
+ *
+ * This is the drop-in boundary for the hot path of NguyenThaiHoc1/CustomKnowledgeGraphEmbedding:
+ * the score-function plugins (`TFKGEModel.model_func`, tensorflow_codes/model.py:109-112), the
+ * per-mode gather + score + reduce of `TFKGEModel.call` (model.py:114-205), and the embedding
+ * lookup / score path of the upstream PyTorch `KGEModel.forward` (KnowledgeGraphEmbedding/codes/
+ * model.py — absent from the snapshot, restated in oracle/kge_oracle.py).
+ *
+ * Contract (all entry points):
+ *   - every pointer is caller-owned DEVICE memory (the library never allocates or frees);
+ *   - every launch is asynchronous on the caller's hipStream_t (`stream`, may be NULL = default
+ *     stream); no host synchronisation happens inside the library, so calls are graph-capturable;
+ *   - return 0 on success or a negative errno-style code (KGE_EINVAL, KGE_ENOTSUP, KGE_EHIP);
+ *     the message for the calling thread is in kge_last_error();
+ *   - forward results are deterministic (fixed reduction order, no atomics);
+ *   - an out-of-range entity/relation index reads a ZERO row, like TF's GPU `tf.gather`
+ *     (model.py:130-136,152-158,178-185); it never faults.
+ *
+ * Layout: tables are row-major fp32, row i of the entity table at ent + i*ent_ld.
+ *   Split models keep the two halves of a row back to back: [re | im] for ComplEx/RotatE,
+ *   [a | b] for InterHT (model.py:208,210), so a row holds 2*D floats; D is the per-half width
+ *   (= hidden_dim). TransE/DistMult rows hold D floats.
+ *   The relation part a score function reads starts at rel + r*rel_ld + rel_off: InterHT reads
+ *   only the middle third (re_mid, model.py:209 -> rel_off = D), everything else rel_off = 0.
+ */
+#ifndef KGE_HIP_H
+#define KGE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KGE_ABI_VERSION 1
+
+/* score functions: model_func keys (model.py:109-112 + upstream codes/model.py model_func) */
+enum kge_fn {
+    KGE_TRANSE = 0,   /* upstream TransE:   gamma - ||h + r - t||_1                        */
+    KGE_DISTMULT = 1, /* upstream DistMult: sum(h * r * t)                                  */
+    KGE_COMPLEX = 2,  /* upstream ComplEx:  Re<h, r, conj(t)>                               */
+    KGE_ROTATE = 3,   /* upstream RotatE:   gamma - sum |h o e^{i theta_r} - t|             */
+    KGE_INTERHT = 4,  /* model.py:207-224                                                   */
+    KGE_PROTATE = 5   /* upstream pRotatE:  gamma - modulus * sum |sin(ph_h + ph_r - ph_t)| */
+};
+
+/* mode codes of the TF reference (Q1: model.py:124,203; supervisor.py:18) */
+enum kge_mode {
+    KGE_HEAD_BATCH = 0, /* candidates replace the head  (model.py:148-172) */
+    KGE_TAIL_BATCH = 1, /* candidates replace the tail  (model.py:174-199) */
+    KGE_SINGLE = 3      /* the positive triple only     (model.py:127-146) */
+};
+
+#define KGE_EINVAL (-22)
+#define KGE_ENOTSUP (-95)
+#define KGE_EHIP (-1000)
+
+/* Version of this ABI (KGE_ABI_VERSION). */
+int kge_abi_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* kge_last_error(void);
+
+/* Largest per-half width D the forward kernels accept for a score function (in floats). */
+int64_t kge_max_dim(int fn);
+
+/*
+ * Fused gather + score (replaces model.py:127-137,148-159,174-185 gathers + model_func calls at
+ * :139-144,161-166,187-192; upstream KGEModel.forward gathers + model_func).
+ *   pos    [B,3] int64 (h, r, t) rows of the batch, row stride 3
+ *   neg    [B,N] int64 candidate entity ids (row stride neg_ld); ignored for KGE_SINGLE
+ *   scores [B,N] fp32 raw scores out (row stride scores_ld); N is forced to 1 for KGE_SINGLE
+ *   gamma, emb_range: model.py:60-63 (emb_range = (gamma + 2) / hidden_dim);
+ *   modulus: pRotatE only (upstream 0.5 * emb_range initial value; pass the current parameter).
+ */
+int kge_score_indexed(int fn, int mode,
+                      const float* ent, int64_t nentity, int64_t ent_ld,
+                      const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off,
+                      const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                      int64_t B, int64_t N, int64_t D,
+                      float gamma, float emb_range, float modulus,
+                      float* scores, int64_t scores_ld, void* stream);
+
+/*
+ * Score pre-gathered rows: the model_func plugin surface itself,
+ * `model_func[name](head, relation, tail, mode) -> [B, 1|N]` (model.py:109-112,207).
+ *   head [B, Nh, *] rows (row stride head_ld), Nh = N for KGE_HEAD_BATCH else 1
+ *   rel  [B, *]     rows (row stride rel_ld), the used part starts at rel_off
+ *   tail [B, Nt, *] rows (row stride tail_ld), Nt = N for KGE_TAIL_BATCH else 1
+ */
+int kge_score_dense(int fn, int mode,
+                    const float* head, int64_t head_ld,
+                    const float* rel, int64_t rel_ld, int64_t rel_off,
+                    const float* tail, int64_t tail_ld,
+                    int64_t B, int64_t N, int64_t D,
+                    float gamma, float emb_range, float modulus,
+                    float* scores, int64_t scores_ld, void* stream);
+
+/*
+ * Per-row negative reduction of TFKGEModel (model.py:168-171,195-198; Q3) and upstream train_step:
+ *   adversarial != 0: out[b] = sum_n softmax(T * s[b,:])_n * logsigmoid(-s[b,n])
+ *   adversarial == 0: out[b] = mean_n logsigmoid(-s[b,n])
+ * scores [B,N] (row stride ld), out [B].
+ */
+int kge_neg_reduce(const float* scores, int64_t B, int64_t N, int64_t ld,
+                   float temperature, int adversarial, float* out, void* stream);
+
+/* out[i] = logsigmoid(x[i]) (model.py:145), n elements. */
+int kge_log_sigmoid(const float* x, int64_t n, float* out, void* stream);
+
+/*
+ * Backward of kge_neg_reduce: d_scores[b,n] = d_out[b] * d(out[b])/d(s[b,n]).
+ *   detach != 0 stops the gradient through the softmax weights (upstream `.detach()`);
+ *   detach == 0 is the TF reference (Q3: model.py:168-171 does not stop it).
+ */
+int kge_neg_reduce_bwd(const float* scores, int64_t B, int64_t N, int64_t ld,
+                       float temperature, int adversarial, int detach,
+                       const float* d_out, float* d_scores, int64_t d_ld, void* stream);
+
+/* d_x[i] = d_out[i] * sigmoid(-x[i])  (backward of kge_log_sigmoid). */
+int kge_log_sigmoid_bwd(const float* x, const float* d_out, int64_t n, float* d_x, void* stream);
+
+/*
+ * Backward of kge_score_indexed (GradientTape through the gathers, supervisor.py:25).
+ * Accumulates (+=) into d_ent [nentity, ent_ld] and d_rel [nrelation, rel_ld] (same strides as
+ * the tables). The query-side rows get one deterministic per-row sum over the N candidates; the
+ * candidate rows are scattered with fp32 atomics (order of accumulation between candidates that hit
+ * the same entity is not fixed: results are reproducible to fp32 rounding, not bitwise).
+ * workspace: device scratch of kge_score_bwd_workspace_size(...) bytes (caller-owned).
+ */
+int64_t kge_score_bwd_workspace_size(int fn, int mode, int64_t B, int64_t N, int64_t D);
+int kge_score_indexed_bwd(int fn, int mode,
+                          const float* ent, int64_t nentity, int64_t ent_ld,
+                          const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off,
+                          const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                          int64_t B, int64_t N, int64_t D,
+                          float gamma, float emb_range, float modulus,
+                          const float* d_scores, int64_t d_ld,
+                          float* d_ent, float* d_rel, float* d_modulus,
+                          void* workspace, void* stream);
+
+/*
+ * Backward of kge_score_dense (gradient of the model_func plugin w.r.t. its gathered inputs).
+ * Accumulates (+=) into d_head / d_rel / d_tail, laid out like head / rel / tail.
+ */
+int kge_score_dense_bwd(int fn, int mode,
+                        const float* head, int64_t head_ld,
+                        const float* rel, int64_t rel_ld, int64_t rel_off,
+                        const float* tail, int64_t tail_ld,
+                        int64_t B, int64_t N, int64_t D,
+                        float gamma, float emb_range, float modulus,
+                        const float* d_scores, int64_t d_ld,
+                        float* d_head, float* d_rel, float* d_tail, float* d_modulus, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KGE_HIP_H */

@@ -1,0 +1,108 @@
+"""CPU tests of the C-ABI boundary: libkge_hip.so loads, exports every symbol include/kge_hip.h
+declares, and rejects bad arguments with the documented codes before touching the GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+import customknowledgegraphembedding_amd as kge
+from customknowledgegraphembedding_amd import _lib, ops
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "kge_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(kge_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("kge_score_indexed", "kge_score_dense", "kge_neg_reduce", "kge_score_indexed_bwd",
+              "kge_last_error", "kge_abi_version"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_every_declared_symbol():
+    assert sorted(_lib.SIGNATURES) == declared_symbols()
+
+
+def test_abi_version_and_limits():
+    lib = kge.load()
+    assert lib.kge_abi_version() == 1
+    assert lib.kge_max_dim(4) == 2048
+    assert lib.kge_max_dim(99) == 0
+    assert lib.kge_score_bwd_workspace_size(4, 1, 512, 256, 1000) >= 0
+
+
+def test_bad_arguments_are_rejected_without_a_launch():
+    lib = kge.load()
+    dummy = ctypes.c_void_p(16)
+    # unknown score function id
+    rc = lib.kge_score_indexed(99, 1, dummy, 10, 4, dummy, 2, 4, 0, dummy, dummy, 4, 2, 4, 4,
+                               1.0, 1.0, 0.0, dummy, 4, None)
+    assert rc == -22 and b"score function" in lib.kge_last_error()
+    # bad mode
+    rc = lib.kge_score_indexed(0, 7, dummy, 10, 4, dummy, 2, 4, 0, dummy, dummy, 4, 2, 4, 4,
+                               1.0, 1.0, 0.0, dummy, 4, None)
+    assert rc == -22 and b"mode" in lib.kge_last_error()
+    # missing pos / neg
+    rc = lib.kge_score_indexed(0, 1, dummy, 10, 4, dummy, 2, 4, 0, None, dummy, 4, 2, 4, 4,
+                               1.0, 1.0, 0.0, dummy, 4, None)
+    assert rc == -22
+    rc = lib.kge_score_indexed(0, 1, dummy, 10, 4, dummy, 2, 4, 0, dummy, None, 4, 2, 4, 4,
+                               1.0, 1.0, 0.0, dummy, 4, None)
+    assert rc == -22
+    # dimension beyond the register-resident limit
+    rc = lib.kge_score_indexed(1, 1, dummy, 10, 4096, dummy, 2, 4096, 0, dummy, dummy, 4, 2, 4, 4096,
+                               1.0, 1.0, 0.0, dummy, 4, None)
+    assert rc == -95 and b"exceeds" in lib.kge_last_error()
+    # empty problems are a successful no-op
+    assert lib.kge_score_indexed(0, 1, dummy, 10, 4, dummy, 2, 4, 0, dummy, dummy, 4, 0, 4, 4,
+                                 1.0, 1.0, 0.0, dummy, 4, None) == 0
+    assert lib.kge_neg_reduce(dummy, 0, 4, 4, 1.0, 1, dummy, None) == 0
+    assert lib.kge_neg_reduce(dummy, 2, 0, 4, 1.0, 1, dummy, None) == -22
+
+
+def test_check_raises_with_message():
+    lib = kge.load()
+    dummy = ctypes.c_void_p(16)
+    rc = lib.kge_score_indexed(0, 9, dummy, 10, 4, dummy, 2, 4, 0, dummy, dummy, 4, 2, 4, 4,
+                               1.0, 1.0, 0.0, dummy, 4, None)
+    with pytest.raises(kge.KGEHipError, match="mode"):
+        _lib.check(rc, "kge_score_indexed")
+
+
+def test_no_cpu_fallback():
+    ent = torch.zeros(10, 8)
+    rel = torch.zeros(3, 8)
+    pos = torch.zeros(2, 3, dtype=torch.int64)
+    neg = torch.zeros(2, 4, dtype=torch.int64)
+    with pytest.raises(kge.KGEHipError, match="no CPU fallback"):
+        ops.score_indexed_raw(0, 1, ent, rel, 0, pos, neg, 8, 1.0, 1.0)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(kge.KGEHipError, match="not found"):
+        _lib.load(str(tmp_path / "nope.so"))
+
+
+def test_mode_codes_q1():
+    assert ops.mode_id(0) == kge.HEAD_BATCH
+    assert ops.mode_id(1) == kge.TAIL_BATCH
+    assert ops.mode_id(2) == kge.TAIL_BATCH  # model.py:124: anything but 0 is tail-batch
+    assert ops.mode_id(3) == kge.SINGLE
+    assert ops.mode_id("head-batch") == kge.HEAD_BATCH
+    assert ops.mode_id(torch.tensor(0)) == kge.HEAD_BATCH
+    with pytest.raises(ValueError):
+        ops.mode_id("sideways")

@@ -1,0 +1,53 @@
+"""CPU tests of the host-side model mirrors (construction, dims, validation, plugin surface)."""
+import pytest
+import torch
+
+from customknowledgegraphembedding_amd import KGEModel, TFKGEModel
+from customknowledgegraphembedding_amd.model import _dims_for
+from oracle import kge_oracle as O
+
+
+def test_tf_model_dims_match_reference_flags():
+    m = TFKGEModel("InterHT", 40, 3, 10, 24.0, True, True, True, device="cpu")
+    assert (m.entity_dim, m.relation_dim) == O.tf_dims("InterHT", 10, True, True, True) == (20, 30)
+    assert m.u == 1 and m.epsilon == 2.0
+    assert abs(float(m.embedding_range) - 2.6) < 1e-6
+    assert m._D == 10 and m._rel_off == 10
+
+
+def test_tf_model_tables_follow_q8_and_oracle_rng():
+    m = TFKGEModel("InterHT", 40, 3, 10, 24.0, True, False, True, device="cpu", seed=5)
+    ent, rel, rng = O.make_tables(40, 3, 20, 30, 24.0, 10, seed=5)
+    assert torch.equal(m.entity_embedding.detach(), ent)
+    assert torch.equal(m.relation_embedding.detach(), rel)
+
+
+def test_interht_without_tr_is_rejected_like_the_reference_shapes():
+    with pytest.raises(ValueError):
+        TFKGEModel("InterHT", 40, 3, 10, 24.0, True, False, False, device="cpu")
+
+
+def test_model_func_plugin_surface():
+    m = TFKGEModel("InterHT", 40, 3, 10, 24.0, True, False, True, device="cpu")
+    for name in ("TransE", "DistMult", "ComplEx", "RotatE", "InterHT", "pRotatE"):
+        assert callable(m.model_func[name])
+
+
+def test_upstream_model_validation():
+    with pytest.raises(ValueError, match="RotatE"):
+        KGEModel("RotatE", 10, 2, 8, 12.0, double_entity_embedding=False, device="cpu")
+    with pytest.raises(ValueError, match="ComplEx"):
+        KGEModel("ComplEx", 10, 2, 8, 12.0, double_entity_embedding=True, device="cpu")
+    m = KGEModel("ComplEx", 10, 2, 8, 12.0, True, True, device="cpu")
+    assert (m.entity_dim, m.relation_dim, m._D) == (16, 16, 8)
+    m = KGEModel("RotatE", 10, 2, 8, 12.0, True, False, device="cpu")
+    assert (m.entity_dim, m.relation_dim, m._D) == (16, 8, 8)
+
+
+def test_dims_for_errors():
+    with pytest.raises(ValueError):
+        _dims_for("TransE", 10, 20)
+    with pytest.raises(NotImplementedError):
+        _dims_for("TranSparse", 10, 10)
+    with pytest.raises(ValueError):
+        _dims_for("Nope", 10, 10)

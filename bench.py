@@ -93,17 +93,17 @@ def make_inputs(w, rank, device, n_batches=8):
 
 
 def run_step(m, pos, neg, mode, fn, ev=None):
-    """Forward of supervisor.py:17-18 with the raw HIP ops (no autograd bookkeeping)."""
+    """Forward of supervisor.py:17-18 (both model calls) = kge_step_forward, issued as its two
+    halves so the dominant kernel can be bracketed by events on its own stream:
+    kge_score_indexed (fused negative gather + score) then kge_step_finish (positives + per-row
+    self-adversarial reductions)."""
     ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
     if ev is not None:
         ev[0].record()
-    s = ops.score_indexed_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
+    ns = ops.score_indexed_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
     if ev is not None:
         ev[1].record()
-    n_red = ops.neg_reduce_raw(s, 1.0, True)
-    p = ops.score_indexed_raw(fn, 3, ent, rel, m._rel_off, pos, None, m._D, m._gamma_f, m._range_f)
-    p_ls = ops.log_sigmoid_raw(p)
-    return n_red, p_ls
+    return ops.step_finish_raw(fn, ent, rel, m._rel_off, pos, m._D, m._gamma_f, m._range_f, ns)
 
 
 def cpu_baseline(w, budget_s=15.0, rows=64):

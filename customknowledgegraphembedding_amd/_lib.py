@@ -40,6 +40,16 @@ SIGNATURES = {
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_i64, _c_p],
     ),
+    "kge_step_forward": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p],
+    ),
+    "kge_step_finish": (
+        _c_i,
+        [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64,
+         _c_f, _c_f, _c_f, _c_p, _c_i64, _c_i64, _c_f, _c_i, _c_p, _c_p, _c_p, _c_p],
+    ),
     "kge_score_dense": (
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64,

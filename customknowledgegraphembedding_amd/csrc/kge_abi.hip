@@ -1,0 +1,434 @@
+// kge_abi.hip — the C-ABI of libkge_hip.so (include/kge_hip.h): argument checking, kernel
+// selection, the per-row reduction kernels and the extern "C" entry points.
+#include <string.h>
+
+#include <string>
+
+#include "kge_device.h"
+
+namespace kge_impl {
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Per-row reductions (model.py:145, 168-171, 195-198; upstream train_step). One wave per row.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void neg_reduce_kernel(const float* __restrict__ s, int64_t B, int64_t N,
+                                                            int64_t ld, float T, int adversarial,
+                                                            float* __restrict__ out) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= B) return;
+    const int lane = threadIdx.x & 63;
+    const float res = row_reduce(s + b * ld, N, T, adversarial, lane);
+    if (lane == 0) out[b] = res;
+}
+
+__global__ __launch_bounds__(kBlock) void neg_reduce_bwd_kernel(const float* __restrict__ s, int64_t B, int64_t N,
+                                                                int64_t ld, float T, int adversarial, int detach,
+                                                                const float* __restrict__ d_out,
+                                                                float* __restrict__ d_s, int64_t d_ld) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= B) return;
+    const int lane = threadIdx.x & 63;
+    const float* row = s + b * ld;
+    float* drow = d_s + b * d_ld;
+    const float go = d_out[b];
+    if (adversarial) {
+        float m = -INFINITY;
+        for (int64_t n = lane; n < N; n += kWave) m = fmaxf(m, T * row[n]);
+        m = wave_max(m);
+        float z = 0.f, w = 0.f;
+        for (int64_t n = lane; n < N; n += kWave) {
+            const float x = row[n];
+            const float e = expf(T * x - m);
+            z += e;
+            w += e * log_sigmoid(-x);
+        }
+        z = wave_sum(z);
+        w = wave_sum(w);
+        const float outv = w / z;
+        // d/ds_n [sum_m p_m L_m] = p_n * dL_n/ds_n + T p_n (L_n - out)   (second term: no detach)
+        for (int64_t n = lane; n < N; n += kWave) {
+            const float x = row[n];
+            const float pn = expf(T * x - m) / z;
+            float gsn = pn * (-sigmoidf(x));
+            if (!detach) gsn += T * pn * (log_sigmoid(-x) - outv);
+            drow[n] = go * gsn;
+        }
+    } else {
+        const float inv = 1.f / (float)N;
+        for (int64_t n = lane; n < N; n += kWave) drow[n] = go * (-sigmoidf(row[n])) * inv;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void log_sigmoid_kernel(const float* __restrict__ x, int64_t n,
+                                                             float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) out[i] = log_sigmoid(x[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void log_sigmoid_bwd_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ d_out, int64_t n,
+                                                                 float* __restrict__ d_x) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) d_x[i] = d_out[i] * sigmoidf(-x[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host helpers
+// ---------------------------------------------------------------------------------------------
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int ok() {
+    g_last_error.clear();
+    return 0;
+}
+
+int check_launch(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(KGE_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    return ok();
+}
+
+bool aligned(const void* ptr, int bytes) { return ptr == nullptr || ((uintptr_t)ptr % (uintptr_t)bytes) == 0; }
+
+// widest vector width every operand allows, then the groups-per-lane bucket
+int pick_vg(const ScoreParams& p, int& V, int& G) {
+    const int cand[3] = {4, 2, 1};
+    V = 1;
+    for (int v : cand) {
+        if (p.D % v == 0 && p.q_ld % v == 0 && p.r_ld % v == 0 && p.r_off % v == 0 && p.c_ld % v == 0 &&
+            aligned(p.qent, 4 * v) && aligned(p.rel, 4 * v) && aligned(p.cent, 4 * v)) {
+            V = v;
+            break;
+        }
+    }
+    const int groups = (p.D / V + kWave - 1) / kWave;
+    G = 1;
+    while (G < groups) G <<= 1;
+    if (G > kMaxG)
+        return fail(KGE_ENOTSUP, "per-half dim " + std::to_string(p.D) + " exceeds the register-resident limit " +
+                                     std::to_string(kMaxG * kWave * V) + " for vector width " + std::to_string(V));
+    return 0;
+}
+
+// candidates per wave: long runs amortise the per-wave query build; keep >= 8192 waves in flight
+int pick_cpw(int64_t B, int64_t N) {
+    if (N <= 1) return 1;
+    int64_t cpw = 16;
+    while (cpw > 4 && B * ((N + cpw - 1) / cpw) < 8192) cpw >>= 1;
+    return (int)cpw;
+}
+
+int dispatch(int fn, const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G) {
+    switch (fn) {
+        case KGE_TRANSE: return launch_transe(p, kind, st, blocks, ch, V, G);
+        case KGE_DISTMULT: return launch_distmult(p, kind, st, blocks, ch, V, G);
+        case KGE_COMPLEX: return launch_complex(p, kind, st, blocks, ch, V, G);
+        case KGE_ROTATE: return launch_rotate(p, kind, st, blocks, ch, V, G);
+        case KGE_INTERHT: return launch_interht(p, kind, st, blocks, ch, V, G);
+        case KGE_PROTATE: return launch_protate(p, kind, st, blocks, ch, V, G);
+        default: return KGE_EINVAL;
+    }
+}
+
+int check_fn_mode(int fn, int mode) {
+    if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH && mode != KGE_SINGLE)
+        return fail(KGE_EINVAL, "mode must be 0 (head-batch), 1 (tail-batch) or 3 (single)");
+    if (fn < KGE_TRANSE || fn > KGE_PROTATE) return fail(KGE_EINVAL, "unknown score function id " + std::to_string(fn));
+    return 0;
+}
+
+int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (p.B < 0 || p.N < 0 || p.D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (p.B == 0 || p.N == 0) return ok();
+    if (!p.qent || !p.rel || !p.cent) return fail(KGE_EINVAL, "null table pointer");
+    int V = 1, G = 1;
+    rc = pick_vg(p, V, G);
+    if (rc) return rc;
+    int64_t waves;
+    if (kind == KIND_FINISH) {
+        p.cpw = 1;
+        p.wpr = 1;
+        waves = p.B;
+    } else {
+        p.cpw = pick_cpw(p.B, p.N);
+        p.wpr = (int)((p.N + p.cpw - 1) / p.cpw);
+        waves = p.B * p.wpr;
+    }
+    const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (blocks > INT32_MAX) return fail(KGE_EINVAL, "problem too large for one launch");
+    const bool ch = (kind != KIND_FINISH) && mode == KGE_HEAD_BATCH;
+    rc = dispatch(fn, p, kind, (hipStream_t)stream, (int)blocks, ch, V, G);
+    if (rc) return fail(rc, "no kernel for this (function, width) combination");
+    return check_launch(kind == KIND_BWD ? "kge score backward launch"
+                                         : (kind == KIND_FINISH ? "kge finish launch" : "kge score launch"));
+}
+
+float phase_div_for(int fn, float emb_range) {
+    // torch: tensor / (python float: emb_range.item() / pi) -> the divisor is rounded to fp32
+    const double pi = (fn == KGE_PROTATE) ? 3.14159262358979323846 : 3.14159265358979323846;
+    return (float)((double)emb_range / pi);
+}
+
+void fill_indexed(ScoreParams& p, int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld,
+                  const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos,
+                  const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range,
+                  float modulus) {
+    memset(&p, 0, sizeof(p));
+    const bool ch = mode == KGE_HEAD_BATCH;
+    p.qent = ent;
+    p.q_idx = pos ? pos + (ch ? 2 : 0) : nullptr;
+    p.q_ld = ent_ld;
+    p.q_stride = 3;
+    p.q_rows = nentity;
+    p.rel = rel;
+    p.r_idx = pos ? pos + 1 : nullptr;
+    p.r_ld = rel_ld;
+    p.r_stride = 3;
+    p.r_rows = nrelation;
+    p.r_off = rel_off;
+    p.cent = ent;
+    p.c_ld = ent_ld;
+    p.c_rows = nentity;
+    if (mode == KGE_SINGLE) {
+        p.c_idx = pos ? pos + 2 : nullptr;
+        p.c_stride = 3;
+        N = 1;
+    } else {
+        p.c_idx = neg;
+        p.c_stride = neg_ld;
+    }
+    p.B = B;
+    p.N = N;
+    p.D = (int)D;
+    p.gamma = gamma;
+    p.phase_div = phase_div_for(fn, emb_range);
+    p.modulus = modulus;
+}
+
+void fill_dense(ScoreParams& p, int fn, int mode, const float* head, int64_t head_ld, const float* rel,
+                int64_t rel_ld, int64_t rel_off, const float* tail, int64_t tail_ld, int64_t B, int64_t N, int64_t D,
+                float gamma, float emb_range, float modulus) {
+    memset(&p, 0, sizeof(p));
+    const bool ch = mode == KGE_HEAD_BATCH;
+    if (mode == KGE_SINGLE) N = 1;
+    p.qent = ch ? tail : head;
+    p.q_ld = ch ? tail_ld : head_ld;
+    p.q_rows = B;
+    p.rel = rel;
+    p.r_ld = rel_ld;
+    p.r_off = rel_off;
+    p.r_rows = B;
+    p.cent = ch ? head : tail;
+    p.c_ld = ch ? head_ld : tail_ld;
+    p.c_dense = N;
+    p.c_rows = B * N;
+    p.B = B;
+    p.N = N;
+    p.D = (int)D;
+    p.gamma = gamma;
+    p.phase_div = phase_div_for(fn, emb_range);
+    p.modulus = modulus;
+}
+
+bool empty(int64_t B, int64_t N) { return B == 0 || N == 0; }
+
+}  // namespace
+}  // namespace kge_impl
+
+using namespace kge_impl;
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+int kge_abi_version(void) { return KGE_ABI_VERSION; }
+
+const char* kge_last_error(void) { return g_last_error.c_str(); }
+
+int64_t kge_max_dim(int fn) {
+    if (fn < KGE_TRANSE || fn > KGE_PROTATE) return 0;
+    return (int64_t)kMaxG * kWave * 4;
+}
+
+int kge_score_indexed(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                      int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                      int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
+                      float* scores, int64_t scores_ld, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (B < 0 || N < 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (empty(B, mode == KGE_SINGLE ? 1 : N)) return ok();
+    if (!pos) return fail(KGE_EINVAL, "pos must not be NULL");
+    if (mode != KGE_SINGLE && !neg) return fail(KGE_EINVAL, "neg must not be NULL in head/tail-batch mode");
+    if (!scores) return fail(KGE_EINVAL, "scores must not be NULL");
+    ScoreParams p;
+    fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D, gamma,
+                 emb_range, modulus);
+    p.out = scores;
+    p.out_ld = scores_ld;
+    return run_score(fn, mode, p, KIND_FWD, stream);
+}
+
+int kge_step_finish(int fn, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel, int64_t nrelation,
+                    int64_t rel_ld, int64_t rel_off, const int64_t* pos, int64_t B, int64_t D, float gamma,
+                    float emb_range, float modulus, const float* neg_scores, int64_t N, int64_t ns_ld,
+                    float temperature, int adversarial, float* out_neg, float* pos_scores, float* out_pos,
+                    void* stream) {
+    int rc = check_fn_mode(fn, KGE_SINGLE);
+    if (rc) return rc;
+    if (B < 0 || N <= 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (B == 0) return ok();
+    if (!pos || !neg_scores || !out_neg || !out_pos) return fail(KGE_EINVAL, "null pointer");
+    ScoreParams f;
+    fill_indexed(f, fn, KGE_SINGLE, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, nullptr, 0, B, 1, D,
+                 gamma, emb_range, modulus);
+    f.neg_scores = neg_scores;
+    f.ns_ld = ns_ld;
+    f.n_neg = N;
+    f.temperature = temperature;
+    f.adversarial = adversarial;
+    f.out_neg = out_neg;
+    f.out_pos_raw = pos_scores;
+    f.out_pos_ls = out_pos;
+    return run_score(fn, KGE_SINGLE, f, KIND_FINISH, stream);
+}
+
+int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                     int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                     int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
+                     float temperature, int adversarial, float* neg_scores, int64_t ns_ld, float* out_neg,
+                     float* pos_scores, float* out_pos, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_forward needs a negative mode (0 or 1)");
+    if (B < 0 || N <= 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (B == 0) return ok();
+    if (!pos || !neg || !neg_scores || !out_neg || !out_pos) return fail(KGE_EINVAL, "null pointer");
+    rc = kge_score_indexed(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D,
+                           gamma, emb_range, modulus, neg_scores, ns_ld, stream);
+    if (rc) return rc;
+    return kge_step_finish(fn, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, B, D, gamma, emb_range,
+                           modulus, neg_scores, N, ns_ld, temperature, adversarial, out_neg, pos_scores, out_pos,
+                           stream);
+}
+
+int kge_score_dense(int fn, int mode, const float* head, int64_t head_ld, const float* rel, int64_t rel_ld,
+                    int64_t rel_off, const float* tail, int64_t tail_ld, int64_t B, int64_t N, int64_t D, float gamma,
+                    float emb_range, float modulus, float* scores, int64_t scores_ld, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (B < 0 || N < 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (empty(B, mode == KGE_SINGLE ? 1 : N)) return ok();
+    if (!scores) return fail(KGE_EINVAL, "scores must not be NULL");
+    ScoreParams p;
+    fill_dense(p, fn, mode, head, head_ld, rel, rel_ld, rel_off, tail, tail_ld, B, N, D, gamma, emb_range, modulus);
+    p.out = scores;
+    p.out_ld = scores_ld;
+    return run_score(fn, mode, p, KIND_FWD, stream);
+}
+
+int kge_score_dense_bwd(int fn, int mode, const float* head, int64_t head_ld, const float* rel, int64_t rel_ld,
+                        int64_t rel_off, const float* tail, int64_t tail_ld, int64_t B, int64_t N, int64_t D,
+                        float gamma, float emb_range, float modulus, const float* d_scores, int64_t d_ld,
+                        float* d_head, float* d_rel, float* d_tail, float* d_modulus, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (B < 0 || N < 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (empty(B, mode == KGE_SINGLE ? 1 : N)) return ok();
+    if (!d_scores || !d_head || !d_rel || !d_tail) return fail(KGE_EINVAL, "null gradient pointer");
+    ScoreParams p;
+    fill_dense(p, fn, mode, head, head_ld, rel, rel_ld, rel_off, tail, tail_ld, B, N, D, gamma, emb_range, modulus);
+    const bool ch = mode == KGE_HEAD_BATCH;
+    p.d_scores = d_scores;
+    p.d_ld = d_ld;
+    p.d_qent = ch ? d_tail : d_head;
+    p.d_cent = ch ? d_head : d_tail;
+    p.d_rel = d_rel;
+    p.d_modulus = d_modulus;
+    return run_score(fn, mode, p, KIND_BWD, stream);
+}
+
+int kge_neg_reduce(const float* scores, int64_t B, int64_t N, int64_t ld, float temperature, int adversarial,
+                   float* out, void* stream) {
+    if (B < 0 || N <= 0) return fail(KGE_EINVAL, "bad shape (B, N)");
+    if (B == 0) return ok();
+    if (!scores || !out) return fail(KGE_EINVAL, "null pointer");
+    const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(neg_reduce_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, scores, B, N,
+                       ld, temperature, adversarial, out);
+    return check_launch("kge_neg_reduce");
+}
+
+int kge_neg_reduce_bwd(const float* scores, int64_t B, int64_t N, int64_t ld, float temperature, int adversarial,
+                       int detach, const float* d_out, float* d_scores, int64_t d_ld, void* stream) {
+    if (B < 0 || N <= 0) return fail(KGE_EINVAL, "bad shape (B, N)");
+    if (B == 0) return ok();
+    if (!scores || !d_out || !d_scores) return fail(KGE_EINVAL, "null pointer");
+    const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(neg_reduce_bwd_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, scores,
+                       B, N, ld, temperature, adversarial, detach, d_out, d_scores, d_ld);
+    return check_launch("kge_neg_reduce_bwd");
+}
+
+int kge_log_sigmoid(const float* x, int64_t n, float* out, void* stream) {
+    if (n < 0) return fail(KGE_EINVAL, "bad size");
+    if (n == 0) return ok();
+    if (!x || !out) return fail(KGE_EINVAL, "null pointer");
+    hipLaunchKernelGGL(log_sigmoid_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, x, n, out);
+    return check_launch("kge_log_sigmoid");
+}
+
+int kge_log_sigmoid_bwd(const float* x, const float* d_out, int64_t n, float* d_x, void* stream) {
+    if (n < 0) return fail(KGE_EINVAL, "bad size");
+    if (n == 0) return ok();
+    if (!x || !d_out || !d_x) return fail(KGE_EINVAL, "null pointer");
+    hipLaunchKernelGGL(log_sigmoid_bwd_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, x, d_out, n, d_x);
+    return check_launch("kge_log_sigmoid_bwd");
+}
+
+int64_t kge_score_bwd_workspace_size(int fn, int mode, int64_t B, int64_t N, int64_t D) {
+    (void)fn;
+    (void)mode;
+    (void)B;
+    (void)N;
+    (void)D;
+    return 0;  // the atomic-scatter backward needs no scratch
+}
+
+int kge_score_indexed_bwd(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                          int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                          int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
+                          const float* d_scores, int64_t d_ld, float* d_ent, float* d_rel, float* d_modulus,
+                          void* workspace, void* stream) {
+    (void)workspace;
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (B < 0 || N < 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (empty(B, mode == KGE_SINGLE ? 1 : N)) return ok();
+    if (!pos) return fail(KGE_EINVAL, "pos must not be NULL");
+    if (mode != KGE_SINGLE && !neg) return fail(KGE_EINVAL, "neg must not be NULL in head/tail-batch mode");
+    if (!d_scores || !d_ent || !d_rel) return fail(KGE_EINVAL, "null gradient pointer");
+    ScoreParams p;
+    fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D, gamma,
+                 emb_range, modulus);
+    p.d_scores = d_scores;
+    p.d_ld = d_ld;
+    p.d_qent = d_ent;
+    p.d_cent = d_ent;
+    p.d_rel = d_rel;
+    p.d_modulus = d_modulus;
+    return run_score(fn, mode, p, KIND_BWD, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,662 @@
+// kge_device.h — device templates of the fused gather + score kernels (gfx950 / CDNA4).
+//
+// What they replace (reference, /root/reference):
+//   tensorflow_codes/model.py:127-199  single/head-batch/tail-batch gathers (tf.gather) + model_func
+//   tensorflow_codes/model.py:207-224  InterHT score
+//   tensorflow_codes/model.py:145,168-171,195-198  logsigmoid / self-adversarial reduction (Q3, Q4)
+//   KnowledgeGraphEmbedding/codes/model.py (absent; restated in oracle/kge_oracle.py):
+//     TransE / DistMult / ComplEx / RotatE / pRotatE score functions and KGEModel.forward gathers.
+//
+// Work decomposition: one wave64 owns one batch row b and a run of `cpw` consecutive candidates of
+// that row. The query side shared by every candidate of row b — (h, r) in tail-batch / single
+// mode, (r, t) in head-batch mode — is built ONCE per wave and kept in VGPRs. Candidate rows are
+// gathered from HBM straight into VGPRs with 16-B loads (lane l owns float4 groups l, l+64, ...
+// of each half-row) and software-pipelined: the next row is in flight while the current one is
+// reduced. Reductions along the hidden dim are DPP row butterflies + 4 readlanes (fixed order:
+// deterministic). Nothing [B, N, d]-shaped is materialised.
+#pragma once
+
+#include <math.h>
+
+#include "kge_internal.h"
+
+namespace kge_impl {
+
+template <int V>
+struct alignas(4 * V) vecf {
+    float a[V];
+};
+
+template <int V>
+__device__ __forceinline__ vecf<V> vzero() {
+    vecf<V> r;
+#pragma unroll
+    for (int i = 0; i < V; ++i) r.a[i] = 0.f;
+    return r;
+}
+
+template <int V>
+__device__ __forceinline__ vecf<V> vload(const float* p, bool ok) {
+    if (ok) return *reinterpret_cast<const vecf<V>*>(p);
+    return vzero<V>();
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 64 lanes, result in every lane: quad_perm xor1, xor2, row_half_mirror, row_mirror
+// (each 16-lane row then holds its sum in all lanes), then the 4 row sums via readlane.
+__device__ __forceinline__ float wave_sum(float v) {
+    v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp<0x141>(v);  // row_half_mirror
+    v += dpp<0x140>(v);  // row_mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, dpp<0xB1>(v));
+    v = fmaxf(v, dpp<0x4E>(v));
+    v = fmaxf(v, dpp<0x141>(v));
+    v = fmaxf(v, dpp<0x140>(v));
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int j) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ float readlanef(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+__device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
+
+// logsigmoid(x) = min(x,0) - log1p(exp(-|x|))   (tf.math.log_sigmoid, model.py:145,169)
+__device__ __forceinline__ float log_sigmoid(float x) { return fminf(x, 0.f) - log1pf(expf(-fabsf(x))); }
+__device__ __forceinline__ float sigmoidf(float x) {
+    if (x >= 0.f) return 1.f / (1.f + expf(-x));
+    const float e = expf(x);
+    return e / (1.f + e);
+}
+
+constexpr bool is_split(int fn) { return fn == KGE_COMPLEX || fn == KGE_ROTATE || fn == KGE_INTERHT; }
+constexpr bool rel_split(int fn) { return fn == KGE_COMPLEX; }
+
+// ---------------------------------------------------------------------------------------------
+// Query side. CH = candidate is the head (head-batch); otherwise the candidate is the tail
+// (tail-batch and single, which upstream scores with the same "else" branch).
+//   q0,q1,q2: per-element query operands kept in VGPRs; zero on groups past D.
+//   na_inv,nb_inv: InterHT query reciprocal norms (1/||a||, 1/||b||; no epsilon, Q7)
+// ---------------------------------------------------------------------------------------------
+template <int FN, bool CH, int V, int G>
+struct Query {
+    vecf<V> q0[G], q1[G], q2[G];
+    float na_inv, nb_inv;
+
+    __device__ __forceinline__ void build(const float* qrow, bool qok, const float* rrow, bool rok,
+                                          int D, int lane, const ScoreParams& p) {
+        const int DV = D / V;
+        vecf<V> ea[G], eb[G], ra[G], rb[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int g = lane + k * kWave;
+            const bool in = g < DV;
+            const int e = g * V;
+            ea[k] = vload<V>(qrow + e, qok && in);
+            eb[k] = is_split(FN) ? vload<V>(qrow + D + e, qok && in) : vzero<V>();
+            ra[k] = vload<V>(rrow + e, rok && in);
+            rb[k] = rel_split(FN) ? vload<V>(rrow + D + e, rok && in) : vzero<V>();
+        }
+        na_inv = nb_inv = 0.f;
+        if constexpr (FN == KGE_INTERHT) {
+            float sa = 0.f, sb = 0.f;
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    sa += ea[k].a[i] * ea[k].a[i];
+                    sb += eb[k].a[i] * eb[k].a[i];
+                }
+            na_inv = 1.f / sqrtf(wave_sum(sa));
+            nb_inv = 1.f / sqrtf(wave_sum(sb));
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const bool in = (lane + k * kWave) < DV;
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const float x = ea[k].a[i], y = eb[k].a[i];
+                const float r = ra[k].a[i], s = rb[k].a[i];
+                float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+                if constexpr (FN == KGE_TRANSE) {
+                    // tail: (h + r) - t ; head: h + (r - t)
+                    o0 = CH ? (r - x) : (x + r);
+                } else if constexpr (FN == KGE_DISTMULT) {
+                    // tail: (h * r) * t ; head: h * (r * t)
+                    o0 = CH ? (r * x) : (x * r);
+                } else if constexpr (FN == KGE_COMPLEX) {
+                    if (!CH) {  // re_h*re_r - im_h*im_r ; re_h*im_r + im_h*re_r
+                        o0 = x * r - y * s;
+                        o1 = x * s + y * r;
+                    } else {  // re_r*re_t + im_r*im_t ; re_r*im_t - im_r*re_t
+                        o0 = r * x + s * y;
+                        o1 = r * y - s * x;
+                    }
+                } else if constexpr (FN == KGE_ROTATE) {
+                    const float ph = r / p.phase_div;
+                    const float c = cosf(ph), sn = sinf(ph);
+                    if (!CH) {  // re_h*re_r - im_h*im_r ; re_h*im_r + im_h*re_r
+                        o0 = x * c - y * sn;
+                        o1 = x * sn + y * c;
+                    } else {  // re_r*re_t + im_r*im_t ; re_r*im_t - im_r*re_t
+                        o0 = c * x + sn * y;
+                        o1 = c * y - sn * x;
+                    }
+                    if (!in) o0 = o1 = 0.f;
+                } else if constexpr (FN == KGE_PROTATE) {
+                    const float pe = x / p.phase_div, pr = r / p.phase_div;
+                    o0 = CH ? (pr - pe) : (pe + pr);
+                } else if constexpr (FN == KGE_INTERHT) {
+                    // query entity halves normalised (Q7), b-half shifted by u = 1 (model.py:215-220)
+                    o0 = in ? x * na_inv : 0.f;
+                    o1 = in ? (y * nb_inv + 1.f) : 0.f;
+                    o2 = r;
+                }
+                q0[k].a[i] = o0;
+                q1[k].a[i] = o1;
+                q2[k].a[i] = o2;
+            }
+        }
+    }
+};
+
+// Candidate registers: first half (or whole row) in ca, second half in cb.
+template <int FN, int V, int G>
+struct Cand {
+    vecf<V> ca[G], cb[G];
+    __device__ __forceinline__ void load(const float* row, bool ok, int D, int lane) {
+        const int DV = D / V;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int g = lane + k * kWave;
+            const bool in = ok && g < DV;
+            ca[k] = vload<V>(row + g * V, in);
+            if constexpr (is_split(FN)) cb[k] = vload<V>(row + D + g * V, in);
+        }
+    }
+};
+
+// Forward score of one candidate held in registers (every lane returns the full score).
+template <int FN, bool CH, int V, int G>
+__device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Query<FN, CH, V, G>& q,
+                                            const ScoreParams& p) {
+    float acc = 0.f;
+    if constexpr (FN == KGE_INTERHT) {
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                sa += c.ca[k].a[i] * c.ca[k].a[i];
+                sb += c.cb[k].a[i] * c.cb[k].a[i];
+            }
+        const float ia = 1.f / sqrtf(wave_sum(sa)), ib = 1.f / sqrtf(wave_sum(sb));
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const float ah = c.ca[k].a[i] * ia;        // normalised candidate a-half
+                const float bh = c.cb[k].a[i] * ib + 1.f;  // normalised candidate b-half + u
+                float x;
+                if (CH)  // a_head * b_tail - a_tail * b_head + re_mid   (model.py:222)
+                    x = ah * q.q1[k].a[i] - q.q0[k].a[i] * bh + q.q2[k].a[i];
+                else
+                    x = q.q0[k].a[i] * bh - ah * q.q1[k].a[i] + q.q2[k].a[i];
+                acc += fabsf(x);
+            }
+        // groups past D: candidate zero-loaded and query zero -> x = 0
+    } else {
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const float x = c.ca[k].a[i];
+                if constexpr (FN == KGE_TRANSE) {
+                    acc += fabsf(CH ? (x + q.q0[k].a[i]) : (q.q0[k].a[i] - x));
+                } else if constexpr (FN == KGE_DISTMULT) {
+                    acc += CH ? (x * q.q0[k].a[i]) : (q.q0[k].a[i] * x);
+                } else if constexpr (FN == KGE_COMPLEX) {
+                    const float y = c.cb[k].a[i];
+                    acc += CH ? (x * q.q0[k].a[i] + y * q.q1[k].a[i]) : (q.q0[k].a[i] * x + q.q1[k].a[i] * y);
+                } else if constexpr (FN == KGE_ROTATE) {
+                    const float y = c.cb[k].a[i];
+                    const float xr = q.q0[k].a[i] - x, xi = q.q1[k].a[i] - y;
+                    acc += sqrtf(xr * xr + xi * xi);
+                } else if constexpr (FN == KGE_PROTATE) {
+                    const float pc = x / p.phase_div;
+                    acc += fabsf(sinf(CH ? (pc + q.q0[k].a[i]) : (q.q0[k].a[i] - pc)));
+                }
+            }
+    }
+    acc = wave_sum(acc);
+    if constexpr (FN == KGE_DISTMULT || FN == KGE_COMPLEX) return acc;
+    else if constexpr (FN == KGE_PROTATE) return p.gamma - acc * p.modulus;
+    else return p.gamma - acc;
+}
+
+struct WaveTask {
+    int64_t b, n0;
+    int nc;
+};
+
+__device__ __forceinline__ bool wave_task(const ScoreParams& p, WaveTask& t) {
+    const int64_t wid = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    t.b = wid / p.wpr;
+    if (t.b >= p.B) return false;
+    t.n0 = (wid - t.b * p.wpr) * (int64_t)p.cpw;
+    if (t.n0 >= p.N) return false;
+    t.nc = (int)min((int64_t)p.cpw, p.N - t.n0);
+    return true;
+}
+
+template <int FN, bool CH, int V, int G>
+__device__ __forceinline__ void build_query_for(const ScoreParams& p, int64_t b, int lane, Query<FN, CH, V, G>& q,
+                                                int64_t& qi, int64_t& ri, bool& qok, bool& rok) {
+    qi = p.q_idx ? p.q_idx[b * p.q_stride] : b;
+    ri = p.r_idx ? p.r_idx[b * p.r_stride] : b;
+    qok = qi >= 0 && qi < p.q_rows;
+    rok = ri >= 0 && ri < p.r_rows;
+    q.build(p.qent + (qok ? qi : 0) * p.q_ld, qok, p.rel + (rok ? ri : 0) * p.r_ld + p.r_off, rok, p.D, lane, p);
+}
+
+__device__ __forceinline__ const float* cand_row(const ScoreParams& p, int64_t id, bool& ok) {
+    ok = id >= 0 && id < p.c_rows;
+    return p.cent + (ok ? id : 0) * p.c_ld;
+}
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
+    WaveTask t;
+    if (!wave_task(p, t)) return;
+    const int lane = threadIdx.x & 63;
+    Query<FN, CH, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, CH, V, G>(p, t.b, lane, q, qi, ri, qok, rok);
+
+    int64_t my_id = 0;
+    if (lane < t.nc) my_id = p.c_idx ? p.c_idx[t.b * p.c_stride + t.n0 + lane] : t.b * p.c_dense + t.n0 + lane;
+
+    // software pipeline: row j+1 is in flight while row j is reduced
+    float my_score = 0.f;
+    Cand<FN, V, G> x0, x1;
+    bool ok;
+    const float* row = cand_row(p, readlane64(my_id, 0), ok);
+    x0.load(row, ok, p.D, lane);
+    int j = 0;
+    for (; j + 2 < t.nc; j += 2) {
+        row = cand_row(p, readlane64(my_id, j + 1), ok);
+        x1.load(row, ok, p.D, lane);
+        const float s0 = cand_score<FN, CH, V, G>(x0, q, p);
+        if (lane == j) my_score = s0;
+        row = cand_row(p, readlane64(my_id, j + 2), ok);
+        x0.load(row, ok, p.D, lane);
+        const float s1 = cand_score<FN, CH, V, G>(x1, q, p);
+        if (lane == j + 1) my_score = s1;
+    }
+    if (j + 1 < t.nc) {
+        row = cand_row(p, readlane64(my_id, j + 1), ok);
+        x1.load(row, ok, p.D, lane);
+        const float s0 = cand_score<FN, CH, V, G>(x0, q, p);
+        if (lane == j) my_score = s0;
+        const float s1 = cand_score<FN, CH, V, G>(x1, q, p);
+        if (lane == j + 1) my_score = s1;
+    } else {
+        const float s0 = cand_score<FN, CH, V, G>(x0, q, p);
+        if (lane == j) my_score = s0;
+    }
+    if (lane < t.nc) p.out[t.b * p.out_ld + t.n0 + lane] = my_score;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Finish kernel of the fused train-step forward (supervisor.py:17-18): one wave per batch row b
+//   * positive triple: single-mode score (tail formula) -> raw + logsigmoid   (model.py:127-146)
+//   * negative row b: sum softmax(T s) logsigmoid(-s) or mean logsigmoid(-s)  (model.py:168-171)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float row_reduce(const float* row, int64_t N, float T, int adversarial, int lane) {
+    if (adversarial) {
+        float m = -INFINITY;
+        for (int64_t n = lane; n < N; n += kWave) m = fmaxf(m, T * row[n]);
+        m = wave_max(m);
+        float z = 0.f, w = 0.f;
+        for (int64_t n = lane; n < N; n += kWave) {
+            const float x = row[n];
+            const float e = expf(T * x - m);
+            z += e;
+            w += e * log_sigmoid(-x);
+        }
+        return wave_sum(w) / wave_sum(z);
+    }
+    float w = 0.f;
+    for (int64_t n = lane; n < N; n += kWave) w += log_sigmoid(-row[n]);
+    return wave_sum(w) / (float)N;
+}
+
+template <int FN, int V, int G>
+__global__ __launch_bounds__(kBlock) void finish_kernel(ScoreParams p) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    Query<FN, false, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, false, V, G>(p, b, lane, q, qi, ri, qok, rok);
+    bool ok;
+    const float* row = cand_row(p, p.c_idx ? p.c_idx[b * p.c_stride] : b, ok);
+    Cand<FN, V, G> c;
+    c.load(row, ok, p.D, lane);
+    const float s = cand_score<FN, false, V, G>(c, q, p);
+    const float red = row_reduce(p.neg_scores + b * p.ns_ld, p.n_neg, p.temperature, p.adversarial, lane);
+    if (lane == 0) {
+        if (p.out_pos_raw) p.out_pos_raw[b] = s;
+        p.out_pos_ls[b] = log_sigmoid(s);
+        p.out_neg[b] = red;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward: recompute each candidate's per-element terms, scatter the candidate-row gradient with
+// fp32 atomics, accumulate the query-side gradient in VGPRs over the wave's candidates and add it
+// once per wave (atomics: query rows are shared across waves and batch rows).
+// ---------------------------------------------------------------------------------------------
+template <int V>
+__device__ __forceinline__ void vatomic_add(float* dst, const vecf<V>& v, bool ok) {
+    if (!ok) return;
+#pragma unroll
+    for (int i = 0; i < V; ++i) unsafeAtomicAdd(dst + i, v.a[i]);
+}
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void score_bwd_kernel(ScoreParams p) {
+    WaveTask t;
+    if (!wave_task(p, t)) return;
+    const int lane = threadIdx.x & 63;
+    const int D = p.D, DV = D / V;
+
+    Query<FN, CH, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, CH, V, G>(p, t.b, lane, q, qi, ri, qok, rok);
+    const float* qrow = p.qent + (qok ? qi : 0) * p.q_ld;
+    const float* rrow = p.rel + (rok ? ri : 0) * p.r_ld + p.r_off;
+
+    int64_t my_id = 0;
+    float my_g = 0.f;
+    if (lane < t.nc) {
+        my_id = p.c_idx ? p.c_idx[t.b * p.c_stride + t.n0 + lane] : t.b * p.c_dense + t.n0 + lane;
+        my_g = p.d_scores[t.b * p.d_ld + t.n0 + lane];
+    }
+
+    vecf<V> dq0[G], dq1[G], dq2[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) dq0[k] = dq1[k] = dq2[k] = vzero<V>();
+    float dmod = 0.f;
+
+    for (int j = 0; j < t.nc; ++j) {
+        const int64_t ci = readlane64(my_id, j);
+        const float g = readlanef(my_g, j);
+        bool ok;
+        const float* crow = cand_row(p, ci, ok);
+        Cand<FN, V, G> c;
+        c.load(crow, ok, D, lane);
+        vecf<V> dca[G], dcb[G];
+        if constexpr (FN == KGE_INTERHT) {
+            float sa = 0.f, sb = 0.f;
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    sa += c.ca[k].a[i] * c.ca[k].a[i];
+                    sb += c.cb[k].a[i] * c.cb[k].a[i];
+                }
+            const float ia = 1.f / sqrtf(wave_sum(sa)), ib = 1.f / sqrtf(wave_sum(sb));
+            float dota = 0.f, dotb = 0.f;
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    const float ah = c.ca[k].a[i] * ia;
+                    const float bn = c.cb[k].a[i] * ib;
+                    const float bh = bn + 1.f;
+                    const float q0 = q.q0[k].a[i], q1 = q.q1[k].a[i], q2 = q.q2[k].a[i];
+                    float x, dah, dbn;
+                    const bool in = (lane + k * kWave) < DV;
+                    if (CH) {
+                        x = ah * q1 - q0 * bh + q2;
+                        const float Gx = in ? -g * sgnf(x) : 0.f;
+                        dah = Gx * q1;
+                        dbn = -Gx * q0;
+                        dq1[k].a[i] += Gx * ah;
+                        dq0[k].a[i] += -Gx * bh;
+                        dq2[k].a[i] += Gx;
+                    } else {
+                        x = q0 * bh - ah * q1 + q2;
+                        const float Gx = in ? -g * sgnf(x) : 0.f;
+                        dah = -Gx * q1;
+                        dbn = Gx * q0;
+                        dq0[k].a[i] += Gx * bh;
+                        dq1[k].a[i] += -Gx * ah;
+                        dq2[k].a[i] += Gx;
+                    }
+                    dca[k].a[i] = dah;
+                    dcb[k].a[i] = dbn;
+                    dota += ah * dah;
+                    dotb += bn * dbn;
+                }
+            dota = wave_sum(dota);
+            dotb = wave_sum(dotb);
+            // d(x/n) = (dy - y <y, dy>) / n
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    const float ah = c.ca[k].a[i] * ia;
+                    const float bn = c.cb[k].a[i] * ib;
+                    dca[k].a[i] = (dca[k].a[i] - ah * dota) * ia;
+                    dcb[k].a[i] = (dcb[k].a[i] - bn * dotb) * ib;
+                }
+        } else {
+            float ysum = 0.f;
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    const float x = c.ca[k].a[i];
+                    const bool in = (lane + k * kWave) < DV;
+                    float da = 0.f, db = 0.f;
+                    if constexpr (FN == KGE_TRANSE) {
+                        const float r = CH ? (x + q.q0[k].a[i]) : (q.q0[k].a[i] - x);
+                        const float Gx = -g * sgnf(r);  // dL/d(residual)
+                        da = CH ? Gx : -Gx;
+                        dq0[k].a[i] += Gx;
+                    } else if constexpr (FN == KGE_DISTMULT) {
+                        da = g * q.q0[k].a[i];
+                        dq0[k].a[i] += g * x;
+                    } else if constexpr (FN == KGE_COMPLEX) {
+                        const float y = c.cb[k].a[i];
+                        da = g * q.q0[k].a[i];
+                        db = g * q.q1[k].a[i];
+                        dq0[k].a[i] += g * x;
+                        dq1[k].a[i] += g * y;
+                    } else if constexpr (FN == KGE_ROTATE) {
+                        const float y = c.cb[k].a[i];
+                        const float xr = q.q0[k].a[i] - x, xi = q.q1[k].a[i] - y;
+                        const float m = sqrtf(xr * xr + xi * xi);
+                        const float fr = (m > 0.f) ? xr / m : 0.f, fi = (m > 0.f) ? xi / m : 0.f;
+                        da = g * fr;
+                        db = g * fi;
+                        dq0[k].a[i] += -g * fr;
+                        dq1[k].a[i] += -g * fi;
+                    } else if constexpr (FN == KGE_PROTATE) {
+                        const float pc = x / p.phase_div;
+                        const float z = CH ? (pc + q.q0[k].a[i]) : (q.q0[k].a[i] - pc);
+                        const float sz = sinf(z);
+                        const float Gx = in ? -g * p.modulus * sgnf(sz) * cosf(z) : 0.f;
+                        da = (CH ? Gx : -Gx) / p.phase_div;
+                        dq0[k].a[i] += Gx;
+                        ysum += in ? fabsf(sz) : 0.f;
+                    }
+                    dca[k].a[i] = in ? da : 0.f;
+                    dcb[k].a[i] = in ? db : 0.f;
+                }
+            if constexpr (FN == KGE_PROTATE) dmod += -g * wave_sum(ysum);
+        }
+        float* drow = p.d_cent + (ok ? ci : 0) * p.c_ld;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int gi = lane + k * kWave;
+            const bool in = ok && gi < DV;
+            vatomic_add<V>(drow + gi * V, dca[k], in);
+            if constexpr (is_split(FN)) vatomic_add<V>(drow + D + gi * V, dcb[k], in);
+        }
+    }
+
+    // query-side chain rule -> raw query entity row and relation row
+    float dna = 0.f, dnb = 0.f;
+    if constexpr (FN == KGE_INTERHT) {
+        float da = 0.f, db = 0.f;
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const bool in = (lane + k * kWave) < DV;
+                da += q.q0[k].a[i] * dq0[k].a[i];
+                db += (in ? q.q1[k].a[i] - 1.f : 0.f) * dq1[k].a[i];
+            }
+        dna = wave_sum(da);
+        dnb = wave_sum(db);
+    }
+    float* dq_row = p.d_qent + (qok ? qi : 0) * p.q_ld;
+    float* dr_row = p.d_rel + (rok ? ri : 0) * p.r_ld + p.r_off;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const int gi = lane + k * kWave;
+        const bool in = gi < DV;
+        const int e = gi * V;
+        const vecf<V> ea = vload<V>(qrow + e, qok && in);
+        const vecf<V> eb = is_split(FN) ? vload<V>(qrow + D + e, qok && in) : vzero<V>();
+        const vecf<V> ra = vload<V>(rrow + e, rok && in);
+        const vecf<V> rb = rel_split(FN) ? vload<V>(rrow + D + e, rok && in) : vzero<V>();
+        vecf<V> gea = vzero<V>(), geb = vzero<V>(), gra = vzero<V>(), grb = vzero<V>();
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const float x = ea.a[i], y = eb.a[i], r = ra.a[i], s = rb.a[i];
+            const float d0 = dq0[k].a[i], d1 = dq1[k].a[i], d2 = dq2[k].a[i];
+            if constexpr (FN == KGE_TRANSE) {
+                gea.a[i] = CH ? -d0 : d0;
+                gra.a[i] = d0;
+            } else if constexpr (FN == KGE_DISTMULT) {
+                gea.a[i] = d0 * r;
+                gra.a[i] = d0 * x;
+            } else if constexpr (FN == KGE_COMPLEX) {
+                if (!CH) {
+                    gea.a[i] = d0 * r + d1 * s;
+                    geb.a[i] = -d0 * s + d1 * r;
+                    gra.a[i] = d0 * x + d1 * y;
+                    grb.a[i] = -d0 * y + d1 * x;
+                } else {
+                    gea.a[i] = d0 * r - d1 * s;
+                    geb.a[i] = d0 * s + d1 * r;
+                    gra.a[i] = d0 * x + d1 * y;
+                    grb.a[i] = d0 * y - d1 * x;
+                }
+            } else if constexpr (FN == KGE_ROTATE) {
+                const float ph = r / p.phase_div;
+                const float c = cosf(ph), sn = sinf(ph);
+                const float Q0 = q.q0[k].a[i], Q1 = q.q1[k].a[i];
+                float dth;
+                if (!CH) {
+                    gea.a[i] = d0 * c + d1 * sn;
+                    geb.a[i] = -d0 * sn + d1 * c;
+                    dth = -d0 * Q1 + d1 * Q0;
+                } else {
+                    gea.a[i] = d0 * c - d1 * sn;
+                    geb.a[i] = d0 * sn + d1 * c;
+                    dth = d0 * Q1 - d1 * Q0;
+                }
+                gra.a[i] = dth / p.phase_div;
+            } else if constexpr (FN == KGE_PROTATE) {
+                gea.a[i] = (CH ? -d0 : d0) / p.phase_div;
+                gra.a[i] = d0 / p.phase_div;
+            } else if constexpr (FN == KGE_INTERHT) {
+                const float Q0 = q.q0[k].a[i];
+                const float bn = in ? q.q1[k].a[i] - 1.f : 0.f;
+                gea.a[i] = (d0 - Q0 * dna) * q.na_inv;
+                geb.a[i] = (d1 - bn * dnb) * q.nb_inv;
+                gra.a[i] = d2;
+            }
+            if (!in) gea.a[i] = geb.a[i] = gra.a[i] = grb.a[i] = 0.f;
+        }
+        vatomic_add<V>(dq_row + e, gea, qok && in);
+        if constexpr (is_split(FN)) vatomic_add<V>(dq_row + D + e, geb, qok && in);
+        vatomic_add<V>(dr_row + e, gra, rok && in);
+        if constexpr (rel_split(FN)) vatomic_add<V>(dr_row + D + e, grb, rok && in);
+    }
+    if constexpr (FN == KGE_PROTATE) {
+        if (lane == 0 && p.d_modulus) unsafeAtomicAdd(p.d_modulus, dmod);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dispatch over (kind, candidate side, vector width, groups per lane) for one score function
+// ---------------------------------------------------------------------------------------------
+template <int FN, bool CH, int V, int G>
+void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
+    if (kind == KIND_BWD)
+        hipLaunchKernelGGL((score_bwd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_FINISH) {
+        if constexpr (!CH) hipLaunchKernelGGL((finish_kernel<FN, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    } else
+        hipLaunchKernelGGL((score_fwd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+}
+
+template <int FN, bool CH, int V>
+int launch_g(const ScoreParams& p, int kind, hipStream_t st, int blocks, int G) {
+    switch (G) {
+        case 1: launch_one<FN, CH, V, 1>(p, kind, st, blocks); return 0;
+        case 2: launch_one<FN, CH, V, 2>(p, kind, st, blocks); return 0;
+        case 4: launch_one<FN, CH, V, 4>(p, kind, st, blocks); return 0;
+        case 8: launch_one<FN, CH, V, 8>(p, kind, st, blocks); return 0;
+        default: return KGE_ENOTSUP;
+    }
+}
+
+template <int FN, bool CH>
+int launch_v(const ScoreParams& p, int kind, hipStream_t st, int blocks, int V, int G) {
+    switch (V) {
+        case 4: return launch_g<FN, CH, 4>(p, kind, st, blocks, G);
+        case 2: return launch_g<FN, CH, 2>(p, kind, st, blocks, G);
+        case 1: return launch_g<FN, CH, 1>(p, kind, st, blocks, G);
+        default: return KGE_ENOTSUP;
+    }
+}
+
+template <int FN>
+int launch_fn_tmpl(const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G) {
+    return ch ? launch_v<FN, true>(p, kind, st, blocks, V, G) : launch_v<FN, false>(p, kind, st, blocks, V, G);
+}
+
+}  // namespace kge_impl

@@ -1,0 +1,66 @@
+// kge_internal.h — host/device shared definitions of libkge_hip.so (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kge_hip.h"
+
+namespace kge_impl {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kMaxG = 8;  // float4 groups per lane per half-row kept in VGPRs (D <= 2048)
+
+enum Kind { KIND_FWD = 0, KIND_BWD = 1, KIND_FINISH = 2 };
+
+// Parameters of one scoring launch. Rows are addressed as base + row * ld (floats).
+//   query entity row of batch row b:  q_idx ? q_idx[b * q_stride] : b
+//   relation row of batch row b:      r_idx ? r_idx[b * r_stride] : b      (+ r_off floats)
+//   candidate n of batch row b:       c_idx ? c_idx[b * c_stride + n] : b * c_dense + n
+struct ScoreParams {
+    const float* qent;
+    const int64_t* q_idx;
+    int64_t q_ld, q_stride, q_rows;
+    const float* rel;
+    const int64_t* r_idx;
+    int64_t r_ld, r_stride, r_rows, r_off;
+    const float* cent;
+    const int64_t* c_idx;
+    int64_t c_ld, c_stride, c_rows, c_dense;
+    float* out;
+    int64_t out_ld;
+    int64_t B, N;
+    int D;    // per-half width
+    int cpw;  // candidates per wave
+    int wpr;  // waves per batch row = ceil(N / cpw)
+    float gamma;
+    float phase_div;  // emb_range / pi (RotatE) or emb_range / pi' (pRotatE), fp32 as torch does
+    float modulus;    // pRotatE
+    // backward only
+    const float* d_scores;
+    int64_t d_ld;
+    float* d_qent;  // gradient table for query entity rows (== d_cent for indexed scoring)
+    float* d_rel;
+    float* d_cent;
+    float* d_modulus;
+    // finish kernel only (one wave per batch row: positive score + negative-row reduction)
+    const float* neg_scores;
+    int64_t ns_ld, n_neg;
+    float temperature;
+    int adversarial;
+    float* out_neg;      // [B] reduced negative branch
+    float* out_pos_raw;  // [B] raw positive score (may be null)
+    float* out_pos_ls;   // [B] logsigmoid(positive score)
+};
+
+// per-score-function launchers (one translation unit each, see kge_fn_*.hip)
+int launch_transe(const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G);
+int launch_distmult(const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G);
+int launch_complex(const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G);
+int launch_rotate(const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G);
+int launch_interht(const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G);
+int launch_protate(const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G);
+
+}  // namespace kge_impl

@@ -144,6 +144,19 @@ class TFKGEModel(_KGEBase):
 
     call = forward
 
+    def step_forward(self, positive_sample, negative_sample, mode):
+        """Both calls of supervisor.py:17-18 fused into two launches:
+        returns (self(((pos, neg), mode)), self(((pos, neg), 3))), each [B, 1], differentiable."""
+        m = ops.mode_id(mode)
+        if m == SINGLE:
+            raise ValueError("step_forward needs the batch's negative mode")
+        modulus = self.modulus if self.model_name == "pRotatE" else None
+        neg, pos = ops.step_forward(FN_IDS[self.model_name], m, self.entity_embedding,
+                                    self.relation_embedding, positive_sample, negative_sample,
+                                    self._D, self._gamma_f, self._range_f, rel_off=self._rel_off,
+                                    modulus=modulus, temperature=1.0, adversarial=True, detach=False)
+        return neg.unsqueeze(1), pos.unsqueeze(1)
+
 
 class KGEModel(_KGEBase):
     """Drop-in for the upstream PyTorch ``KGEModel`` (KnowledgeGraphEmbedding/codes/model.py)."""

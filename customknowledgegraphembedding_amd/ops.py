@@ -117,6 +117,55 @@ def score_indexed_bwd_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_r
     check(rc, "kge_score_indexed_bwd")
 
 
+def step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus=0.0,
+                     temperature=1.0, adversarial=True, neg_scores=None):
+    """Both model calls of supervisor.py:17-18 in two launches -> (out_neg [B], out_pos [B],
+    neg_scores [B, N], pos_scores [B])."""
+    _need_gpu(ent, rel, pos, neg)
+    _fp32(ent, "entity_embedding")
+    _fp32(rel, "relation_embedding")
+    _i64(pos, "positive_sample")
+    _i64(neg, "negative_sample")
+    if mode not in (HEAD_BATCH, TAIL_BATCH):
+        raise ValueError("step_forward needs a negative mode (0 head-batch or 1 tail-batch)")
+    if pos.dim() != 2 or pos.shape[1] != 3 or not pos.is_contiguous():
+        raise ValueError("positive_sample must be a contiguous [B, 3] int64 tensor")
+    B, N = neg.shape
+    if neg.stride(1) != 1 or B != pos.shape[0]:
+        raise ValueError("negative_sample must be a row-contiguous [B, N] int64 tensor")
+    dev = ent.device
+    if neg_scores is None:
+        neg_scores = torch.empty((B, N), dtype=torch.float32, device=dev)
+    out_neg = torch.empty((B,), dtype=torch.float32, device=dev)
+    out_pos = torch.empty((B,), dtype=torch.float32, device=dev)
+    pos_scores = torch.empty((B,), dtype=torch.float32, device=dev)
+    rc = _lib.load().kge_step_forward(
+        fn, mode, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0],
+        rel.stride(0), rel_off, pos.data_ptr(), neg.data_ptr(), neg.stride(0), B, N, D,
+        float(gamma), float(emb_range), float(modulus), float(temperature), int(bool(adversarial)),
+        neg_scores.data_ptr(), neg_scores.stride(0), out_neg.data_ptr(), pos_scores.data_ptr(),
+        out_pos.data_ptr(), _stream(dev))
+    check(rc, "kge_step_forward")
+    return out_neg, out_pos, neg_scores, pos_scores
+
+
+def step_finish_raw(fn, ent, rel, rel_off, pos, D, gamma, emb_range, neg_scores, modulus=0.0,
+                    temperature=1.0, adversarial=True):
+    """Second launch of step_forward_raw: positives + per-row reductions of `neg_scores`."""
+    B, N = neg_scores.shape
+    dev = ent.device
+    out_neg = torch.empty((B,), dtype=torch.float32, device=dev)
+    out_pos = torch.empty((B,), dtype=torch.float32, device=dev)
+    pos_scores = torch.empty((B,), dtype=torch.float32, device=dev)
+    rc = _lib.load().kge_step_finish(
+        fn, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0),
+        rel_off, pos.data_ptr(), B, D, float(gamma), float(emb_range), float(modulus),
+        neg_scores.data_ptr(), N, neg_scores.stride(0), float(temperature), int(bool(adversarial)),
+        out_neg.data_ptr(), pos_scores.data_ptr(), out_pos.data_ptr(), _stream(dev))
+    check(rc, "kge_step_finish")
+    return out_neg, out_pos, pos_scores
+
+
 def _dense_shapes(mode, head, relation, tail):
     B = head.shape[0]
     if mode == HEAD_BATCH:
@@ -273,6 +322,58 @@ class _LogSigmoid(torch.autograd.Function):
                                              d_x.data_ptr(), _stream(x.device))
         check(rc, "kge_log_sigmoid_bwd")
         return d_x
+
+
+class _StepForward(torch.autograd.Function):
+    """Differentiable fused forward of supervisor.py:17-18 (GradientTape through both calls)."""
+
+    @staticmethod
+    def forward(ctx, ent, rel, modulus_t, pos, neg, fn, mode, rel_off, D, gamma, emb_range,
+                temperature, adversarial, detach):
+        modulus = float(modulus_t.item()) if (fn == FN_IDS["pRotatE"]) else 0.0
+        out_neg, out_pos, ns, ps = step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma,
+                                                    emb_range, modulus, temperature, adversarial)
+        ctx.save_for_backward(ent, rel, pos, neg, ns, ps)
+        ctx.cfg = (fn, mode, rel_off, D, gamma, emb_range, modulus, temperature, adversarial, detach,
+                   None if modulus_t is None else modulus_t.shape)
+        return out_neg, out_pos
+
+    @staticmethod
+    def backward(ctx, d_neg, d_pos):
+        ent, rel, pos, neg, ns, ps = ctx.saved_tensors
+        (fn, mode, rel_off, D, gamma, emb_range, modulus, temperature, adversarial, detach,
+         mod_shape) = ctx.cfg
+        lib = _lib.load()
+        st = _stream(ent.device)
+        B, N = ns.shape
+        d_ent = torch.zeros_like(ent)
+        d_rel = torch.zeros_like(rel)
+        d_mod = torch.zeros(1, dtype=torch.float32, device=ent.device) if mod_shape is not None else None
+        if d_neg is not None:
+            d_neg = d_neg.contiguous()
+            d_ns = torch.empty_like(ns)
+            check(lib.kge_neg_reduce_bwd(ns.data_ptr(), B, N, ns.stride(0), float(temperature),
+                                         int(bool(adversarial)), int(bool(detach)), d_neg.data_ptr(),
+                                         d_ns.data_ptr(), d_ns.stride(0), st), "kge_neg_reduce_bwd")
+            score_indexed_bwd_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus,
+                                  d_ns, d_ent, d_rel, d_mod)
+        if d_pos is not None:
+            d_pos = d_pos.contiguous()
+            d_ps = torch.empty_like(ps)
+            check(lib.kge_log_sigmoid_bwd(ps.data_ptr(), d_pos.data_ptr(), B, d_ps.data_ptr(), st),
+                  "kge_log_sigmoid_bwd")
+            score_indexed_bwd_raw(fn, SINGLE, ent, rel, rel_off, pos, None, D, gamma, emb_range,
+                                  modulus, d_ps.view(B, 1), d_ent, d_rel, d_mod)
+        if d_mod is not None:
+            d_mod = d_mod.view(mod_shape)
+        return (d_ent, d_rel, d_mod) + (None,) * 11
+
+
+def step_forward(fn, mode, ent, rel, pos, neg, D, gamma, emb_range, rel_off=0, modulus=None,
+                 temperature=1.0, adversarial=True, detach=False):
+    """Fused, differentiable forward of both model calls of one train step -> (neg [B], pos [B])."""
+    return _StepForward.apply(ent, rel, modulus, pos, neg, fn, mode, rel_off, D, gamma, emb_range,
+                              float(temperature), bool(adversarial), bool(detach))
 
 
 def score_indexed(fn, mode, ent, rel, pos, neg, D, gamma, emb_range, rel_off=0, modulus=None):

@@ -83,6 +83,39 @@ int kge_score_indexed(int fn, int mode,
                       float* scores, int64_t scores_ld, void* stream);
 
 /*
+ * Fused forward of one TF train step (supervisor.py:17-18): the negative call
+ * model(((pos, neg), mode)) and the positive call model(((pos, neg), 3)) in two launches.
+ *   mode       KGE_HEAD_BATCH or KGE_TAIL_BATCH (the batch's negative mode)
+ *   neg_scores [B,N] raw negative scores (out, row stride ns_ld) — kept for the backward
+ *   out_neg    [B]   reduced negative branch: adversarial != 0 -> sum softmax(T s) logsigmoid(-s)
+ *                    (model.py:168-171,195-198), else mean logsigmoid(-s)
+ *   pos_scores [B]   raw positive scores, single-mode formula (out, may be NULL)
+ *   out_pos    [B]   logsigmoid(positive score) (model.py:145)
+ */
+int kge_step_forward(int fn, int mode,
+                     const float* ent, int64_t nentity, int64_t ent_ld,
+                     const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off,
+                     const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                     int64_t B, int64_t N, int64_t D,
+                     float gamma, float emb_range, float modulus,
+                     float temperature, int adversarial,
+                     float* neg_scores, int64_t ns_ld, float* out_neg,
+                     float* pos_scores, float* out_pos, void* stream);
+
+/*
+ * Second half of kge_step_forward, on scores kge_score_indexed already wrote: one wave per batch
+ * row scores the positive triple (single mode) and reduces the row's N negative scores.
+ */
+int kge_step_finish(int fn,
+                    const float* ent, int64_t nentity, int64_t ent_ld,
+                    const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off,
+                    const int64_t* pos, int64_t B, int64_t D,
+                    float gamma, float emb_range, float modulus,
+                    const float* neg_scores, int64_t N, int64_t ns_ld,
+                    float temperature, int adversarial,
+                    float* out_neg, float* pos_scores, float* out_pos, void* stream);
+
+/*
  * Score pre-gathered rows: the model_func plugin surface itself,
  * `model_func[name](head, relation, tail, mode) -> [B, 1|N]` (model.py:109-112,207).
  *   head [B, Nh, *] rows (row stride head_ld), Nh = N for KGE_HEAD_BATCH else 1

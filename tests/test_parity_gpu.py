@@ -280,3 +280,57 @@ def test_c2_full_size_properties():
     single = ops.score_indexed_raw(fn, 3, entd, reld, d, posd, None, d, gamma, rng)
     tail_true = ops.score_indexed_raw(fn, 1, entd, reld, d, posd, posd[:, 2:3].contiguous(), d, gamma, rng)
     assert torch.equal(single, tail_true)
+
+
+@pytest.mark.parametrize("path", _golden("c1_") + _golden("c2_"), ids=os.path.basename)
+def test_fused_step_forward_matches_both_calls(path):
+    """kge_step_forward == (call(((pos,neg),mode)), call(((pos,neg),3))) (supervisor.py:17-18)."""
+    z = np.load(path)
+    name = _name_of(path)
+    d = int(z["hidden_dim"])
+    ent = torch.from_numpy(z["ent"])
+    rel = torch.from_numpy(z["rel"])
+    m = kge.TFKGEModel(name, ent.shape[0], rel.shape[0], d, float(z["gamma"]),
+                       double_entity_embedding=(name == "InterHT"), triple_relation_embedding=(name == "InterHT"),
+                       device=DEV)
+    with torch.no_grad():
+        m.entity_embedding.copy_(ent)
+        m.relation_embedding.copy_(rel)
+    pos, neg = torch.from_numpy(z["pos"]).to(DEV), torch.from_numpy(z["neg"]).to(DEV)
+    for mode in (0, 1):
+        n, p = m.step_forward(pos, neg, mode)
+        assert rel_close(n.detach().cpu().numpy(), z[f"tf_call_mode{mode}"]) <= TOL
+        assert rel_close(p.detach().cpu().numpy(), z["tf_call_mode3"]) <= TOL
+        # and bitwise identical to the unfused calls
+        assert torch.equal(n, m(((pos, neg), mode)))
+        assert torch.equal(p, m(((pos, neg), 3)))
+
+
+@pytest.mark.parametrize("path", _golden("train_"), ids=os.path.basename)
+def test_fused_step_train_grads(path):
+    """Loss + tape.gradient of supervisor.py:17-25 through the fused step_forward."""
+    z = np.load(path)
+    name = _name_of(path)
+    d = int(z["hidden_dim"])
+    ent = torch.from_numpy(z["ent"])
+    rel = torch.from_numpy(z["rel"])
+    m = kge.TFKGEModel(name, ent.shape[0], rel.shape[0], d, float(z["gamma"]),
+                       double_entity_embedding=MULT[name][0] == 2, double_relation_embedding=(name == "ComplEx"),
+                       triple_relation_embedding=(name == "InterHT"), device=DEV)
+    if name == "pRotatE":
+        m.modulus.requires_grad_(False)
+        with torch.no_grad():
+            m.modulus.fill_(0.5 * float(z["embedding_range"]))
+    pos, neg = torch.from_numpy(z["pos"]).to(DEV), torch.from_numpy(z["neg"]).to(DEV)
+    w = torch.from_numpy(z["weight"]).float().to(DEV)
+    for mode in (0, 1):
+        with torch.no_grad():
+            m.entity_embedding.copy_(ent)
+            m.relation_embedding.copy_(rel)
+        m.zero_grad(set_to_none=True)
+        negative_score, positive_score = m.step_forward(pos, neg, mode)
+        loss = (-torch.sum(w * positive_score) / torch.sum(w) - torch.sum(w * negative_score) / torch.sum(w)) / 2
+        loss.backward()
+        assert rel_close(loss.item(), z[f"loss_mode{mode}"]) <= TOL
+        assert _grad_close(m.entity_embedding.grad.cpu(), z[f"d_ent_mode{mode}"]), name
+        assert _grad_close(m.relation_embedding.grad.cpu(), z[f"d_rel_mode{mode}"]), name

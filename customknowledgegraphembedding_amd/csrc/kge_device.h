@@ -41,6 +41,46 @@ __device__ __forceinline__ vecf<V> vload(const float* p, bool ok) {
     return vzero<V>();
 }
 
+// Raw buffer descriptor over `bytes` bytes at `base`, built from wave-uniform values only (the
+// readfirstlanes make that provable to the compiler, so no waterfall loop is emitted). Loads at or
+// past `bytes` return 0 (hardware range check): rows past D, or a whole invalid row (bytes = 0),
+// need no masks or branches.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
+}
+
+template <int V>
+__device__ __forceinline__ vecf<V> bload(rsrc_t r, uint32_t off) {
+    vecf<V> o;
+    if constexpr (V == 4) {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        o.a[0] = __uint_as_float(u[0]);
+        o.a[1] = __uint_as_float(u[1]);
+        o.a[2] = __uint_as_float(u[2]);
+        o.a[3] = __uint_as_float(u[3]);
+    } else if constexpr (V == 2) {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        o.a[0] = __uint_as_float(u[0]);
+        o.a[1] = __uint_as_float(u[1]);
+    } else {
+        o.a[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    }
+    return o;
+}
+
+// byte offset of lane `lane`'s group k in a half-row
+template <int V>
+__device__ __forceinline__ uint32_t goff(int lane, int k) {
+    return (uint32_t)((lane + k * kWave) * V * 4);
+}
+
+__device__ __forceinline__ float rsqrt_f(float x) { return __builtin_amdgcn_rsqf(x); }
+
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -109,16 +149,29 @@ struct Query {
     __device__ __forceinline__ void build(const float* qrow, bool qok, const float* rrow, bool rok,
                                           int D, int lane, const ScoreParams& p) {
         const int DV = D / V;
+        const uint32_t qb = qok ? (uint32_t)D * 4u : 0u, rbytes = rok ? (uint32_t)D * 4u : 0u;
+        const rsrc_t sqa = make_rsrc(qrow, qb), sra = make_rsrc(rrow, rbytes);
         vecf<V> ea[G], eb[G], ra[G], rb[G];
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            const int g = lane + k * kWave;
-            const bool in = g < DV;
-            const int e = g * V;
-            ea[k] = vload<V>(qrow + e, qok && in);
-            eb[k] = is_split(FN) ? vload<V>(qrow + D + e, qok && in) : vzero<V>();
-            ra[k] = vload<V>(rrow + e, rok && in);
-            rb[k] = rel_split(FN) ? vload<V>(rrow + D + e, rok && in) : vzero<V>();
+            ea[k] = bload<V>(sqa, goff<V>(lane, k));
+            ra[k] = bload<V>(sra, goff<V>(lane, k));
+        }
+        if constexpr (is_split(FN)) {
+            const rsrc_t sqb = make_rsrc(qrow + D, qb);
+#pragma unroll
+            for (int k = 0; k < G; ++k) eb[k] = bload<V>(sqb, goff<V>(lane, k));
+        } else {
+#pragma unroll
+            for (int k = 0; k < G; ++k) eb[k] = vzero<V>();
+        }
+        if constexpr (rel_split(FN)) {
+            const rsrc_t srb = make_rsrc(rrow + D, rbytes);
+#pragma unroll
+            for (int k = 0; k < G; ++k) rb[k] = bload<V>(srb, goff<V>(lane, k));
+        } else {
+#pragma unroll
+            for (int k = 0; k < G; ++k) rb[k] = vzero<V>();
         }
         na_inv = nb_inv = 0.f;
         if constexpr (FN == KGE_INTERHT) {
@@ -130,8 +183,8 @@ struct Query {
                     sa += ea[k].a[i] * ea[k].a[i];
                     sb += eb[k].a[i] * eb[k].a[i];
                 }
-            na_inv = 1.f / sqrtf(wave_sum(sa));
-            nb_inv = 1.f / sqrtf(wave_sum(sb));
+            na_inv = rsqrt_f(wave_sum(sa));
+            nb_inv = rsqrt_f(wave_sum(sb));
         }
 #pragma unroll
         for (int k = 0; k < G; ++k) {
@@ -188,13 +241,14 @@ template <int FN, int V, int G>
 struct Cand {
     vecf<V> ca[G], cb[G];
     __device__ __forceinline__ void load(const float* row, bool ok, int D, int lane) {
-        const int DV = D / V;
+        const uint32_t nb = ok ? (uint32_t)D * 4u : 0u;
+        const rsrc_t sa = make_rsrc(row, nb);
 #pragma unroll
-        for (int k = 0; k < G; ++k) {
-            const int g = lane + k * kWave;
-            const bool in = ok && g < DV;
-            ca[k] = vload<V>(row + g * V, in);
-            if constexpr (is_split(FN)) cb[k] = vload<V>(row + D + g * V, in);
+        for (int k = 0; k < G; ++k) ca[k] = bload<V>(sa, goff<V>(lane, k));
+        if constexpr (is_split(FN)) {
+            const rsrc_t sb = make_rsrc(row + D, nb);
+#pragma unroll
+            for (int k = 0; k < G; ++k) cb[k] = bload<V>(sb, goff<V>(lane, k));
         }
     }
 };
@@ -213,7 +267,7 @@ __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Query
                 sa += c.ca[k].a[i] * c.ca[k].a[i];
                 sb += c.cb[k].a[i] * c.cb[k].a[i];
             }
-        const float ia = 1.f / sqrtf(wave_sum(sa)), ib = 1.f / sqrtf(wave_sum(sb));
+        const float ia = rsqrt_f(wave_sum(sa)), ib = rsqrt_f(wave_sum(sb));
 #pragma unroll
         for (int k = 0; k < G; ++k)
 #pragma unroll
@@ -360,16 +414,18 @@ __global__ __launch_bounds__(kBlock) void finish_kernel(ScoreParams p) {
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (b >= p.B) return;
     const int lane = threadIdx.x & 63;
-    Query<FN, false, V, G> q;
-    int64_t qi, ri;
-    bool qok, rok;
-    build_query_for<FN, false, V, G>(p, b, lane, q, qi, ri, qok, rok);
+    // issue every independent load before the first reduction: the positive tail row, then the
+    // query rows (h, r), then the negative row's scores (latency-bound: one wave per batch row)
     bool ok;
     const float* row = cand_row(p, p.c_idx ? p.c_idx[b * p.c_stride] : b, ok);
     Cand<FN, V, G> c;
     c.load(row, ok, p.D, lane);
-    const float s = cand_score<FN, false, V, G>(c, q, p);
+    Query<FN, false, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, false, V, G>(p, b, lane, q, qi, ri, qok, rok);
     const float red = row_reduce(p.neg_scores + b * p.ns_ld, p.n_neg, p.temperature, p.adversarial, lane);
+    const float s = cand_score<FN, false, V, G>(c, q, p);
     if (lane == 0) {
         if (p.out_pos_raw) p.out_pos_raw[b] = s;
         p.out_pos_ls[b] = log_sigmoid(s);
@@ -432,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void score_bwd_kernel(ScoreParams p) {
                     sa += c.ca[k].a[i] * c.ca[k].a[i];
                     sb += c.cb[k].a[i] * c.cb[k].a[i];
                 }
-            const float ia = 1.f / sqrtf(wave_sum(sa)), ib = 1.f / sqrtf(wave_sum(sb));
+            const float ia = rsqrt_f(wave_sum(sa)), ib = rsqrt_f(wave_sum(sb));
             float dota = 0.f, dotb = 0.f;
 #pragma unroll
             for (int k = 0; k < G; ++k)

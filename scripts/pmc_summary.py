@@ -1,0 +1,34 @@
+"""Summarise rocprofv3 --pmc passes (gpurun_out/pmc/<workload>/p*/run_counter_collection.csv):
+per kernel, the mean of each counter per dispatch, plus the gfx950-corrected HBM bytes
+(MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of a 16-B/lane streaming read -> x2; kB -> bytes)."""
+import collections
+import csv
+import glob
+import os
+import sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc/c2"
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
+    for row in csv.DictReader(open(f)):
+        k = row["Kernel_Name"]
+        k = k.split("(")[0].replace("void ", "").replace("kge_impl::", "")
+        per = vals[k][row["Counter_Name"]]
+        per.append(float(row["Counter_Value"]))
+out = []
+for k, cs in vals.items():
+    line = {"kernel": k}
+    for c, v in sorted(cs.items()):
+        line[c] = sum(v) / len(v)
+    if "FETCH_SIZE" in line:
+        line["hbm_read_bytes_corrected"] = line["FETCH_SIZE"] * 1024 * 2
+    if "WRITE_SIZE" in line:
+        line["hbm_write_bytes"] = line["WRITE_SIZE"] * 1024
+    if "TCC_HIT_sum" in line:
+        line["l2_hit_rate"] = line["TCC_HIT_sum"] / max(1.0, line["TCC_HIT_sum"] + line["TCC_MISS_sum"])
+    out.append(line)
+for line in out:
+    print(line["kernel"])
+    for c, v in line.items():
+        if c != "kernel":
+            print(f"    {c:28s} {v:,.1f}")

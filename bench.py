@@ -106,6 +106,35 @@ def run_step(m, pos, neg, mode, fn, ev=None):
     return ops.step_finish_raw(fn, ent, rel, m._rel_off, pos, m._D, m._gamma_f, m._range_f, ns)
 
 
+def train_step_bench(m, batches, steps, warmup):
+    """supervisor.py:13-30 train step (fused forward, HIP backward, HIP Keras Adam) on the same
+    workload: reported beside the scoring metric, never as `value`."""
+    from customknowledgegraphembedding_amd.optim import Adam
+    from customknowledgegraphembedding_amd.supervisor import Strategy, Sum, Trainer
+
+    B = batches[0][0].shape[0]
+    w = torch.ones(B, 1, device=batches[0][0].device)
+    data = [(pos, neg, w, torch.tensor([i % 2])) for i, (pos, neg) in enumerate(batches)]
+
+    def cycle():
+        while True:
+            yield from data
+
+    tr = Trainer(Strategy(), data, m, Adam(m.parameters(), lr=5e-5), Sum())
+    it = cycle()
+    for _ in range(warmup):
+        tr.train_step(it)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.train_step(it)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    N = batches[0][1].shape[1]
+    return {"ms_per_step": dt * 1e3, "triples_per_s": (B * N + B) / dt, "steps": steps,
+            "what": "fwd (kge_step_forward) + loss + bwd (HIP, fp32 atomics) + Keras Adam (HIP) on both tables"}
+
+
 def cpu_baseline(w, budget_s=15.0, rows=64):
     """The oracle's torch-CPU fp32 restatement of the reference graph (model.py:114-235 with all
     three branches per call, Q2; two calls per step as supervisor.py:17-18) on a bounded sample:
@@ -171,6 +200,7 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--train-steps", type=int, default=10, help="train-step side measurement (0 = skip)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -240,6 +270,8 @@ def main():
                      "kernel": "score_fwd_kernel (negatives)", "kernel_avg_us": kern_avg_s * 1e6,
                      "algorithmic_bytes_per_launch": neg_bytes},
     }
+    if a.train_steps > 0:
+        line["train_step"] = train_step_bench(m, batches, a.train_steps, 2)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w, a.cpu_budget)
     if rank == 0:

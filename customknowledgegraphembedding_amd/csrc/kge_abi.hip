@@ -2,6 +2,9 @@
 // selection, the per-row reduction kernels and the extern "C" entry points.
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
+
 #include <string>
 
 #include "kge_device.h"
@@ -71,6 +74,54 @@ __global__ __launch_bounds__(kBlock) void log_sigmoid_bwd_kernel(const float* __
                                                                  float* __restrict__ d_x) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n) d_x[i] = d_out[i] * sigmoidf(-x[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Dense Adam over a whole table (supervisor.py:26 optimizer.apply_gradients; run.py:111 Keras Adam).
+//   keras: m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2); p -= m * alpha / (sqrt(v) + eps),
+//          alpha = lr * sqrt(1 - b2^t) / (1 - b1^t)
+//   torch: m = lerp(m, g, 1 - b1); v = v * b2 + (1 - b2) g^2;
+//          p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// HBM-bound elementwise pass: 16-B loads/stores, grid-stride; optionally zeroes the gradient.
+// ---------------------------------------------------------------------------------------------
+struct AdamArgs {
+    float b1, b2, eps, alpha, step_size, bc2_sqrt;
+    int keras, zero_grad;
+};
+
+__device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v, const AdamArgs& a) {
+    const float gg = g;
+    if (a.keras) {
+        m += (gg - m) * (1.f - a.b1);
+        v += (gg * gg - v) * (1.f - a.b2);
+        p -= (m * a.alpha) / (sqrtf(v) + a.eps);
+    } else {
+        m = m + (1.f - a.b1) * (gg - m);
+        v = v * a.b2 + (1.f - a.b2) * gg * gg;
+        p -= a.step_size * m / (sqrtf(v) / a.bc2_sqrt + a.eps);
+    }
+    if (a.zero_grad) g = 0.f;
+}
+
+__global__ __launch_bounds__(kBlock) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                      float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                      AdamArgs a) {
+    const int64_t n4 = n / 4;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
+        float4 P = reinterpret_cast<float4*>(p)[i], G = reinterpret_cast<float4*>(g)[i];
+        float4 M = reinterpret_cast<float4*>(m)[i], Vv = reinterpret_cast<float4*>(v)[i];
+        adam_one(P.x, G.x, M.x, Vv.x, a);
+        adam_one(P.y, G.y, M.y, Vv.y, a);
+        adam_one(P.z, G.z, M.z, Vv.z, a);
+        adam_one(P.w, G.w, M.w, Vv.w, a);
+        reinterpret_cast<float4*>(p)[i] = P;
+        reinterpret_cast<float4*>(m)[i] = M;
+        reinterpret_cast<float4*>(v)[i] = Vv;
+        if (a.zero_grad) reinterpret_cast<float4*>(g)[i] = G;
+    }
+    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        adam_one(p[i], g[i], m[i], v[i], a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -395,6 +446,31 @@ int kge_log_sigmoid_bwd(const float* x, const float* d_out, int64_t n, float* d_
     hipLaunchKernelGGL(log_sigmoid_bwd_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        (hipStream_t)stream, x, d_out, n, d_x);
     return check_launch("kge_log_sigmoid_bwd");
+}
+
+int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
+                    float beta2, float eps, int64_t step, int keras, int zero_grad, void* stream) {
+    if (n < 0 || step < 1) return fail(KGE_EINVAL, "bad size or step (step is 1-based)");
+    if (n == 0) return ok();
+    if (!param || !grad || !exp_avg || !exp_avg_sq) return fail(KGE_EINVAL, "null pointer");
+    if (!aligned(param, 16) || !aligned(grad, 16) || !aligned(exp_avg, 16) || !aligned(exp_avg_sq, 16))
+        return fail(KGE_EINVAL, "adam buffers must be 16-byte aligned");
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    AdamArgs a;
+    a.b1 = beta1;
+    a.b2 = beta2;
+    a.eps = eps;
+    a.alpha = (float)((double)lr * std::sqrt(bc2) / bc1);
+    a.step_size = (float)((double)lr / bc1);
+    a.bc2_sqrt = (float)std::sqrt(bc2);
+    a.keras = keras;
+    a.zero_grad = zero_grad;
+    const int64_t want = (n / 4 + kBlock - 1) / kBlock;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, 256 * 8));
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, param, grad, exp_avg,
+                       exp_avg_sq, n, a);
+    return check_launch("kge_adam_update");
 }
 
 int64_t kge_score_bwd_workspace_size(int fn, int mode, int64_t B, int64_t N, int64_t D) {

@@ -1,0 +1,127 @@
+"""Training-step driver: mirror of tensorflow_codes/supervisor.py (Trainer) and run.py:8-17
+(check_device) on PyTorch-ROCm.
+
+`Trainer.train_step` is the caller of the hot path: the two model calls of supervisor.py:17-18 run
+as one fused `TFKGEModel.step_forward` (2 HIP launches), the loss is supervisor.py:19-23, the
+backward runs the HIP backward kernels, and the optimizer (customknowledgegraphembedding_amd.optim.Adam)
+runs the HIP Adam kernel.
+
+Multi-replica (torch.distributed, one process per GPU): the dense table gradients are summed across
+ranks with all-reduce before the optimizer step, as tf.distribute aggregates replica gradients with
+SUM in `apply_gradients` (supervisor.py:26); `metrics` receives `loss * num_replicas_in_sync`
+(supervisor.py:28).
+"""
+from __future__ import annotations
+
+import contextlib
+import time
+
+import torch
+
+
+class Strategy:
+    """The part of a tf.distribute strategy the reference uses (run.py:8-17, supervisor.py:28-30)."""
+
+    def __init__(self):
+        import torch.distributed as dist
+
+        self._dist = dist if (dist.is_available() and dist.is_initialized()) else None
+        self.num_replicas_in_sync = self._dist.get_world_size() if self._dist else 1
+
+    def scope(self):
+        return contextlib.nullcontext()
+
+    def run(self, fn, args=()):
+        return fn(*args)
+
+    def all_reduce_grads(self, params):
+        if self._dist is None or self.num_replicas_in_sync == 1:
+            return
+        for p in params:
+            if p.grad is not None:
+                self._dist.all_reduce(p.grad, op=self._dist.ReduceOp.SUM)
+
+
+def check_device() -> Strategy:
+    """run.py:8-17: the strategy for the visible accelerators."""
+    s = Strategy()
+    print("Number of accelerators: ", s.num_replicas_in_sync)
+    return s
+
+
+class Sum:
+    """tf.keras.metrics.Sum (run.py:114): accumulates on device, reads back on result()."""
+
+    def __init__(self, name="training_loss"):
+        self.name = name
+        self._total = None
+
+    def update_state(self, value):
+        v = value.detach().to(torch.float32).reshape(())
+        self._total = v.clone() if self._total is None else self._total + v
+
+    def result(self):
+        return torch.tensor(0.0) if self._total is None else self._total.detach().cpu()
+
+    def reset_states(self):
+        self._total = None
+
+
+class Trainer:
+    """supervisor.py:5-58."""
+
+    def __init__(self, strategy, dataloader, model, optimizer, metrics):
+        self.dataloader = dataloader
+        self.model = model
+        self.optimizer = optimizer
+        self.metrics = metrics
+        self.strategy = strategy
+
+    def loss(self, positive_sample, negative_sample, subsampling_weight, mode):
+        """supervisor.py:17-23 — both calls fused, then the weighted loss."""
+        negative_score, positive_score = self.model.step_forward(positive_sample, negative_sample, mode[0])
+        w = subsampling_weight.reshape(-1, 1).to(negative_score.dtype)
+        positive_sample_loss = -torch.sum(w * positive_score) / torch.sum(w)
+        negative_sample_loss = -torch.sum(w * negative_score) / torch.sum(w)
+        return (positive_sample_loss + negative_sample_loss) / 2
+
+    def train_step(self, data_iter):
+        """supervisor.py:13-30."""
+
+        def train_step_fn(positive_sample, negative_sample, subsampling_weight, mode):
+            dev = self.model.entity_embedding.device
+            positive_sample = positive_sample.to(dev, non_blocking=True)
+            negative_sample = negative_sample.to(dev, non_blocking=True)
+            subsampling_weight = subsampling_weight.to(dev, non_blocking=True)
+            mode = mode.cpu() if torch.is_tensor(mode) else mode
+            self.optimizer.zero_grad(set_to_none=True)
+            loss = self.loss(positive_sample, negative_sample, subsampling_weight, mode)
+            loss.backward()                                                    # :25
+            self.strategy.all_reduce_grads(self.model.parameters())
+            self.optimizer.step()                                              # :26
+            self.metrics.update_state(loss * self.strategy.num_replicas_in_sync)  # :28
+            return loss
+
+        return self.strategy.run(train_step_fn, next(data_iter))
+
+    def training(self, steps_per_tpu_call, epochs, steps_per_epoch):
+        """supervisor.py:32-58. Reproduces the reference loop, including its step accounting
+        (`step += steps_per_tpu_call` per single train_step call, supervisor.py:41-42)."""
+        step = 0
+        epoch = 0
+        epoch_start_time = time.time()
+        iteration_data = iter(self.dataloader)
+        while True:
+            self.train_step(iteration_data)
+            step += steps_per_tpu_call
+            print("=", end="", flush=True)
+            epoch_time = time.time() - epoch_start_time
+            print("\nEPOCH {:d}/{:d}".format(epoch + 1, epochs))
+            print("time: {:0.1f}s".format(epoch_time),
+                  "loss: {:0.4f}".format(round(float(self.metrics.result()), 4)), flush=True)
+            epoch = step // steps_per_epoch
+            epoch_start_time = time.time()
+            self.metrics.reset_states()
+            if epoch >= epochs:
+                break
+        print("DONE")

@@ -155,6 +155,18 @@ int kge_neg_reduce_bwd(const float* scores, int64_t B, int64_t N, int64_t ld,
 int kge_log_sigmoid_bwd(const float* x, const float* d_out, int64_t n, float* d_x, void* stream);
 
 /*
+ * Dense Adam step over n floats (supervisor.py:26 `optimizer.apply_gradients`, run.py:111 Keras Adam).
+ *   keras != 0: Keras Adam  (m += (g-m)(1-b1); v += (g^2-v)(1-b2);
+ *                            p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t))
+ *   keras == 0: torch.optim.Adam (p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps))
+ *   step is the 1-based step t; zero_grad != 0 also zeroes grad in the same pass.
+ * All four buffers 16-byte aligned, n floats each.
+ */
+int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                    float lr, float beta1, float beta2, float eps, int64_t step,
+                    int keras, int zero_grad, void* stream);
+
+/*
  * Backward of kge_score_indexed (GradientTape through the gathers, supervisor.py:25).
  * Accumulates (+=) into d_ent [nentity, ent_ld] and d_rel [nrelation, rel_ld] (same strides as
  * the tables). The query-side rows get one deterministic per-row sum over the N candidates; the

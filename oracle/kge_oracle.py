@@ -271,3 +271,27 @@ def make_tables(nentity, nrelation, entity_dim, relation_dim, gamma, hidden_dim,
     ent = torch.empty(nentity, entity_dim).uniform_(-init_range, init_range, generator=g)
     rel = torch.empty(nrelation, relation_dim).uniform_(-init_range, init_range, generator=g)
     return ent.to(dtype), rel.to(dtype), init_range
+
+
+# ------------------------------------------------------------------------------------------------
+# optimizer (supervisor.py:26 optimizer.apply_gradients; run.py:111 tf.keras.optimizers.Adam)
+# ------------------------------------------------------------------------------------------------
+def keras_adam_step(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, epsilon=1e-7):
+    """Keras Adam `update_step`, dense form (sparse IndexedSlices gradients are deduplicated by
+    summation before the update, which makes the sparse and dense forms equal). Returns (p, m, v)."""
+    alpha = lr * (1 - beta2 ** t) ** 0.5 / (1 - beta1 ** t)
+    m = m + (g - m) * (1 - beta1)
+    v = v + (g * g - v) * (1 - beta2)
+    p = p - (m * alpha) / (torch.sqrt(v) + epsilon)
+    return p, m, v
+
+
+def lrfn(epoch, num_replicas=1):
+    """run.py:69-84: linear warm-up over 5 epochs to 5e-5 * replicas, then 0.8**epoch decay."""
+    LR_START, LR_MAX, LR_MIN = 0.00001, 0.00005 * num_replicas, 0.00001
+    LR_RAMPUP_EPOCHS, LR_SUSTAIN_EPOCHS, LR_EXP_DECAY = 5.0, 0.0, 0.8
+    if float(epoch) < LR_RAMPUP_EPOCHS:
+        return (LR_MAX - LR_START) / LR_RAMPUP_EPOCHS * float(epoch) + LR_START
+    if float(epoch) < LR_RAMPUP_EPOCHS + LR_SUSTAIN_EPOCHS:
+        return LR_MAX
+    return (LR_MAX - LR_MIN) * LR_EXP_DECAY ** (float(epoch) - LR_RAMPUP_EPOCHS - LR_SUSTAIN_EPOCHS) + LR_MIN

@@ -1,0 +1,29 @@
+"""CPU tests of the host-side training driver pieces (no GPU calls)."""
+import torch
+
+from customknowledgegraphembedding_amd.supervisor import Strategy, Sum, check_device
+from oracle import kge_oracle as O
+
+
+def test_strategy_single_process():
+    s = check_device()
+    assert s.num_replicas_in_sync == 1
+    assert s.run(lambda a, b: a + b, (2, 3)) == 5
+
+
+def test_sum_metric():
+    m = Sum()
+    m.update_state(torch.tensor(1.5))
+    m.update_state(torch.tensor([2.0]))
+    assert float(m.result()) == 3.5
+    m.reset_states()
+    assert float(m.result()) == 0.0
+
+
+def test_lrfn_schedule_run_py():
+    # run.py:69-84
+    assert abs(O.lrfn(0) - 1e-5) < 1e-12
+    assert abs(O.lrfn(5) - 5e-5) < 1e-12
+    assert abs(O.lrfn(6) - ((5e-5 - 1e-5) * 0.8 + 1e-5)) < 1e-12
+    assert abs(O.lrfn(0, num_replicas=8) - 1e-5) < 1e-12
+    assert abs(O.lrfn(5, num_replicas=8) - 4e-4) < 1e-12

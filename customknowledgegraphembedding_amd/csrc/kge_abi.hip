@@ -103,25 +103,41 @@ __device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v,
     if (a.zero_grad) g = 0.f;
 }
 
+// one thread per 2 float4 (8 floats): all eight 16-B loads issued before any math
+constexpr int kAdamVec = 2;
+
 __global__ __launch_bounds__(kBlock) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                       AdamArgs a) {
     const int64_t n4 = n / 4;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
-        float4 P = reinterpret_cast<float4*>(p)[i], G = reinterpret_cast<float4*>(g)[i];
-        float4 M = reinterpret_cast<float4*>(m)[i], Vv = reinterpret_cast<float4*>(v)[i];
-        adam_one(P.x, G.x, M.x, Vv.x, a);
-        adam_one(P.y, G.y, M.y, Vv.y, a);
-        adam_one(P.z, G.z, M.z, Vv.z, a);
-        adam_one(P.w, G.w, M.w, Vv.w, a);
-        reinterpret_cast<float4*>(p)[i] = P;
-        reinterpret_cast<float4*>(m)[i] = M;
-        reinterpret_cast<float4*>(v)[i] = Vv;
-        if (a.zero_grad) reinterpret_cast<float4*>(g)[i] = G;
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kAdamVec;
+    float4 P[kAdamVec], G[kAdamVec], M[kAdamVec], Vv[kAdamVec];
+#pragma unroll
+    for (int u = 0; u < kAdamVec; ++u) {
+        const int64_t i = i0 + u;
+        if (i < n4) {
+            P[u] = reinterpret_cast<float4*>(p)[i];
+            G[u] = reinterpret_cast<float4*>(g)[i];
+            M[u] = reinterpret_cast<float4*>(m)[i];
+            Vv[u] = reinterpret_cast<float4*>(v)[i];
+        }
     }
-    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-        adam_one(p[i], g[i], m[i], v[i], a);
+#pragma unroll
+    for (int u = 0; u < kAdamVec; ++u) {
+        const int64_t i = i0 + u;
+        if (i < n4) {
+            adam_one(P[u].x, G[u].x, M[u].x, Vv[u].x, a);
+            adam_one(P[u].y, G[u].y, M[u].y, Vv[u].y, a);
+            adam_one(P[u].z, G[u].z, M[u].z, Vv[u].z, a);
+            adam_one(P[u].w, G[u].w, M[u].w, Vv[u].w, a);
+            reinterpret_cast<float4*>(p)[i] = P[u];
+            reinterpret_cast<float4*>(m)[i] = M[u];
+            reinterpret_cast<float4*>(v)[i] = Vv[u];
+            if (a.zero_grad) reinterpret_cast<float4*>(g)[i] = G[u];
+        }
+    }
+    if (blockIdx.x == 0)  // scalar tail (n % 4)
+        for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += kBlock) adam_one(p[i], g[i], m[i], v[i], a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -203,6 +219,16 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     int V = 1, G = 1;
     rc = pick_vg(p, V, G);
     if (rc) return rc;
+    if (kind == KIND_BWD) {
+        // backward: dword-per-lane layout (lane l owns elements l + 64k) so the gradient atomics are
+        // 256-B contiguous per wave-instruction; falls back to the forward layout past D = 1024
+        int g1 = 1;
+        while (g1 * kWave < p.D) g1 <<= 1;
+        if (g1 <= kBwdMaxG) {
+            V = 1;
+            G = g1;
+        }
+    }
     int64_t waves;
     if (kind == KIND_FINISH) {
         p.cpw = 1;
@@ -466,8 +492,10 @@ int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq
     a.bc2_sqrt = (float)std::sqrt(bc2);
     a.keras = keras;
     a.zero_grad = zero_grad;
-    const int64_t want = (n / 4 + kBlock - 1) / kBlock;
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, 256 * 8));
+    const int64_t per_block = (int64_t)kBlock * kAdamVec;
+    const int64_t want = (n / 4 + per_block - 1) / per_block;
+    if (want > INT32_MAX) return fail(KGE_EINVAL, "tensor too large for one launch");
+    const int blocks = (int)std::max<int64_t>(1, want);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, param, grad, exp_avg,
                        exp_avg_sq, n, a);
     return check_launch("kge_adam_update");

@@ -696,6 +696,16 @@ int launch_g(const ScoreParams& p, int kind, hipStream_t st, int blocks, int G) 
         case 2: launch_one<FN, CH, V, 2>(p, kind, st, blocks); return 0;
         case 4: launch_one<FN, CH, V, 4>(p, kind, st, blocks); return 0;
         case 8: launch_one<FN, CH, V, 8>(p, kind, st, blocks); return 0;
+        case 16:
+            // dword-per-lane backward for D <= 1024 (kBwdMaxG): every atomic wave-instruction then
+            // covers 256 contiguous bytes, the full-rate shape for global float atomics
+            if constexpr (V == 1) {
+                if (kind == KIND_BWD) {
+                    hipLaunchKernelGGL((score_bwd_kernel<FN, CH, 1, 16>), dim3(blocks), dim3(kBlock), 0, st, p);
+                    return 0;
+                }
+            }
+            return KGE_ENOTSUP;
         default: return KGE_ENOTSUP;
     }
 }

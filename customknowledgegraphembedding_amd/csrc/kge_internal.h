@@ -12,6 +12,7 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kMaxG = 8;  // float4 groups per lane per half-row kept in VGPRs (D <= 2048)
+constexpr int kBwdMaxG = 16;  // dword groups per lane of the backward's atomic-friendly layout (D <= 1024)
 
 enum Kind { KIND_FWD = 0, KIND_BWD = 1, KIND_FINISH = 2 };
 

@@ -50,6 +50,13 @@ SIGNATURES = {
         [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64,
          _c_f, _c_f, _c_f, _c_p, _c_i64, _c_i64, _c_f, _c_i, _c_p, _c_p, _c_p, _c_p],
     ),
+    "kge_score_sharded": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64,
+         _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_i64, _c_p],
+    ),
+    "kge_gather_rows": (
+        _c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
     "kge_score_dense": (
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64,

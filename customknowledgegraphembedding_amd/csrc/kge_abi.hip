@@ -141,6 +141,32 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float* __restrict__ p, flo
 }
 
 // ---------------------------------------------------------------------------------------------
+// Owned-row gather of a row-sharded table: out[i] = table[ids[i*stride] - lo] if this shard owns
+// the id, else zeros (so a SUM all-reduce over shards assembles the rows exactly). One wave per row.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void gather_owned_kernel(const float* __restrict__ tab, int64_t rows, int64_t ld,
+                                                              int64_t lo, const int64_t* __restrict__ ids,
+                                                              int64_t stride, int64_t n, int64_t width,
+                                                              float* __restrict__ out, int64_t out_ld, int vec4) {
+    const int64_t i = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t id = ids[i * stride] - lo;
+    const bool ok = id >= 0 && id < rows;
+    const float* src = tab + (ok ? id : 0) * ld;
+    float* dst = out + i * out_ld;
+    if (vec4) {
+        const rsrc_t r = make_rsrc(src, ok ? (uint32_t)(width * 4) : 0u);
+        for (int64_t e = (int64_t)lane * 4; e < width; e += 4 * kWave) {
+            const vecf<4> v = bload<4>(r, (uint32_t)(e * 4));
+            *reinterpret_cast<vecf<4>*>(dst + e) = v;
+        }
+    } else {
+        for (int64_t e = lane; e < width; e += kWave) dst[e] = ok ? src[e] : 0.f;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // host helpers
 // ---------------------------------------------------------------------------------------------
 thread_local std::string g_last_error;
@@ -396,6 +422,44 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
     return kge_step_finish(fn, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, B, D, gamma, emb_range,
                            modulus, neg_scores, N, ns_ld, temperature, adversarial, out_neg, pos_scores, out_pos,
                            stream);
+}
+
+int kge_score_sharded(int fn, int mode, const float* qent, int64_t q_ld, const float* rel, int64_t nrelation,
+                      int64_t rel_ld, int64_t rel_off, const float* shard, int64_t shard_rows, int64_t shard_ld,
+                      int64_t shard_lo, const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N,
+                      int64_t D, float gamma, float emb_range, float modulus, float* scores, int64_t scores_ld,
+                      void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (B < 0 || N < 0 || D <= 0 || shard_rows < 0) return fail(KGE_EINVAL, "bad shape");
+    if (empty(B, mode == KGE_SINGLE ? 1 : N)) return ok();
+    if (!pos || (mode != KGE_SINGLE && !neg) || !scores || !qent || !shard)
+        return fail(KGE_EINVAL, "null pointer");
+    ScoreParams p;
+    fill_indexed(p, fn, mode, shard, shard_rows, shard_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
+                 D, gamma, emb_range, modulus);
+    // query entity rows come pre-assembled (row b of qent); candidates from the local shard
+    p.qent = qent;
+    p.q_idx = nullptr;
+    p.q_ld = q_ld;
+    p.q_rows = B;
+    p.c_base = shard_lo;
+    p.skip_foreign = 1;
+    p.out = scores;
+    p.out_ld = scores_ld;
+    return run_score(fn, mode, p, KIND_FWD, stream);
+}
+
+int kge_gather_rows(const float* table, int64_t rows, int64_t ld, int64_t lo, const int64_t* ids, int64_t id_stride,
+                    int64_t n, int64_t width, float* out, int64_t out_ld, void* stream) {
+    if (n < 0 || width < 0 || rows < 0) return fail(KGE_EINVAL, "bad shape");
+    if (n == 0 || width == 0) return ok();
+    if (!table || !ids || !out) return fail(KGE_EINVAL, "null pointer");
+    const int vec4 = (width % 4 == 0 && ld % 4 == 0 && out_ld % 4 == 0 && aligned(table, 16) && aligned(out, 16));
+    const int64_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(gather_owned_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, table, rows,
+                       ld, lo, ids, id_stride, n, width, out, out_ld, vec4);
+    return check_launch("kge_gather_rows");
 }
 
 int kge_score_dense(int fn, int mode, const float* head, int64_t head_ld, const float* rel, int64_t rel_ld,

@@ -337,6 +337,7 @@ __device__ __forceinline__ void build_query_for(const ScoreParams& p, int64_t b,
 }
 
 __device__ __forceinline__ const float* cand_row(const ScoreParams& p, int64_t id, bool& ok) {
+    id -= p.c_base;
     ok = id >= 0 && id < p.c_rows;
     return p.cent + (ok ? id : 0) * p.c_ld;
 }
@@ -354,32 +355,33 @@ __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
     int64_t my_id = 0;
     if (lane < t.nc) my_id = p.c_idx ? p.c_idx[t.b * p.c_stride + t.n0 + lane] : t.b * p.c_dense + t.n0 + lane;
 
-    // software pipeline: row j+1 is in flight while row j is reduced
+    // software pipeline: row j+1 is in flight while row j is reduced. A foreign candidate of a
+    // row-sharded table (skip_foreign) loads nothing (0-byte descriptor) and scores 0.
     float my_score = 0.f;
     Cand<FN, V, G> x0, x1;
-    bool ok;
-    const float* row = cand_row(p, readlane64(my_id, 0), ok);
-    x0.load(row, ok, p.D, lane);
+    bool ok0, ok1;
+    const float* row = cand_row(p, readlane64(my_id, 0), ok0);
+    x0.load(row, ok0, p.D, lane);
     int j = 0;
     for (; j + 2 < t.nc; j += 2) {
-        row = cand_row(p, readlane64(my_id, j + 1), ok);
-        x1.load(row, ok, p.D, lane);
-        const float s0 = cand_score<FN, CH, V, G>(x0, q, p);
+        row = cand_row(p, readlane64(my_id, j + 1), ok1);
+        x1.load(row, ok1, p.D, lane);
+        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p);
         if (lane == j) my_score = s0;
-        row = cand_row(p, readlane64(my_id, j + 2), ok);
-        x0.load(row, ok, p.D, lane);
-        const float s1 = cand_score<FN, CH, V, G>(x1, q, p);
+        row = cand_row(p, readlane64(my_id, j + 2), ok0);
+        x0.load(row, ok0, p.D, lane);
+        const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p);
         if (lane == j + 1) my_score = s1;
     }
     if (j + 1 < t.nc) {
-        row = cand_row(p, readlane64(my_id, j + 1), ok);
-        x1.load(row, ok, p.D, lane);
-        const float s0 = cand_score<FN, CH, V, G>(x0, q, p);
+        row = cand_row(p, readlane64(my_id, j + 1), ok1);
+        x1.load(row, ok1, p.D, lane);
+        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p);
         if (lane == j) my_score = s0;
-        const float s1 = cand_score<FN, CH, V, G>(x1, q, p);
+        const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p);
         if (lane == j + 1) my_score = s1;
     } else {
-        const float s0 = cand_score<FN, CH, V, G>(x0, q, p);
+        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p);
         if (lane == j) my_score = s0;
     }
     if (lane < t.nc) p.out[t.b * p.out_ld + t.n0 + lane] = my_score;

@@ -30,6 +30,8 @@ struct ScoreParams {
     const float* cent;
     const int64_t* c_idx;
     int64_t c_ld, c_stride, c_rows, c_dense;
+    int64_t c_base;    // candidate ids are global: row = id - c_base (row-sharded tables)
+    int skip_foreign;  // sharded scoring: a candidate outside [c_base, c_base + c_rows) scores 0, no work
     float* out;
     int64_t out_ld;
     int64_t B, N;

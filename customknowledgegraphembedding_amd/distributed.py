@@ -1,0 +1,152 @@
+"""Multi-GPU scoring: one process per GPU, torch.distributed over RCCL (backend "nccl") on xGMI.
+
+Two layouts:
+
+* Replicas (C2 WN18RR, C3 FB15k-237; any table that fits one GPU's 288 GB): every rank holds the
+  whole table and scores its own batch rows; the data path has no collective (bench.py --gpus N).
+* Row-sharded owner-computes (`ShardedKGE`; C4 YAGO3-10 as the north star names it, and any table
+  larger than one GPU): rank r owns entity rows [lo_r, hi_r). The global batch (W*B rows) is known
+  to every rank (the sampler seed is replicated, so no ids move). One step:
+    1. query-entity rows: each rank gathers the rows it owns (zeros elsewhere)      kge_gather_rows
+       -> SUM all-reduce [W*B, ent_dim]                                              RCCL
+    2. every rank scores the candidates it owns (others exactly 0, no traffic) and
+       the positives whose tail it owns                                              kge_score_sharded
+    3. SUM reduce-scatter of the [W*B, N+1] partial scores -> each rank's home rows  RCCL
+    4. home rank: self-adversarial reduction + logsigmoid of its B rows               kge_neg_reduce/...
+  Each (row, candidate) has exactly one owner, so the SUMs add exact zeros: the sharded scores
+  equal the unsharded ones bitwise. Table rows never cross xGMI; per step a rank moves
+  W*B*ent_dim*4 bytes of query rows and W*B*(N+1)*4 bytes of scores.
+
+The GPU kernels are reached through a small backend object (`HipShardKernels`); tests on CPU swap
+in an oracle-backed backend to check the orchestration with gloo (tests/test_distributed_cpu.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from ._lib import FN_IDS, HEAD_BATCH, SINGLE, TAIL_BATCH, check
+from . import _lib
+from .model import _dims_for
+
+
+def shard_bounds(nentity: int, world: int, rank: int):
+    """Block partition of entity rows: the first (nentity % world) ranks get one extra row."""
+    base, extra = divmod(nentity, world)
+    lo = rank * base + min(rank, extra)
+    hi = lo + base + (1 if rank < extra else 0)
+    return lo, hi
+
+
+class HipShardKernels:
+    """libkge_hip.so entry points used by ShardedKGE (device tensors, torch's current stream)."""
+
+    @staticmethod
+    def gather_rows(table, lo, ids, id_stride, n, out):
+        rc = _lib.load().kge_gather_rows(table.data_ptr(), table.shape[0], table.stride(0), lo, ids.data_ptr(),
+                                         id_stride, n, out.shape[1], out.data_ptr(), out.stride(0),
+                                         torch.cuda.current_stream(table.device).cuda_stream)
+        check(rc, "kge_gather_rows")
+
+    @staticmethod
+    def score_sharded(fn, mode, qent, rel, rel_off, shard, lo, pos, neg, D, gamma, emb_range, modulus, out):
+        B = pos.shape[0]
+        N = 1 if mode == SINGLE else neg.shape[1]
+        rc = _lib.load().kge_score_sharded(
+            fn, mode, qent.data_ptr(), qent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), rel_off,
+            shard.data_ptr(), shard.shape[0], shard.stride(0), lo, pos.data_ptr(),
+            None if mode == SINGLE else neg.data_ptr(), 0 if mode == SINGLE else neg.stride(0), B, N, D,
+            float(gamma), float(emb_range), float(modulus), out.data_ptr(), out.stride(0),
+            torch.cuda.current_stream(shard.device).cuda_stream)
+        check(rc, "kge_score_sharded")
+
+    @staticmethod
+    def neg_reduce(scores, temperature, adversarial):
+        return ops.neg_reduce_raw(scores, temperature, adversarial)
+
+    @staticmethod
+    def log_sigmoid(x):
+        return ops.log_sigmoid_raw(x)
+
+
+def _reduce_scatter_rows(full, world, rank, group):
+    """SUM over ranks of `full` [W*B, C], returning this rank's [B, C] block. RCCL has a native
+    reduce-scatter; gloo (CPU tests) falls back to all-reduce + slice."""
+    B = full.shape[0] // world
+    if full.is_cuda:
+        out = torch.empty((B,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
+        dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=group)
+        return out
+    dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
+    return full[rank * B:(rank + 1) * B].contiguous()
+
+
+class ShardedKGE:
+    """Row-sharded owner-computes forward of supervisor.py:17-18 (both model calls).
+
+    The shard is the slice [lo, hi) of exactly the table TFKGEModel(seed) would build, so sharded
+    results can be compared with the unsharded model row for row.
+    """
+
+    def __init__(self, model_name, nentity, nrelation, hidden_dim, gamma, double_entity_embedding=False,
+                 double_relation_embedding=False, triple_relation_embedding=False, device=None, seed=0,
+                 group=None, kernels=None, full_tables=None):
+        from .model import TFKGEModel
+
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.kernels = kernels or HipShardKernels()
+        self.model_name = model_name
+        self.fn = FN_IDS[model_name]
+        self.nentity = nentity
+        self.lo, self.hi = shard_bounds(nentity, self.world, self.rank)
+        if full_tables is None:
+            ref = TFKGEModel(model_name, nentity, nrelation, hidden_dim, gamma, double_entity_embedding,
+                             double_relation_embedding, triple_relation_embedding, device="cpu", seed=seed)
+            ent, rel = ref.entity_embedding.detach(), ref.relation_embedding.detach()
+            self.gamma, self.emb_range = ref._gamma_f, ref._range_f
+            self.modulus = float(ref.modulus.reshape(-1)[0]) if model_name == "pRotatE" else 0.0
+        else:
+            ent, rel, self.gamma, self.emb_range, self.modulus = full_tables
+        self.entity_dim, self.relation_dim = ent.shape[1], rel.shape[1]
+        self.D, self.rel_off = _dims_for(model_name, self.entity_dim, self.relation_dim)
+        dev = device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu")
+        self.shard = ent[self.lo:self.hi].contiguous().to(dev)
+        self.relation_embedding = rel.contiguous().to(dev)  # replicated (R rows)
+        self.device = torch.device(dev)
+
+    def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True):
+        """pos_g [W*B, 3], neg_g [W*B, N] (the global batch, identical on every rank) ->
+        (out_neg [B], out_pos [B], scores [B, N]) for this rank's home rows [rank*B, (rank+1)*B)."""
+        mode = ops.mode_id(mode)
+        if mode not in (HEAD_BATCH, TAIL_BATCH):
+            raise ValueError("step_forward needs a negative mode (0 or 1)")
+        WB, N = neg_g.shape
+        if WB % self.world:
+            raise ValueError("global batch must split evenly over ranks")
+        k = self.kernels
+        dev = self.device
+        # 1. query-entity rows (t for head-batch, h otherwise) and, in head-batch mode, the
+        #    positives' h rows, assembled by a SUM all-reduce of owner-gathered rows
+        qcols = [2, 0] if mode == HEAD_BATCH else [0]
+        rows = torch.empty((len(qcols), WB, self.entity_dim), dtype=torch.float32, device=dev)
+        for i, c in enumerate(qcols):
+            k.gather_rows(self.shard, self.lo, pos_g[:, c:], 3, WB, rows[i])
+        if self.world > 1:
+            dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=self.group)
+        qe, ph = rows[0], rows[-1]
+        # 2. owner-computes scores: negatives in `mode`, positives in single mode -> column N
+        part = torch.empty((WB, N + 1), dtype=torch.float32, device=dev)
+        k.score_sharded(self.fn, mode, qe, self.relation_embedding, self.rel_off, self.shard, self.lo, pos_g,
+                        neg_g, self.D, self.gamma, self.emb_range, self.modulus, part)
+        k.score_sharded(self.fn, SINGLE, ph, self.relation_embedding, self.rel_off, self.shard, self.lo, pos_g,
+                        None, self.D, self.gamma, self.emb_range, self.modulus, part[:, N:])
+        # 3. SUM reduce-scatter -> home rows
+        home = _reduce_scatter_rows(part, self.world, self.rank, self.group) if self.world > 1 else part
+        scores = home[:, :N].contiguous()
+        # 4. per-row reductions on the home rank
+        out_neg = k.neg_reduce(scores, temperature, adversarial)
+        out_pos = k.log_sigmoid(home[:, N].contiguous())
+        return out_neg, out_pos, scores

@@ -116,6 +116,30 @@ int kge_step_finish(int fn,
                     float* out_neg, float* pos_scores, float* out_pos, void* stream);
 
 /*
+ * Owner-computes scoring on a ROW-SHARDED entity table. This shard holds global rows
+ * [shard_lo, shard_lo + shard_rows). Query-entity rows are pre-assembled by the caller (row b of
+ * `qent`, e.g. kge_gather_rows + a SUM all-reduce over shards); the relation table is replicated.
+ * Candidates this shard does not own score exactly 0 and cost no memory traffic, so a SUM
+ * reduce over shards yields the unsharded scores bitwise. For KGE_SINGLE the candidate is pos[b,2].
+ */
+int kge_score_sharded(int fn, int mode,
+                      const float* qent, int64_t q_ld,
+                      const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off,
+                      const float* shard, int64_t shard_rows, int64_t shard_ld, int64_t shard_lo,
+                      const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                      int64_t B, int64_t N, int64_t D,
+                      float gamma, float emb_range, float modulus,
+                      float* scores, int64_t scores_ld, void* stream);
+
+/*
+ * out[i, 0:width] = table[ids[i*id_stride] - lo, 0:width] if 0 <= ids[..] - lo < rows, else 0.
+ * Row gather from a (sharded) table; the zero rows make a SUM all-reduce over shards exact.
+ */
+int kge_gather_rows(const float* table, int64_t rows, int64_t ld, int64_t lo,
+                    const int64_t* ids, int64_t id_stride, int64_t n, int64_t width,
+                    float* out, int64_t out_ld, void* stream);
+
+/*
  * Score pre-gathered rows: the model_func plugin surface itself,
  * `model_func[name](head, relation, tail, mode) -> [B, 1|N]` (model.py:109-112,207).
  *   head [B, Nh, *] rows (row stride head_ld), Nh = N for KGE_HEAD_BATCH else 1

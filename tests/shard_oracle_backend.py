@@ -1,0 +1,46 @@
+"""Oracle-backed stand-in for distributed.HipShardKernels (TEST INFRASTRUCTURE ONLY): lets the
+row-sharded orchestration run on CPU under gloo, with the oracle as the local scorer/checker."""
+import torch
+import torch.nn.functional as F
+
+from customknowledgegraphembedding_amd._lib import FN_IDS, HEAD_BATCH, SINGLE
+from oracle import kge_oracle as O
+
+NAMES = {v: k for k, v in FN_IDS.items()}
+MODES = {0: "head-batch", 1: "tail-batch", 3: "single"}
+
+
+class OracleShardKernels:
+    @staticmethod
+    def gather_rows(table, lo, ids, id_stride, n, out):
+        flat = ids.as_strided((n,), (id_stride,))  # the C-ABI's ids[i * id_stride]
+        for i in range(n):
+            r = int(flat[i]) - lo
+            out[i] = table[r] if 0 <= r < table.shape[0] else 0.0
+
+    @staticmethod
+    def score_sharded(fn, mode, qent, rel, rel_off, shard, lo, pos, neg, D, gamma, emb_range, modulus, out):
+        name = NAMES[fn]
+        B = pos.shape[0]
+        cand = pos[:, 2:3] if mode == SINGLE else neg
+        for b in range(B):
+            q = qent[b].double().view(1, 1, -1)
+            r = rel[int(pos[b, 1])].double().view(1, 1, -1)
+            for n in range(cand.shape[1]):
+                row = int(cand[b, n]) - lo
+                if not (0 <= row < shard.shape[0]):
+                    out[b, n] = 0.0
+                    continue
+                c = shard[row].double().view(1, 1, -1)
+                h, t = (c, q) if mode == HEAD_BATCH else (q, c)
+                out[b, n] = float(O.model_func(name, h, r, t, MODES[mode], gamma, emb_range, modulus)[0, 0])
+
+    @staticmethod
+    def neg_reduce(scores, temperature, adversarial):
+        s = scores.double()
+        red = O.adv_reduce(s, temperature) if adversarial else O.mean_reduce(s)
+        return red[:, 0]
+
+    @staticmethod
+    def log_sigmoid(x):
+        return F.logsigmoid(x.double())

@@ -1,0 +1,76 @@
+"""World-size-2 gloo test of the row-sharded owner-computes scorer (distributed.ShardedKGE) with
+the oracle as each rank's local scorer: the sharded forward must equal the unsharded reference
+graph (TF call semantics) for every home row."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from customknowledgegraphembedding_amd.distributed import ShardedKGE, shard_bounds
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, name, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.shard_oracle_backend import OracleShardKernels
+        from oracle import kge_oracle as O
+
+        E, R, d, B, N, gamma = 37, 5, 6, 3, 7, 9.0
+        de = name in ("ComplEx", "RotatE", "InterHT")
+        sk = ShardedKGE(name, E, R, d, gamma, double_entity_embedding=de,
+                        double_relation_embedding=(name == "ComplEx"), triple_relation_embedding=(name == "InterHT"),
+                        device="cpu", seed=3, kernels=OracleShardKernels())
+        g = np.random.RandomState(8)
+        WB = world * B
+        pos = torch.from_numpy(np.stack([g.randint(E, size=WB), g.randint(R, size=WB), g.randint(E, size=WB)], 1))
+        neg = torch.from_numpy(g.randint(E, size=(WB, N)))
+        from customknowledgegraphembedding_amd.model import TFKGEModel
+        ref = TFKGEModel(name, E, R, d, gamma, de, name == "ComplEx", name == "InterHT", device="cpu", seed=3)
+        ent, rel = ref.entity_embedding.detach().double(), ref.relation_embedding.detach().double()
+        home = slice(rank * B, (rank + 1) * B)
+        errs = []
+        for mode in (0, 1):
+            out_neg, out_pos, scores = sk.step_forward(pos, neg, mode)
+            want_s = O.score(name, ent, rel, pos[home], neg[home], mode, gamma, ref._range_f, sk.modulus)
+            want_neg = O.tf_call(name, ent, rel, pos[home], neg[home], mode, gamma, ref._range_f, sk.modulus)
+            want_pos = O.tf_call(name, ent, rel, pos[home], neg[home], 3, gamma, ref._range_f, sk.modulus)
+            errs.append(float((scores.double() - want_s).abs().max()))
+            errs.append(float((out_neg.double() - want_neg[:, 0]).abs().max()))
+            errs.append(float((out_pos.double() - want_pos[:, 0]).abs().max()))
+        results[rank] = max(errs)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["DistMult", "InterHT", "RotatE"])
+def test_sharded_owner_computes_world2_gloo(name):
+    world = 2
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), name, results), nprocs=world, join=True)
+    assert len(results) == world
+    for r in range(world):
+        assert results[r] < 1e-5, (r, results[r])
+
+
+def test_shard_bounds_cover_every_row_once():
+    for E, W in ((10, 3), (123182, 8), (7, 8)):
+        rows = []
+        for r in range(W):
+            lo, hi = shard_bounds(E, W, r)
+            rows.extend(range(lo, hi))
+        assert rows == list(range(E))

@@ -49,6 +49,16 @@ WORKLOADS = {
     "c4": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512", fn="DistMult",
                nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False, dr=False,
                B=512, N=1024),
+    # configs[3] as the north star states it: entity table row-sharded over the ranks
+    # (owner-computes, distributed.ShardedKGE; bz=512 per rank)
+    # configs[4]: FB15k link-prediction eval, each query vs all 14 951 entities, filtered ranks
+    # (DistMult d=1000 assumed); a step = one batch of 1024 queries, one mode
+    "c5": dict(name="FB15k filtered eval DistMult d=1000, 1024 queries/step vs all 14951 entities",
+               fn="DistMult", nentity=14951, nrelation=1345, hidden_dim=1000, gamma=24.0, de=False, tr=False,
+               dr=False, B=1024, N=14951, eval=True),
+    "c4s": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512/rank, row-sharded owner-computes",
+                fn="DistMult", nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False,
+                dr=False, B=512, N=1024, sharded=True),
 }
 
 
@@ -104,6 +114,99 @@ def run_step(m, pos, neg, mode, fn, ev=None):
     if ev is not None:
         ev[1].record()
     return ops.step_finish_raw(fn, ent, rel, m._rel_off, pos, m._D, m._gamma_f, m._range_f, ns)
+
+
+def sharded_bench(w, a, world, rank, device, dist_on):
+    """c4s: ShardedKGE.step_forward on the global batch (replicated by seed on every rank); the
+    timed step includes the two RCCL collectives. Returns (elapsed_s, per-step kernel-free info)."""
+    from customknowledgegraphembedding_amd.distributed import ShardedKGE
+    sk = ShardedKGE(w["fn"], w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"],
+                    double_entity_embedding=w["de"], double_relation_embedding=w["dr"],
+                    triple_relation_embedding=w["tr"], device=device, seed=0)
+    E, R, B, N = w["nentity"], w["nrelation"], w["B"], w["N"]
+    WB = world * B
+    batches = []
+    for i in range(4):
+        g = np.random.RandomState(100 + i)  # same seed on every rank: the global batch is replicated
+        pos = np.stack([g.randint(E, size=WB), g.randint(R, size=WB), g.randint(E, size=WB)], 1)
+        neg = np.random.RandomState(200 + i).randint(E, size=(WB, N))
+        batches.append((torch.from_numpy(pos).to(device), torch.from_numpy(neg).to(device)))
+    for i in range(a.warmup):
+        sk.step_forward(*batches[i % 4], i % 2)
+    torch.cuda.synchronize()
+    if dist_on:
+        import torch.distributed as tdist
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        sk.step_forward(*batches[i % 4], i % 2)
+    torch.cuda.synchronize()
+    if dist_on:
+        tdist.barrier()
+    return time.perf_counter() - t0
+
+
+def eval_bench(w, a, device):
+    """c5: upstream test_step's scoring + filtered ranking for batches of queries: kge_eval_query +
+    kge_gemm_nt (fp32 MFMA, events around it) + kge_rank_filtered. Returns the JSON line."""
+    from customknowledgegraphembedding_amd import evaluate
+    from customknowledgegraphembedding_amd.model import KGEModel
+    m = KGEModel(w["fn"], w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"], device=device, seed=0)
+    E, R, Bq = w["nentity"], w["nrelation"], w["B"]
+    g = np.random.RandomState(7)
+    true = np.stack([g.randint(E, size=200000), g.randint(R, size=200000), g.randint(E, size=200000)], 1)
+    batches = []
+    for i in range(4):
+        q = true[i * Bq:(i + 1) * Bq]
+        mode = "head-batch" if i % 2 == 0 else "tail-batch"
+        ptr, ids = evaluate.build_filter(q, mode, true)
+        col = 0 if mode == "head-batch" else 2
+        pos = torch.from_numpy(q).to(device)
+        batches.append((pos, mode, pos[:, col].contiguous(), torch.from_numpy(ptr).to(device),
+                        torch.from_numpy(ids).to(device)))
+    S = torch.empty((Bq, E), dtype=torch.float32, device=device)
+    K = m.entity_embedding.shape[1]
+    ent = m.entity_embedding.detach()
+    Q = torch.empty((Bq, K), dtype=torch.float32, device=device)
+    lib = __import__("customknowledgegraphembedding_amd._lib", fromlist=["load"]).load()
+
+    def step(b, ev=None):
+        pos, mode, truth, fptr, fids = b
+        st = torch.cuda.current_stream().cuda_stream
+        lib.kge_eval_query(FN_IDS[w["fn"]], 0 if mode == "head-batch" else 1, ent.data_ptr(), E, ent.stride(0),
+                           m.relation_embedding.data_ptr(), R, m.relation_embedding.stride(0), pos.data_ptr(), Bq,
+                           m._D, Q.data_ptr(), K, st)
+        if ev is not None:
+            ev[0].record()
+        lib.kge_gemm_nt(Q.data_ptr(), K, ent.data_ptr(), ent.stride(0), S.data_ptr(), E, Bq, E, K, st)
+        if ev is not None:
+            ev[1].record()
+        return evaluate.rank_filtered(S, truth, fptr, fids)
+
+    for i in range(a.warmup):
+        step(batches[i % 4])
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    ranks = []
+    for i in range(a.steps):
+        ranks.append(step(batches[i % 4], evs[i]))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    gemm_s = statistics.mean(e0.elapsed_time(e1) for e0, e1 in evs) / 1e3
+    flops = 2.0 * Bq * E * K
+    r = torch.cat(ranks).cpu().numpy()
+    met = evaluate.metrics_from_ranks(r)
+    return {"metric": f"ranked queries/sec, {w['name']}", "value": Bq * a.steps / dt, "unit": "queries/s",
+            "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic triples (random init: MRR is not a quality number)",
+            "config": {"workload": w["name"], "queries_per_step": Bq, "entities": E, "K": K},
+            "roofline": {"bound": "mfma", "achieved": flops / gemm_s / 1e12, "peak": 157.3, "unit": "TFLOP/s",
+                         "frac": flops / gemm_s / 1e12 / 157.3, "traffic": None,
+                         "kernel": "gemm_nt_f32_kernel (v_mfma_f32_32x32x2_f32)", "kernel_avg_us": gemm_s * 1e6},
+            "filtered_metrics": met}
 
 
 def train_step_bench(m, batches, steps, warmup):
@@ -216,8 +319,38 @@ def main():
 
     w = WORKLOADS[a.workload]
     fn = FN_IDS[w["fn"]]
-    m, batches = make_inputs(w, rank, device)
     B, N = w["B"], w["N"]
+    if w.get("eval"):
+        line = eval_bench(w, a, device)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist:
+            tdist.destroy_process_group()
+        return
+    if w.get("sharded"):
+        elapsed = sharded_bench(w, a, world, rank, device, dist)
+        if dist:
+            t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        ent, _, _, rel_used = dims(w)
+        owned_bytes = B * N * (4 * ent + 12)  # per rank per step, on average
+        line = {"metric": f"scored (pos+neg) triples/sec, {w['name']}", "value": (B * N + B) * a.steps * world / elapsed,
+                "unit": "triples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "f32", "data": "synthetic global batch replicated by seed",
+                "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N,
+                           "parallelism": f"rowshard{world}"},
+                "roofline": {"bound": "hbm", "achieved": owned_bytes / (elapsed / a.steps) / 1e9,
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": owned_bytes / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                             "kernel": "whole sharded step (gather, all-reduce, score, reduce-scatter, finish)"}}
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist:
+            tdist.destroy_process_group()
+        return
+    m, batches = make_inputs(w, rank, device)
 
     def barrier():
         if dist:

@@ -57,6 +57,10 @@ SIGNATURES = {
     ),
     "kge_gather_rows": (
         _c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
+    "kge_eval_query": (
+        _c_i, [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
+    "kge_gemm_nt": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p]),
+    "kge_rank_filtered": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "kge_score_dense": (
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64,

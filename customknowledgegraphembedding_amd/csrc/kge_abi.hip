@@ -462,6 +462,56 @@ int kge_gather_rows(const float* table, int64_t rows, int64_t ld, int64_t lo, co
     return check_launch("kge_gather_rows");
 }
 
+int kge_eval_query(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                   int64_t nrelation, int64_t rel_ld, const int64_t* pos, int64_t B, int64_t D, float* Q, int64_t ldq,
+                   void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (fn != KGE_DISTMULT && fn != KGE_COMPLEX)
+        return fail(KGE_ENOTSUP, "kge_eval_query: only DistMult and ComplEx score as a dense contraction");
+    if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_eval_query needs mode 0 or 1");
+    if (B < 0 || D <= 0) return fail(KGE_EINVAL, "bad shape");
+    if (B == 0) return ok();
+    if (!ent || !rel || !pos || !Q) return fail(KGE_EINVAL, "null pointer");
+    ScoreParams p;
+    fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, 0, pos, nullptr, 0, B, 1, D, 0.f, 1.f,
+                 0.f);
+    int V = 1, G = 1;
+    rc = pick_vg(p, V, G);
+    if (rc) return rc;
+    if (ldq % V) V = 1;
+    while (V > 1 && !aligned(Q, 4 * V)) V >>= 1;
+    G = 1;
+    while (G * kWave * V < D) G <<= 1;
+    if (G > kMaxG) return fail(KGE_ENOTSUP, "dimension too large");
+    const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
+    rc = launch_eval_query_any(fn, mode == KGE_HEAD_BATCH, p, (hipStream_t)stream, (int)blocks, V, G, Q, ldq);
+    if (rc) return fail(rc, "no eval-query kernel for this width");
+    return check_launch("kge_eval_query");
+}
+
+int kge_gemm_nt(const float* A, int64_t lda, const float* Bm, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                int64_t N, int64_t K, void* stream) {
+    if (M < 0 || N < 0 || K < 0) return fail(KGE_EINVAL, "bad shape");
+    if (M == 0 || N == 0) return ok();
+    if (!A || !Bm || !C) return fail(KGE_EINVAL, "null pointer");
+    if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return fail(KGE_EINVAL, "shape exceeds int32");
+    if (K % 4 || lda % 4 || ldb % 4 || !aligned(A, 16) || !aligned(Bm, 16))
+        return fail(KGE_ENOTSUP, "kge_gemm_nt needs K, lda, ldb multiples of 4 and 16-byte aligned A, B");
+    launch_gemm_nt(A, Bm, C, (int)M, (int)N, (int)K, lda, ldb, ldc, (hipStream_t)stream);
+    return check_launch("kge_gemm_nt");
+}
+
+int kge_rank_filtered(const float* scores, int64_t M, int64_t N, int64_t ld, const int64_t* truth,
+                      const int64_t* filter_ptr, const int64_t* filter_ids, int64_t* ranks, void* stream) {
+    if (M < 0 || N < 0) return fail(KGE_EINVAL, "bad shape");
+    if (M == 0) return ok();
+    if (!scores || !truth || !ranks || (filter_ptr && !filter_ids)) return fail(KGE_EINVAL, "null pointer");
+    if (M > INT32_MAX) return fail(KGE_EINVAL, "too many rows");
+    launch_rank(scores, M, N, ld, truth, filter_ptr, filter_ids, ranks, (hipStream_t)stream);
+    return check_launch("kge_rank_filtered");
+}
+
 int kge_score_dense(int fn, int mode, const float* head, int64_t head_ld, const float* rel, int64_t rel_ld,
                     int64_t rel_off, const float* tail, int64_t tail_ld, int64_t B, int64_t N, int64_t D, float gamma,
                     float emb_range, float modulus, float* scores, int64_t scores_ld, void* stream) {

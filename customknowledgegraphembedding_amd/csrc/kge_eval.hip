@@ -1,0 +1,230 @@
+// kge_eval.hip — filtered link-prediction evaluation against ALL entities (SURVEY §8f rank 3,
+// BASELINE config C5: FB15k, each test triple vs all 14 951 entities, filtered MRR).
+//
+// Reference: upstream KGEModel.test_step (KnowledgeGraphEmbedding/codes/model.py, absent; restated in
+// oracle/kge_oracle.py:eval_ranks): for every test triple and mode, score every entity as the
+// candidate, push filtered candidates (other true triples) below the positive, and rank the positive.
+//
+//   * DistMult / ComplEx: scoring against all entities is a true dense contraction
+//     S[q, e] = Q[q, :] . E[e, :]  (Q = h*r or r*t; ComplEx: [re_q | im_q] against [re_e | im_e]),
+//     run on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: exact f32, k-ordered fma chain).
+//   * Every score function: S via the VALU scorer with the candidate row stride 0 (kge_abi.hip).
+//   * kge_rank_filtered: exact integer ranks from S, the true entity and a CSR filter list.
+#include <string>
+
+#include "kge_device.h"
+
+namespace kge_impl {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------------------------
+// Query operand rows for the MFMA contraction: Q[b] = q0 (DistMult) or [q0 | q1] (ComplEx), built by
+// the same Query<> code the scoring kernels use (tail mode: (h, r); head mode: (r, t)).
+// ---------------------------------------------------------------------------------------------
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void eval_query_kernel(ScoreParams p, float* __restrict__ Q, int64_t ldq) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    Query<FN, CH, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+    const int DV = p.D / V;
+    float* row = Q + b * ldq;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const int g = lane + k * kWave;
+        if (g < DV) {
+            *reinterpret_cast<vecf<V>*>(row + g * V) = q.q0[k];
+            if constexpr (FN == KGE_COMPLEX) *reinterpret_cast<vecf<V>*>(row + p.D + g * V) = q.q1[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// S[M, N] = A[M, K] . B[N, K]^T, fp32 in / fp32 out, on v_mfma_f32_32x32x2_f32.
+// Block 256 threads = 2 x 2 waves, block tile 128 x 128, wave tile 64 x 64 (2 x 2 MFMA tiles, four
+// independent accumulators -> back-to-back issue), K staged through LDS in chunks of 16, double
+// buffered (next chunk's global loads in registers while the current chunk is multiplied).
+// LDS images are k-major ([k][m]) so a wave's fragment read (lanes 0-31 one k, 32-63 the next)
+// is 32 consecutive dwords per half-wave: conflict-free ds_read_b32.
+// ---------------------------------------------------------------------------------------------
+constexpr int GBM = 128, GBN = 128, GBK = 16;
+constexpr int GLD = GBM + 4;  // padded LDS row (floats)
+
+__global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
+                                                             float* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                             int64_t ldb, int64_t ldc) {
+    __shared__ __attribute__((aligned(16))) float As[2][GBK][GLD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][GBK][GLD];
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // XCD-aware: blocks b and b+8 share an XCD (round-robin placement); give each XCD a contiguous
+    // run of N-tiles (entity rows) so its L2 keeps reusing the same B rows across query tiles.
+    const int ntn = (N + GBN - 1) / GBN, ntm = (M + GBM - 1) / GBM;
+    const int nblk = ntn * ntm;
+    int bid = blockIdx.x;
+    if (nblk % 8 == 0) bid = (bid % 8) * (nblk / 8) + bid / 8;
+    const int tn = bid / ntm, tm = bid % ntm;
+    const int m0 = tm * GBM, n0 = tn * GBN;
+
+    // global -> register staging: 128 rows x 16 floats per operand = 512 float4, 2 per thread
+    float4 ra[2], rb[2];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int f = t + u * kBlock;
+            const int r = f >> 2, kq = (f & 3) * 4;
+            const int ka = k0 + kq;
+            const int gm = m0 + r, gn = n0 + r;
+            ra[u] = (gm < M && ka < K) ? *reinterpret_cast<const float4*>(A + (int64_t)gm * lda + ka)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            rb[u] = (gn < N && ka < K) ? *reinterpret_cast<const float4*>(Bm + (int64_t)gn * ldb + ka)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int f = t + u * kBlock;
+            const int r = f >> 2, kq = (f & 3) * 4;
+            As[buf][kq + 0][r] = ra[u].x;
+            As[buf][kq + 1][r] = ra[u].y;
+            As[buf][kq + 2][r] = ra[u].z;
+            As[buf][kq + 3][r] = ra[u].w;
+            Bs[buf][kq + 0][r] = rb[u].x;
+            Bs[buf][kq + 1][r] = rb[u].y;
+            Bs[buf][kq + 2][r] = rb[u].z;
+            Bs[buf][kq + 3][r] = rb[u].w;
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = (K + GBK - 1) / GBK;
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    const int half = lane >> 5, col = lane & 31;
+    for (int kc = 0; kc < nk; ++kc) {
+        const int buf = kc & 1;
+        if (kc + 1 < nk) gload((kc + 1) * GBK);  // next chunk in flight during the MFMAs
+#pragma unroll
+        for (int s = 0; s < GBK / 2; ++s) {
+            const int kk = 2 * s + half;
+            float a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[i] = As[buf][kk][wm * 64 + i * 32 + col];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kk][wn * 64 + j * 32 + col];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (kc + 1 < nk) {
+            sstore(buf ^ 1);
+            __syncthreads();
+        }
+    }
+    // epilogue: C/D map of 32x32 MFMAs: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int gn = n0 + wn * 64 + j * 32 + col;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (gm < M && gn < N) C[(int64_t)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Filtered rank of the true entity in each score row (one block per query row):
+//   rank = 1 + #{ e != true : S[e] > S[true] } - #{ f in filt[q], f != true : S[f] > S[true] }
+// The filter list of a row must hold distinct ids (the host dedups). Integer counts: exact.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void rank_kernel(const float* __restrict__ S, int64_t M, int64_t N, int64_t ld,
+                                                      const int64_t* __restrict__ truth,
+                                                      const int64_t* __restrict__ fptr,
+                                                      const int64_t* __restrict__ fids, int64_t* __restrict__ ranks) {
+    const int64_t q = blockIdx.x;
+    if (q >= M) return;
+    const float* row = S + q * ld;
+    const int64_t tr = truth[q];
+    const bool tok = tr >= 0 && tr < N;
+    const float st = tok ? row[tr] : -INFINITY;
+    unsigned long long cnt = 0;
+    for (int64_t e = threadIdx.x; e < N; e += kBlock) cnt += (e != tr && row[e] > st) ? 1ull : 0ull;
+    if (fptr) {
+        for (int64_t i = fptr[q] + threadIdx.x; i < fptr[q + 1]; i += kBlock) {
+            const int64_t f = fids[i];
+            if (f >= 0 && f < N && f != tr && row[f] > st) cnt -= 1ull;
+        }
+    }
+    // block reduction of the (exact, wrapping) counts
+    __shared__ unsigned long long red[kBlock / kWave];
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, kWave);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long c = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) c += red[w];
+        ranks[q] = 1 + (int64_t)c;
+    }
+}
+
+template <int FN, bool CH>
+int launch_eval_query(const ScoreParams& p, hipStream_t st, int blocks, int V, int G, float* Q, int64_t ldq) {
+#define KGE_EQ(VV, GG)                                                                                   \
+    if (V == VV && G == GG) {                                                                            \
+        hipLaunchKernelGGL((eval_query_kernel<FN, CH, VV, GG>), dim3(blocks), dim3(kBlock), 0, st, p, Q, ldq); \
+        return 0;                                                                                        \
+    }
+    KGE_EQ(4, 1) KGE_EQ(4, 2) KGE_EQ(4, 4) KGE_EQ(4, 8)
+    KGE_EQ(2, 1) KGE_EQ(2, 2) KGE_EQ(2, 4) KGE_EQ(2, 8)
+    KGE_EQ(1, 1) KGE_EQ(1, 2) KGE_EQ(1, 4) KGE_EQ(1, 8)
+#undef KGE_EQ
+    return KGE_ENOTSUP;
+}
+
+}  // namespace
+
+int launch_eval_query_any(int fn, bool ch, const ScoreParams& p, hipStream_t st, int blocks, int V, int G, float* Q,
+                          int64_t ldq) {
+    if (fn == KGE_DISTMULT)
+        return ch ? launch_eval_query<KGE_DISTMULT, true>(p, st, blocks, V, G, Q, ldq)
+                  : launch_eval_query<KGE_DISTMULT, false>(p, st, blocks, V, G, Q, ldq);
+    if (fn == KGE_COMPLEX)
+        return ch ? launch_eval_query<KGE_COMPLEX, true>(p, st, blocks, V, G, Q, ldq)
+                  : launch_eval_query<KGE_COMPLEX, false>(p, st, blocks, V, G, Q, ldq);
+    return KGE_ENOTSUP;
+}
+
+int launch_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                   int64_t ldc, hipStream_t st) {
+    const int blocks = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+    hipLaunchKernelGGL(gemm_nt_f32_kernel, dim3(blocks), dim3(kBlock), 0, st, A, B, C, M, N, K, lda, ldb, ldc);
+    return 0;
+}
+
+int launch_rank(const float* S, int64_t M, int64_t N, int64_t ld, const int64_t* truth, const int64_t* fptr,
+                const int64_t* fids, int64_t* ranks, hipStream_t st) {
+    hipLaunchKernelGGL(rank_kernel, dim3((unsigned)M), dim3(kBlock), 0, st, S, M, N, ld, truth, fptr, fids, ranks);
+    return 0;
+}
+
+}  // namespace kge_impl

@@ -1,0 +1,115 @@
+"""Filtered link-prediction evaluation against all entities: the upstream `KGEModel.test_step`
+(KnowledgeGraphEmbedding/codes/model.py, absent from the snapshot; its TestDataset builds, per test
+triple and mode, a candidate list over every entity in which the other true triples are replaced by
+the positive with bias -1; ranks come from argsort). BASELINE config C5.
+
+The scores of a query batch against all E entities are computed on the GPU:
+  * DistMult / ComplEx: S = Q . E^T on the fp32 matrix cores (kge_eval_query + kge_gemm_nt);
+  * every other score function: the fused VALU scorer with candidate ids 0..E-1 (row stride 0).
+Ranks are exact integers from kge_rank_filtered: rank = 1 + #(unfiltered e != truth with
+s_e > s_truth). Ties count in the positive's favour; upstream's unstable argsort leaves them
+arbitrary, which no test here exercises (continuous random scores).
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+
+import numpy as np
+import torch
+
+from . import ops
+from . import _lib
+from ._lib import FN_IDS, HEAD_BATCH, TAIL_BATCH, check
+
+MFMA_FNS = ("DistMult", "ComplEx")
+
+
+def build_filter(queries: np.ndarray, mode: str, all_true_triples) -> tuple[np.ndarray, np.ndarray]:
+    """CSR (ptr [M+1], ids) of the entities upstream's filter pushes below the positive:
+    head-batch (h, r, t): every h' != h with (h', r, t) true; tail-batch: every t' != t with
+    (h, r, t') true. Ids are distinct and sorted within a row."""
+    by_rt, by_hr = defaultdict(set), defaultdict(set)
+    for h, r, t in all_true_triples:
+        by_rt[(int(r), int(t))].add(int(h))
+        by_hr[(int(h), int(r))].add(int(t))
+    ptr = np.zeros(len(queries) + 1, dtype=np.int64)
+    rows = []
+    for i, (h, r, t) in enumerate(np.asarray(queries, dtype=np.int64)):
+        if mode == "head-batch":
+            s = by_rt.get((int(r), int(t)), set()) - {int(h)}
+        else:
+            s = by_hr.get((int(h), int(r)), set()) - {int(t)}
+        ids = np.array(sorted(s), dtype=np.int64)
+        rows.append(ids)
+        ptr[i + 1] = ptr[i] + len(ids)
+    ids = np.concatenate(rows) if rows else np.zeros(0, dtype=np.int64)
+    return ptr, ids
+
+
+def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor | None = None) -> torch.Tensor:
+    """[B, E] scores of every entity as the candidate (head-batch or tail-batch)."""
+    m = ops.mode_id(mode)
+    ent, rel = model.entity_embedding.detach(), model.relation_embedding.detach()
+    B, E = positive_sample.shape[0], ent.shape[0]
+    dev = ent.device
+    if out is None:
+        out = torch.empty((B, E), dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    if model.model_name in MFMA_FNS:
+        K = ent.shape[1]
+        Q = torch.empty((B, K), dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        check(lib.kge_eval_query(FN_IDS[model.model_name], m, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(),
+                                 rel.shape[0], rel.stride(0), positive_sample.data_ptr(), B, model._D, Q.data_ptr(),
+                                 Q.stride(0), st), "kge_eval_query")
+        check(lib.kge_gemm_nt(Q.data_ptr(), Q.stride(0), ent.data_ptr(), ent.stride(0), out.data_ptr(), out.stride(0),
+                              B, E, K, st), "kge_gemm_nt")
+        return out
+    cand = torch.arange(E, device=dev, dtype=torch.int64).unsqueeze(0).expand(B, E)  # row stride 0
+    modulus = float(model.modulus.reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0
+    return ops.score_indexed_raw(FN_IDS[model.model_name], m, ent, rel, model._rel_off, positive_sample, cand,
+                                 model._D, model._gamma_f, model._range_f, modulus, out=out)
+
+
+def rank_filtered(scores: torch.Tensor, truth: torch.Tensor, filter_ptr: torch.Tensor | None = None,
+                  filter_ids: torch.Tensor | None = None) -> torch.Tensor:
+    M, N = scores.shape
+    ranks = torch.empty(M, dtype=torch.int64, device=scores.device)
+    rc = _lib.load().kge_rank_filtered(scores.data_ptr(), M, N, scores.stride(0), truth.data_ptr(),
+                                       None if filter_ptr is None else filter_ptr.data_ptr(),
+                                       None if filter_ids is None else filter_ids.data_ptr(), ranks.data_ptr(),
+                                       torch.cuda.current_stream(scores.device).cuda_stream)
+    check(rc, "kge_rank_filtered")
+    return ranks
+
+
+def metrics_from_ranks(ranks: np.ndarray) -> dict:
+    r = np.asarray(ranks, dtype=np.float64)
+    return {"MRR": float(np.mean(1.0 / r)), "MR": float(np.mean(r)), "HITS@1": float(np.mean(r <= 1.0)),
+            "HITS@3": float(np.mean(r <= 3.0)), "HITS@10": float(np.mean(r <= 10.0))}
+
+
+def test_step(model, test_triples, all_true_triples, args=None, batch_size=None):
+    """Upstream `KGEModel.test_step(model, test_triples, all_true_triples, args)`: filtered MRR,
+    MR and HITS@{1,3,10} over head-batch and tail-batch ranking of every test triple."""
+    bs = batch_size or int(getattr(args, "test_batch_size", 1024) or 1024)
+    dev = model.entity_embedding.device
+    triples = np.asarray(test_triples, dtype=np.int64).reshape(-1, 3)
+    all_ranks = []
+    with torch.no_grad():
+        for mode in ("head-batch", "tail-batch"):
+            col = 0 if mode == "head-batch" else 2
+            ptr, ids = build_filter(triples, mode, all_true_triples)
+            for s in range(0, len(triples), bs):
+                q = triples[s:s + bs]
+                pos = torch.from_numpy(q).to(dev)
+                S = score_all(model, pos, mode)
+                p = ptr[s:s + len(q) + 1]
+                fptr = torch.from_numpy(p - p[0]).to(dev)
+                fids = torch.from_numpy(ids[p[0]:p[-1]]).to(dev)
+                all_ranks.append(rank_filtered(S, pos[:, col].contiguous(), fptr, fids).cpu().numpy())
+    return metrics_from_ranks(np.concatenate(all_ranks))
+
+
+__all__ = ["build_filter", "score_all", "rank_filtered", "metrics_from_ranks", "test_step", "HEAD_BATCH",
+           "TAIL_BATCH"]

@@ -140,6 +140,32 @@ int kge_gather_rows(const float* table, int64_t rows, int64_t ld, int64_t lo,
                     float* out, int64_t out_ld, void* stream);
 
 /*
+ * Link-prediction evaluation against all entities (upstream KGEModel.test_step; BASELINE config C5).
+ *
+ * kge_eval_query: the query operand of the all-entity contraction for DistMult / ComplEx:
+ *   Q[b] = h*r (tail-batch) or r*t (head-batch); ComplEx: [re_q | im_q] (width 2D). Then
+ *   score(b, e) = Q[b] . E[e] for every entity e.
+ * kge_gemm_nt: C[M,N] = A[M,K] . B[N,K]^T in fp32 on the matrix cores (v_mfma_f32_32x32x2_f32);
+ *   K, lda, ldb multiples of 4; A, B 16-byte aligned.
+ * kge_rank_filtered: ranks[q] = 1 + #{e != truth[q] : S[q,e] > S[q,truth[q]]}
+ *                               - #{f in filter[q], f != truth[q] : S[q,f] > S[q,truth[q]]}
+ *   filter[q] = filter_ids[filter_ptr[q] .. filter_ptr[q+1]) (CSR, distinct ids; NULL = no filter):
+ *   the entities upstream's filter_bias pushes below the positive. Integer result, exact.
+ * Any score function can also score all entities through kge_score_indexed with neg = [0..E)
+ * and neg_ld = 0.
+ */
+int kge_eval_query(int fn, int mode,
+                   const float* ent, int64_t nentity, int64_t ent_ld,
+                   const float* rel, int64_t nrelation, int64_t rel_ld,
+                   const int64_t* pos, int64_t B, int64_t D,
+                   float* Q, int64_t ldq, void* stream);
+int kge_gemm_nt(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                int64_t M, int64_t N, int64_t K, void* stream);
+int kge_rank_filtered(const float* scores, int64_t M, int64_t N, int64_t ld, const int64_t* truth,
+                      const int64_t* filter_ptr, const int64_t* filter_ids, int64_t* ranks,
+                      void* stream);
+
+/*
  * Score pre-gathered rows: the model_func plugin surface itself,
  * `model_func[name](head, relation, tail, mode) -> [B, 1|N]` (model.py:109-112,207).
  *   head [B, Nh, *] rows (row stride head_ld), Nh = N for KGE_HEAD_BATCH else 1

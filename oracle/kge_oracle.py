@@ -295,3 +295,30 @@ def lrfn(epoch, num_replicas=1):
     if float(epoch) < LR_RAMPUP_EPOCHS + LR_SUSTAIN_EPOCHS:
         return LR_MAX
     return (LR_MAX - LR_MIN) * LR_EXP_DECAY ** (float(epoch) - LR_RAMPUP_EPOCHS - LR_SUSTAIN_EPOCHS) + LR_MIN
+
+
+# ------------------------------------------------------------------------------------------------
+# link-prediction evaluation (upstream KGEModel.test_step + TestDataset, restated)
+# ------------------------------------------------------------------------------------------------
+def eval_ranks(name, ent, rel, pos, mode, all_true, gamma, embedding_range=None, modulus=None):
+    """Upstream TestDataset/test_step: for each (h, r, t) the candidates are all entities; a
+    candidate that forms another true triple is replaced by the positive with filter_bias -1
+    (`tmp[rand] = (-1, head)`, `tmp[head] = (0, head)`); scores + bias are argsorted descending and
+    the rank is 1 + the position of the positive's slot. Returns int64 ranks [B]."""
+    E = ent.shape[0]
+    true = set(map(tuple, all_true))
+    ranks = []
+    for h, r, t in pos.tolist():
+        neg, bias = [], []
+        for e in range(E):
+            trip = (e, r, t) if mode == "head-batch" else (h, r, e)
+            filtered = trip in true and e != (h if mode == "head-batch" else t)
+            neg.append((h if mode == "head-batch" else t) if filtered else e)
+            bias.append(-1.0 if filtered else 0.0)
+        p = torch.tensor([[h, r, t]], dtype=torch.int64)
+        n = torch.tensor([neg], dtype=torch.int64)
+        s = score(name, ent, rel, p, n, mode, gamma, embedding_range, modulus)[0] + torch.tensor(bias, dtype=ent.dtype)
+        order = torch.argsort(s, descending=True)
+        slot = h if mode == "head-batch" else t
+        ranks.append(int((order == slot).nonzero()[0, 0]) + 1)
+    return torch.tensor(ranks, dtype=torch.int64)

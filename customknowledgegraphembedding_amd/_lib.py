@@ -78,6 +78,13 @@ SIGNATURES = {
     "kge_log_sigmoid_bwd": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p]),
     "kge_adam_update": (
         _c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_i, _c_p]),
+    "kge_step_backward_workspace_size": (_c_i64, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64]),
+    "kge_step_backward": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p,
+         _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p],
+    ),
     "kge_score_bwd_workspace_size": (_c_i64, [_c_i, _c_i, _c_i64, _c_i64, _c_i64]),
     "kge_score_indexed_bwd": (
         _c_i,

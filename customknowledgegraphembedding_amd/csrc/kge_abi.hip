@@ -167,6 +167,116 @@ __global__ __launch_bounds__(kBlock) void gather_owned_kernel(const float* __res
 }
 
 // ---------------------------------------------------------------------------------------------
+// Gradient events of the deterministic backward, bucketed by entity (counting sort).
+//   code in [0, BN)            negative candidate (b = code / N, n = code % N)  key neg[b, n]
+//   code in [BN, BN+B)         positive candidate of row b (single mode)        key pos[b, 2]
+//   code in [BN+B, BN+2B)      query-entity gradient of the negative call's b   key pos[b, 2|0]
+//   code in [BN+2B, BN+3B)     query-entity (h) gradient of the positive call   key pos[b, 0]
+// ---------------------------------------------------------------------------------------------
+struct EvArgs {
+    const int64_t* pos;
+    const int64_t* neg;
+    int64_t neg_ld, B, N, E;
+    int qcol;  // query-entity column of the negative call: 2 (head-batch) or 0
+    int total;
+};
+
+__device__ __forceinline__ int64_t ev_key(const EvArgs& a, int code) {
+    const int64_t BN = a.B * a.N;
+    if (code < BN) return a.neg[(code / a.N) * a.neg_ld + code % a.N];
+    int64_t b = code - BN;
+    if (b < a.B) return a.pos[b * 3 + 2];
+    b -= a.B;
+    if (b < a.B) return a.pos[b * 3 + a.qcol];
+    b -= a.B;
+    return a.pos[b * 3 + 0];
+}
+
+__global__ __launch_bounds__(kBlock) void ev_count_kernel(EvArgs a, int* __restrict__ count) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.total) return;
+    const int64_t k = ev_key(a, i);
+    if (k >= 0 && k < a.E) atomicAdd(&count[k], 1);
+}
+
+// exclusive scan of count[0..E) -> off[0..E], cursor = off; one block of 1024 threads
+__global__ __launch_bounds__(1024) void ev_scan_kernel(const int* __restrict__ count, int64_t E, int* __restrict__ off,
+                                                       int* __restrict__ cursor) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (E + 1023) / 1024;
+    const int64_t lo = t * per, hi = min(E, lo + per);
+    int s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += count[i];
+    part[t] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = part[t] - s;
+    for (int64_t i = lo; i < hi; ++i) {
+        off[i] = run;
+        cursor[i] = run;
+        run += count[i];
+    }
+    if (t == 1023) off[E] = part[1023];
+}
+
+__global__ __launch_bounds__(kBlock) void ev_scatter_kernel(EvArgs a, int* __restrict__ cursor, int* __restrict__ code) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.total) return;
+    const int64_t k = ev_key(a, i);
+    if (k >= 0 && k < a.E) code[atomicAdd(&cursor[k], 1)] = i;
+}
+
+// relation gradient: one wave per relation row; the slots that use it are found 64 at a time by a
+// ballot and added in slot order (deterministic). Lane l owns columns l, l+64, ... (<= 4096).
+constexpr int kRelCols = 64;  // columns per lane -> rel_w <= 4096
+__global__ __launch_bounds__(kBlock) void bwd_rel_kernel(const int64_t* __restrict__ pos, int64_t B, int64_t R,
+                                                         const float* __restrict__ qg_rel, int64_t rel_w,
+                                                         int64_t rel_off, float* __restrict__ d_rel, int64_t rel_ld,
+                                                         int64_t rel_dim, const float* __restrict__ dmod_part,
+                                                         float* __restrict__ d_mod) {
+    const int64_t rho = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d_mod && dmod_part) {
+        float m = 0.f;
+        for (int64_t s = 0; s < 2 * B; ++s) m += dmod_part[s];
+        *d_mod = m;
+    }
+    if (rho >= R) return;
+    float acc[kRelCols];
+#pragma unroll
+    for (int j = 0; j < kRelCols; ++j) acc[j] = 0.f;
+    for (int64_t s0 = 0; s0 < 2 * B; s0 += kWave) {
+        const int64_t s = s0 + lane;
+        const bool hit = s < 2 * B && pos[(s % B) * 3 + 1] == rho;  // slot s: row s % B of either call
+        unsigned long long m = __ballot(hit);
+        while (m) {
+            const int bit = __builtin_ctzll(m);
+            m &= m - 1;
+            const float* row = qg_rel + (s0 + bit) * rel_w;
+#pragma unroll
+            for (int j = 0; j < kRelCols; ++j) {
+                const int64_t c = lane + (int64_t)j * kWave;
+                if (c < rel_w) acc[j] += row[c];
+            }
+        }
+    }
+    float* out = d_rel + rho * rel_ld;
+    for (int64_t c = lane; c < rel_dim; c += kWave)
+        if (c < rel_off || c >= rel_off + rel_w) out[c] = 0.f;  // parts no score function reads
+#pragma unroll
+    for (int j = 0; j < kRelCols; ++j) {
+        const int64_t c = lane + (int64_t)j * kWave;
+        if (c < rel_w) out[rel_off + c] = acc[j];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // host helpers
 // ---------------------------------------------------------------------------------------------
 thread_local std::string g_last_error;
@@ -260,6 +370,10 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         p.cpw = 1;
         p.wpr = 1;
         waves = p.B;
+    } else if (kind == KIND_BWD_ROWS) {
+        waves = p.B * kWavesPerBlock;  // one block per slot
+    } else if (kind == KIND_BWD_ENT) {
+        waves = p.c_rows;  // one wave per entity row
     } else {
         p.cpw = pick_cpw(p.B, p.N);
         p.wpr = (int)((p.N + p.cpw - 1) / p.cpw);
@@ -268,6 +382,7 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > INT32_MAX) return fail(KGE_EINVAL, "problem too large for one launch");
     const bool ch = (kind != KIND_FINISH) && mode == KGE_HEAD_BATCH;
+    if ((kind == KIND_BWD_ROWS || kind == KIND_BWD_ENT) && G > kMaxG) return fail(KGE_ENOTSUP, "dimension too large");
     rc = dispatch(fn, p, kind, (hipStream_t)stream, (int)blocks, ch, V, G);
     if (rc) return fail(rc, "no kernel for this (function, width) combination");
     return check_launch(kind == KIND_BWD ? "kge score backward launch"
@@ -615,6 +730,42 @@ int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq
     return check_launch("kge_adam_update");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Deterministic backward of the fused train step
+// ---------------------------------------------------------------------------------------------
+struct StepWs {
+    float *d_ns, *d_ps, *qbuf, *qg_ent, *qg_rel, *dmod;
+    int *count, *off, *cursor, *code;
+    int64_t bytes;
+};
+
+static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+static StepWs step_ws_layout(char* base, int64_t E, int64_t B, int64_t N, int64_t D, int64_t ent_w, int64_t rel_w) {
+    StepWs w;
+    int64_t o = 0;
+    auto take = [&](int64_t bytes) {
+        char* p = base ? base + o : nullptr;
+        o += align256(bytes);
+        return p;
+    };
+    w.d_ns = (float*)take(B * N * 4);
+    w.d_ps = (float*)take(B * 4);
+    w.qbuf = (float*)take(2 * B * 3 * D * 4);
+    w.qg_ent = (float*)take(2 * B * ent_w * 4);
+    w.qg_rel = (float*)take(2 * B * rel_w * 4);
+    w.dmod = (float*)take(2 * B * 4);
+    w.count = (int*)take(E * 4);
+    w.off = (int*)take((E + 1) * 4);
+    w.cursor = (int*)take(E * 4);
+    w.code = (int*)take((B * N + 3 * B) * 4);
+    w.bytes = o;
+    return w;
+}
+
+static int64_t ent_width(int fn, int64_t D) { return is_split(fn) ? 2 * D : D; }
+static int64_t rel_width(int fn, int64_t D) { return fn == KGE_COMPLEX ? 2 * D : D; }
+
 int64_t kge_score_bwd_workspace_size(int fn, int mode, int64_t B, int64_t N, int64_t D) {
     (void)fn;
     (void)mode;
@@ -647,6 +798,116 @@ int kge_score_indexed_bwd(int fn, int mode, const float* ent, int64_t nentity, i
     p.d_rel = d_rel;
     p.d_modulus = d_modulus;
     return run_score(fn, mode, p, KIND_BWD, stream);
+}
+
+int64_t kge_step_backward_workspace_size(int fn, int64_t nentity, int64_t B, int64_t N, int64_t D) {
+    if (fn < KGE_TRANSE || fn > KGE_PROTATE || nentity < 0 || B < 0 || N < 0 || D <= 0) return -1;
+    return step_ws_layout(nullptr, nentity, B, N, D, ent_width(fn, D), rel_width(fn, D)).bytes;
+}
+
+int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                      int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                      int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
+                      float temperature, int adversarial, int detach, const float* neg_scores, int64_t ns_ld,
+                      const float* pos_scores, const float* d_out_neg, const float* d_out_pos, float* d_ent,
+                      float* d_rel, float* d_modulus, void* workspace, int64_t workspace_bytes, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_backward needs a negative mode (0 or 1)");
+    if (B < 0 || N <= 0 || D <= 0 || nentity < 0 || nrelation < 0) return fail(KGE_EINVAL, "bad shape");
+    if (!ent || !rel || !pos || !neg || !neg_scores || !pos_scores || !d_out_neg || !d_out_pos || !d_ent || !d_rel)
+        return fail(KGE_EINVAL, "null pointer");
+    if (B * N + 3 * B >= (int64_t)INT32_MAX || nentity >= (int64_t)INT32_MAX)
+        return fail(KGE_EINVAL, "too many gradient events for 32-bit codes");
+    if (rel_width(fn, D) > (int64_t)kRelCols * kWave) return fail(KGE_ENOTSUP, "relation part wider than 4096");
+    const int64_t ent_w = ent_width(fn, D), rel_w = rel_width(fn, D);
+    const int64_t rel_dim = rel_ld;  // rows are written over their full stride (padding included)
+    StepWs w = step_ws_layout((char*)workspace, nentity, B, N, D, ent_w, rel_w);
+    if (!workspace || workspace_bytes < w.bytes) return fail(KGE_EINVAL, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    if (B == 0) {
+        if (hipMemsetAsync(d_ent, 0, (size_t)(nentity * ent_ld * 4), st) != hipSuccess ||
+            hipMemsetAsync(d_rel, 0, (size_t)(nrelation * rel_ld * 4), st) != hipSuccess)
+            return check_launch("kge_step_backward memset");
+        if (d_modulus && hipMemsetAsync(d_modulus, 0, 4, st) != hipSuccess) return check_launch("memset");
+        return ok();
+    }
+    // 1. loss -> score gradients
+    rc = kge_neg_reduce_bwd(neg_scores, B, N, ns_ld, temperature, adversarial, detach, d_out_neg, w.d_ns, N, stream);
+    if (rc) return rc;
+    rc = kge_log_sigmoid_bwd(pos_scores, d_out_pos, B, w.d_ps, stream);
+    if (rc) return rc;
+    // 2. phase 1: per-slot query gradients (negative call, then positive call)
+    ScoreParams p;
+    fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D, gamma,
+                 emb_range, modulus);
+    p.d_scores = w.d_ns;
+    p.d_ld = N;
+    p.qbuf = w.qbuf;
+    p.qg_ent = w.qg_ent;
+    p.qg_rel = w.qg_rel;
+    p.dmod_part = w.dmod;
+    p.ent_w = ent_w;
+    p.rel_w = rel_w;
+    p.slot0 = 0;
+    rc = run_score(fn, mode, p, KIND_BWD_ROWS, stream);
+    if (rc) return rc;
+    ScoreParams pp;
+    fill_indexed(pp, fn, KGE_SINGLE, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, nullptr, 0, B, 1, D,
+                 gamma, emb_range, modulus);
+    pp.d_scores = w.d_ps;
+    pp.d_ld = 1;
+    pp.qbuf = w.qbuf;
+    pp.qg_ent = w.qg_ent;
+    pp.qg_rel = w.qg_rel;
+    pp.dmod_part = w.dmod;
+    pp.ent_w = ent_w;
+    pp.rel_w = rel_w;
+    pp.slot0 = B;
+    rc = run_score(fn, KGE_SINGLE, pp, KIND_BWD_ROWS, stream);
+    if (rc) return rc;
+    // 3. bucket the gradient events by entity
+    EvArgs a;
+    a.pos = pos;
+    a.neg = neg;
+    a.neg_ld = neg_ld;
+    a.B = B;
+    a.N = N;
+    a.E = nentity;
+    a.qcol = mode == KGE_HEAD_BATCH ? 2 : 0;
+    a.total = (int)(B * N + 3 * B);
+    if (hipMemsetAsync(w.count, 0, (size_t)(nentity * 4), st) != hipSuccess) return check_launch("memset");
+    const unsigned eb = (unsigned)((a.total + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
+    hipLaunchKernelGGL(ev_scan_kernel, dim3(1), dim3(1024), 0, st, w.count, nentity, w.off, w.cursor);
+    hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
+    rc = check_launch("kge_step_backward events");
+    if (rc) return rc;
+    // 4. phase 2: one wave per entity row, events in code order -> every row of d_ent written
+    ScoreParams q;
+    fill_indexed(q, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D, gamma,
+                 emb_range, modulus);
+    q.qbuf = w.qbuf;
+    q.qg_ent = w.qg_ent;
+    q.ev_off = w.off;
+    q.ev_code = w.code;
+    q.d_ns = w.d_ns;
+    q.d_ps = w.d_ps;
+    q.Bn = B;
+    q.Nn = N;
+    q.ent_w = ent_w;
+    q.d_out_ent = d_ent;
+    if (nentity > 0) {
+        rc = run_score(fn, mode, q, KIND_BWD_ENT, stream);
+        if (rc) return rc;
+    }
+    // 5. relation rows (slot order) and the pRotatE modulus
+    if (nrelation > 0 || d_modulus) {
+        const int64_t rb = std::max<int64_t>(1, (nrelation + kWavesPerBlock - 1) / kWavesPerBlock);
+        hipLaunchKernelGGL(bwd_rel_kernel, dim3((unsigned)rb), dim3(kBlock), 0, st, pos, B, nrelation, w.qg_rel, rel_w,
+                           rel_off, d_rel, rel_ld, rel_dim, w.dmod, d_modulus);
+    }
+    return check_launch("kge_step_backward");
 }
 
 }  // extern "C"

@@ -447,6 +447,223 @@ __device__ __forceinline__ void vatomic_add(float* dst, const vecf<V>& v, bool o
     for (int i = 0; i < V; ++i) unsafeAtomicAdd(dst + i, v.a[i]);
 }
 
+// Gradient of one candidate's score w.r.t. the candidate row (dca, dcb; WANT_C) and the query
+// operands (dq0..dq2 accumulated; ACC_Q), given dL/dscore = g. Also accumulates the pRotatE
+// modulus gradient. Every lane must call it (it reduces across the wave).
+template <int FN, bool CH, int V, int G, bool ACC_Q, bool WANT_C>
+__device__ __forceinline__ void cand_grad(const Cand<FN, V, G>& c, const Query<FN, CH, V, G>& q, float g, int lane,
+                                          int DV, const ScoreParams& p, vecf<V> (&dq0)[G], vecf<V> (&dq1)[G],
+                                          vecf<V> (&dq2)[G], vecf<V> (&dca)[G], vecf<V> (&dcb)[G], float& dmod) {
+    if constexpr (FN == KGE_INTERHT) {
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                sa += c.ca[k].a[i] * c.ca[k].a[i];
+                sb += c.cb[k].a[i] * c.cb[k].a[i];
+            }
+        const float ia = rsqrt_f(wave_sum(sa)), ib = rsqrt_f(wave_sum(sb));
+        float dota = 0.f, dotb = 0.f;
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const float ah = c.ca[k].a[i] * ia;
+                const float bn = c.cb[k].a[i] * ib;
+                const float bh = bn + 1.f;
+                const float q0 = q.q0[k].a[i], q1 = q.q1[k].a[i], q2 = q.q2[k].a[i];
+                const bool in = (lane + k * kWave) < DV;
+                float dah, dbn;
+                if (CH) {  // x = a_head * b_tail - a_tail * b_head + re_mid, candidate = head
+                    const float x = ah * q1 - q0 * bh + q2;
+                    const float Gx = in ? -g * sgnf(x) : 0.f;
+                    dah = Gx * q1;
+                    dbn = -Gx * q0;
+                    if (ACC_Q) {
+                        dq1[k].a[i] += Gx * ah;
+                        dq0[k].a[i] += -Gx * bh;
+                        dq2[k].a[i] += Gx;
+                    }
+                } else {
+                    const float x = q0 * bh - ah * q1 + q2;
+                    const float Gx = in ? -g * sgnf(x) : 0.f;
+                    dah = -Gx * q1;
+                    dbn = Gx * q0;
+                    if (ACC_Q) {
+                        dq0[k].a[i] += Gx * bh;
+                        dq1[k].a[i] += -Gx * ah;
+                        dq2[k].a[i] += Gx;
+                    }
+                }
+                if (WANT_C) {
+                    dca[k].a[i] = dah;
+                    dcb[k].a[i] = dbn;
+                    dota += ah * dah;
+                    dotb += bn * dbn;
+                }
+            }
+        if constexpr (WANT_C) {
+            dota = wave_sum(dota);
+            dotb = wave_sum(dotb);
+            // d(x/n) = (dy - y <y, dy>) / n
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    const float ah = c.ca[k].a[i] * ia;
+                    const float bn = c.cb[k].a[i] * ib;
+                    dca[k].a[i] = (dca[k].a[i] - ah * dota) * ia;
+                    dcb[k].a[i] = (dcb[k].a[i] - bn * dotb) * ib;
+                }
+        }
+    } else {
+        float ysum = 0.f;
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const float x = c.ca[k].a[i];
+                const bool in = (lane + k * kWave) < DV;
+                float da = 0.f, db = 0.f;
+                if constexpr (FN == KGE_TRANSE) {
+                    const float r = CH ? (x + q.q0[k].a[i]) : (q.q0[k].a[i] - x);
+                    const float Gx = -g * sgnf(r);  // dL/d(residual)
+                    da = CH ? Gx : -Gx;
+                    if (ACC_Q) dq0[k].a[i] += Gx;
+                } else if constexpr (FN == KGE_DISTMULT) {
+                    da = g * q.q0[k].a[i];
+                    if (ACC_Q) dq0[k].a[i] += g * x;
+                } else if constexpr (FN == KGE_COMPLEX) {
+                    const float y = c.cb[k].a[i];
+                    da = g * q.q0[k].a[i];
+                    db = g * q.q1[k].a[i];
+                    if (ACC_Q) {
+                        dq0[k].a[i] += g * x;
+                        dq1[k].a[i] += g * y;
+                    }
+                } else if constexpr (FN == KGE_ROTATE) {
+                    const float y = c.cb[k].a[i];
+                    const float xr = q.q0[k].a[i] - x, xi = q.q1[k].a[i] - y;
+                    const float m = sqrtf(xr * xr + xi * xi);
+                    const float fr = (m > 0.f) ? xr / m : 0.f, fi = (m > 0.f) ? xi / m : 0.f;
+                    da = g * fr;
+                    db = g * fi;
+                    if (ACC_Q) {
+                        dq0[k].a[i] += -g * fr;
+                        dq1[k].a[i] += -g * fi;
+                    }
+                } else if constexpr (FN == KGE_PROTATE) {
+                    const float pc = x / p.phase_div;
+                    const float z = CH ? (pc + q.q0[k].a[i]) : (q.q0[k].a[i] - pc);
+                    const float sz = sinf(z);
+                    const float Gx = in ? -g * p.modulus * sgnf(sz) * cosf(z) : 0.f;
+                    da = (CH ? Gx : -Gx) / p.phase_div;
+                    if (ACC_Q) dq0[k].a[i] += Gx;
+                    ysum += in ? fabsf(sz) : 0.f;
+                }
+                if (WANT_C) {
+                    dca[k].a[i] = in ? da : 0.f;
+                    dcb[k].a[i] = in ? db : 0.f;
+                }
+            }
+        if constexpr (FN == KGE_PROTATE) {
+            if (ACC_Q) dmod += -g * wave_sum(ysum);
+        }
+    }
+}
+
+// Query-side chain rule: accumulated query-operand grads (dq0..dq2) -> gradient of the raw query
+// entity row (gea: first half / whole row, geb: second half) and of the used relation part (gra,
+// grb). qrow / rrow are the raw rows (relation row already offset by r_off).
+template <int FN, bool CH, int V, int G>
+__device__ __forceinline__ void query_chain(const Query<FN, CH, V, G>& q, const vecf<V> (&dq0)[G],
+                                            const vecf<V> (&dq1)[G], const vecf<V> (&dq2)[G], const float* qrow,
+                                            bool qok, const float* rrow, bool rok, int lane, int D,
+                                            const ScoreParams& p, vecf<V> (&gea)[G], vecf<V> (&geb)[G],
+                                            vecf<V> (&gra)[G], vecf<V> (&grb)[G]) {
+    const int DV = D / V;
+    float dna = 0.f, dnb = 0.f;
+    if constexpr (FN == KGE_INTERHT) {
+        float da = 0.f, db = 0.f;
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const bool in = (lane + k * kWave) < DV;
+                da += q.q0[k].a[i] * dq0[k].a[i];
+                db += (in ? q.q1[k].a[i] - 1.f : 0.f) * dq1[k].a[i];
+            }
+        dna = wave_sum(da);
+        dnb = wave_sum(db);
+    }
+    const uint32_t qb = qok ? (uint32_t)D * 4u : 0u, rbytes = rok ? (uint32_t)D * 4u : 0u;
+    const rsrc_t sqa = make_rsrc(qrow, qb), sqb = make_rsrc(qrow + D, is_split(FN) ? qb : 0u);
+    const rsrc_t sra = make_rsrc(rrow, rbytes), srb = make_rsrc(rrow + D, rel_split(FN) ? rbytes : 0u);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const bool in = (lane + k * kWave) < DV;
+        const vecf<V> ea = bload<V>(sqa, goff<V>(lane, k)), eb = bload<V>(sqb, goff<V>(lane, k));
+        const vecf<V> ra = bload<V>(sra, goff<V>(lane, k)), rb = bload<V>(srb, goff<V>(lane, k));
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const float x = ea.a[i], y = eb.a[i], r = ra.a[i], s = rb.a[i];
+            const float d0 = dq0[k].a[i], d1 = dq1[k].a[i], d2 = dq2[k].a[i];
+            float o_ea = 0.f, o_eb = 0.f, o_ra = 0.f, o_rb = 0.f;
+            if constexpr (FN == KGE_TRANSE) {
+                o_ea = CH ? -d0 : d0;
+                o_ra = d0;
+            } else if constexpr (FN == KGE_DISTMULT) {
+                o_ea = d0 * r;
+                o_ra = d0 * x;
+            } else if constexpr (FN == KGE_COMPLEX) {
+                if (!CH) {
+                    o_ea = d0 * r + d1 * s;
+                    o_eb = -d0 * s + d1 * r;
+                    o_ra = d0 * x + d1 * y;
+                    o_rb = -d0 * y + d1 * x;
+                } else {
+                    o_ea = d0 * r - d1 * s;
+                    o_eb = d0 * s + d1 * r;
+                    o_ra = d0 * x + d1 * y;
+                    o_rb = d0 * y - d1 * x;
+                }
+            } else if constexpr (FN == KGE_ROTATE) {
+                const float ph = r / p.phase_div;
+                const float c = cosf(ph), sn = sinf(ph);
+                const float Q0 = q.q0[k].a[i], Q1 = q.q1[k].a[i];
+                float dth;
+                if (!CH) {
+                    o_ea = d0 * c + d1 * sn;
+                    o_eb = -d0 * sn + d1 * c;
+                    dth = -d0 * Q1 + d1 * Q0;
+                } else {
+                    o_ea = d0 * c - d1 * sn;
+                    o_eb = d0 * sn + d1 * c;
+                    dth = d0 * Q1 - d1 * Q0;
+                }
+                o_ra = dth / p.phase_div;
+            } else if constexpr (FN == KGE_PROTATE) {
+                o_ea = (CH ? -d0 : d0) / p.phase_div;
+                o_ra = d0 / p.phase_div;
+            } else if constexpr (FN == KGE_INTERHT) {
+                const float Q0 = q.q0[k].a[i];
+                const float bn = in ? q.q1[k].a[i] - 1.f : 0.f;
+                o_ea = (d0 - Q0 * dna) * q.na_inv;
+                o_eb = (d1 - bn * dnb) * q.nb_inv;
+                o_ra = d2;
+            }
+            gea[k].a[i] = in ? o_ea : 0.f;
+            geb[k].a[i] = in ? o_eb : 0.f;
+            gra[k].a[i] = in ? o_ra : 0.f;
+            grb[k].a[i] = in ? o_rb : 0.f;
+        }
+    }
+}
+
+// Atomic-scatter backward (used by kge_score_indexed_bwd / kge_score_dense_bwd): recompute each
+// candidate's terms, scatter its row gradient with fp32 atomics, accumulate the query-side
+// gradient over the wave's run and add it once per wave.
 template <int FN, bool CH, int V, int G>
 __global__ __launch_bounds__(kBlock) void score_bwd_kernel(ScoreParams p) {
     WaveTask t;
@@ -481,108 +698,8 @@ __global__ __launch_bounds__(kBlock) void score_bwd_kernel(ScoreParams p) {
         Cand<FN, V, G> c;
         c.load(crow, ok, D, lane);
         vecf<V> dca[G], dcb[G];
-        if constexpr (FN == KGE_INTERHT) {
-            float sa = 0.f, sb = 0.f;
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-#pragma unroll
-                for (int i = 0; i < V; ++i) {
-                    sa += c.ca[k].a[i] * c.ca[k].a[i];
-                    sb += c.cb[k].a[i] * c.cb[k].a[i];
-                }
-            const float ia = rsqrt_f(wave_sum(sa)), ib = rsqrt_f(wave_sum(sb));
-            float dota = 0.f, dotb = 0.f;
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-#pragma unroll
-                for (int i = 0; i < V; ++i) {
-                    const float ah = c.ca[k].a[i] * ia;
-                    const float bn = c.cb[k].a[i] * ib;
-                    const float bh = bn + 1.f;
-                    const float q0 = q.q0[k].a[i], q1 = q.q1[k].a[i], q2 = q.q2[k].a[i];
-                    float x, dah, dbn;
-                    const bool in = (lane + k * kWave) < DV;
-                    if (CH) {
-                        x = ah * q1 - q0 * bh + q2;
-                        const float Gx = in ? -g * sgnf(x) : 0.f;
-                        dah = Gx * q1;
-                        dbn = -Gx * q0;
-                        dq1[k].a[i] += Gx * ah;
-                        dq0[k].a[i] += -Gx * bh;
-                        dq2[k].a[i] += Gx;
-                    } else {
-                        x = q0 * bh - ah * q1 + q2;
-                        const float Gx = in ? -g * sgnf(x) : 0.f;
-                        dah = -Gx * q1;
-                        dbn = Gx * q0;
-                        dq0[k].a[i] += Gx * bh;
-                        dq1[k].a[i] += -Gx * ah;
-                        dq2[k].a[i] += Gx;
-                    }
-                    dca[k].a[i] = dah;
-                    dcb[k].a[i] = dbn;
-                    dota += ah * dah;
-                    dotb += bn * dbn;
-                }
-            dota = wave_sum(dota);
-            dotb = wave_sum(dotb);
-            // d(x/n) = (dy - y <y, dy>) / n
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-#pragma unroll
-                for (int i = 0; i < V; ++i) {
-                    const float ah = c.ca[k].a[i] * ia;
-                    const float bn = c.cb[k].a[i] * ib;
-                    dca[k].a[i] = (dca[k].a[i] - ah * dota) * ia;
-                    dcb[k].a[i] = (dcb[k].a[i] - bn * dotb) * ib;
-                }
-        } else {
-            float ysum = 0.f;
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-#pragma unroll
-                for (int i = 0; i < V; ++i) {
-                    const float x = c.ca[k].a[i];
-                    const bool in = (lane + k * kWave) < DV;
-                    float da = 0.f, db = 0.f;
-                    if constexpr (FN == KGE_TRANSE) {
-                        const float r = CH ? (x + q.q0[k].a[i]) : (q.q0[k].a[i] - x);
-                        const float Gx = -g * sgnf(r);  // dL/d(residual)
-                        da = CH ? Gx : -Gx;
-                        dq0[k].a[i] += Gx;
-                    } else if constexpr (FN == KGE_DISTMULT) {
-                        da = g * q.q0[k].a[i];
-                        dq0[k].a[i] += g * x;
-                    } else if constexpr (FN == KGE_COMPLEX) {
-                        const float y = c.cb[k].a[i];
-                        da = g * q.q0[k].a[i];
-                        db = g * q.q1[k].a[i];
-                        dq0[k].a[i] += g * x;
-                        dq1[k].a[i] += g * y;
-                    } else if constexpr (FN == KGE_ROTATE) {
-                        const float y = c.cb[k].a[i];
-                        const float xr = q.q0[k].a[i] - x, xi = q.q1[k].a[i] - y;
-                        const float m = sqrtf(xr * xr + xi * xi);
-                        const float fr = (m > 0.f) ? xr / m : 0.f, fi = (m > 0.f) ? xi / m : 0.f;
-                        da = g * fr;
-                        db = g * fi;
-                        dq0[k].a[i] += -g * fr;
-                        dq1[k].a[i] += -g * fi;
-                    } else if constexpr (FN == KGE_PROTATE) {
-                        const float pc = x / p.phase_div;
-                        const float z = CH ? (pc + q.q0[k].a[i]) : (q.q0[k].a[i] - pc);
-                        const float sz = sinf(z);
-                        const float Gx = in ? -g * p.modulus * sgnf(sz) * cosf(z) : 0.f;
-                        da = (CH ? Gx : -Gx) / p.phase_div;
-                        dq0[k].a[i] += Gx;
-                        ysum += in ? fabsf(sz) : 0.f;
-                    }
-                    dca[k].a[i] = in ? da : 0.f;
-                    dcb[k].a[i] = in ? db : 0.f;
-                }
-            if constexpr (FN == KGE_PROTATE) dmod += -g * wave_sum(ysum);
-        }
-        float* drow = p.d_cent + (ok ? ci : 0) * p.c_ld;
+        cand_grad<FN, CH, V, G, true, true>(c, q, g, lane, DV, p, dq0, dq1, dq2, dca, dcb, dmod);
+        float* drow = p.d_cent + (ok ? ci - p.c_base : 0) * p.c_ld;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             const int gi = lane + k * kWave;
@@ -592,21 +709,8 @@ __global__ __launch_bounds__(kBlock) void score_bwd_kernel(ScoreParams p) {
         }
     }
 
-    // query-side chain rule -> raw query entity row and relation row
-    float dna = 0.f, dnb = 0.f;
-    if constexpr (FN == KGE_INTERHT) {
-        float da = 0.f, db = 0.f;
-#pragma unroll
-        for (int k = 0; k < G; ++k)
-#pragma unroll
-            for (int i = 0; i < V; ++i) {
-                const bool in = (lane + k * kWave) < DV;
-                da += q.q0[k].a[i] * dq0[k].a[i];
-                db += (in ? q.q1[k].a[i] - 1.f : 0.f) * dq1[k].a[i];
-            }
-        dna = wave_sum(da);
-        dnb = wave_sum(db);
-    }
+    vecf<V> gea[G], geb[G], gra[G], grb[G];
+    query_chain<FN, CH, V, G>(q, dq0, dq1, dq2, qrow, qok, rrow, rok, lane, D, p, gea, geb, gra, grb);
     float* dq_row = p.d_qent + (qok ? qi : 0) * p.q_ld;
     float* dr_row = p.d_rel + (rok ? ri : 0) * p.r_ld + p.r_off;
 #pragma unroll
@@ -614,67 +718,257 @@ __global__ __launch_bounds__(kBlock) void score_bwd_kernel(ScoreParams p) {
         const int gi = lane + k * kWave;
         const bool in = gi < DV;
         const int e = gi * V;
-        const vecf<V> ea = vload<V>(qrow + e, qok && in);
-        const vecf<V> eb = is_split(FN) ? vload<V>(qrow + D + e, qok && in) : vzero<V>();
-        const vecf<V> ra = vload<V>(rrow + e, rok && in);
-        const vecf<V> rb = rel_split(FN) ? vload<V>(rrow + D + e, rok && in) : vzero<V>();
-        vecf<V> gea = vzero<V>(), geb = vzero<V>(), gra = vzero<V>(), grb = vzero<V>();
-#pragma unroll
-        for (int i = 0; i < V; ++i) {
-            const float x = ea.a[i], y = eb.a[i], r = ra.a[i], s = rb.a[i];
-            const float d0 = dq0[k].a[i], d1 = dq1[k].a[i], d2 = dq2[k].a[i];
-            if constexpr (FN == KGE_TRANSE) {
-                gea.a[i] = CH ? -d0 : d0;
-                gra.a[i] = d0;
-            } else if constexpr (FN == KGE_DISTMULT) {
-                gea.a[i] = d0 * r;
-                gra.a[i] = d0 * x;
-            } else if constexpr (FN == KGE_COMPLEX) {
-                if (!CH) {
-                    gea.a[i] = d0 * r + d1 * s;
-                    geb.a[i] = -d0 * s + d1 * r;
-                    gra.a[i] = d0 * x + d1 * y;
-                    grb.a[i] = -d0 * y + d1 * x;
-                } else {
-                    gea.a[i] = d0 * r - d1 * s;
-                    geb.a[i] = d0 * s + d1 * r;
-                    gra.a[i] = d0 * x + d1 * y;
-                    grb.a[i] = d0 * y - d1 * x;
-                }
-            } else if constexpr (FN == KGE_ROTATE) {
-                const float ph = r / p.phase_div;
-                const float c = cosf(ph), sn = sinf(ph);
-                const float Q0 = q.q0[k].a[i], Q1 = q.q1[k].a[i];
-                float dth;
-                if (!CH) {
-                    gea.a[i] = d0 * c + d1 * sn;
-                    geb.a[i] = -d0 * sn + d1 * c;
-                    dth = -d0 * Q1 + d1 * Q0;
-                } else {
-                    gea.a[i] = d0 * c - d1 * sn;
-                    geb.a[i] = d0 * sn + d1 * c;
-                    dth = d0 * Q1 - d1 * Q0;
-                }
-                gra.a[i] = dth / p.phase_div;
-            } else if constexpr (FN == KGE_PROTATE) {
-                gea.a[i] = (CH ? -d0 : d0) / p.phase_div;
-                gra.a[i] = d0 / p.phase_div;
-            } else if constexpr (FN == KGE_INTERHT) {
-                const float Q0 = q.q0[k].a[i];
-                const float bn = in ? q.q1[k].a[i] - 1.f : 0.f;
-                gea.a[i] = (d0 - Q0 * dna) * q.na_inv;
-                geb.a[i] = (d1 - bn * dnb) * q.nb_inv;
-                gra.a[i] = d2;
-            }
-            if (!in) gea.a[i] = geb.a[i] = gra.a[i] = grb.a[i] = 0.f;
-        }
-        vatomic_add<V>(dq_row + e, gea, qok && in);
-        if constexpr (is_split(FN)) vatomic_add<V>(dq_row + D + e, geb, qok && in);
-        vatomic_add<V>(dr_row + e, gra, rok && in);
-        if constexpr (rel_split(FN)) vatomic_add<V>(dr_row + D + e, grb, rok && in);
+        vatomic_add<V>(dq_row + e, gea[k], qok && in);
+        if constexpr (is_split(FN)) vatomic_add<V>(dq_row + D + e, geb[k], qok && in);
+        vatomic_add<V>(dr_row + e, gra[k], rok && in);
+        if constexpr (rel_split(FN)) vatomic_add<V>(dr_row + D + e, grb[k], rok && in);
     }
     if constexpr (FN == KGE_PROTATE) {
         if (lane == 0 && p.d_modulus) unsafeAtomicAdd(p.d_modulus, dmod);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deterministic two-phase backward of the fused train step (kge_step_backward). No atomics on
+// floats anywhere: every sum has a fixed order, so gradients are bitwise reproducible.
+//
+// Phase 1 (bwd_rows_kernel): one block of 4 waves per batch row (a "slot"); the waves split the
+//   row's candidates, accumulate the query-side gradient in VGPRs (cand_grad, ACC_Q), combine the
+//   four partials through LDS in wave order, and wave 0 applies the query chain rule. Writes the
+//   slot's query operands (for phase 2), its query-entity row gradient and relation gradient.
+// Phase 2 (bwd_ent_kernel): one wave per entity row e. It loads row e once and walks the gradient
+//   events bucketed to e (counting sort by entity) in ascending event-code order: a candidate event
+//   (slot, dL/dscore) recomputes the candidate-row gradient against the slot's stored query; a row
+//   event adds a slot's query-entity gradient. Every row of the gradient table is written once
+//   (no memset; rows without events are written as zeros).
+// ---------------------------------------------------------------------------------------------
+template <int FN, bool CH, int V, int G>
+__device__ __forceinline__ void load_prebuilt_query(Query<FN, CH, V, G>& q, const float* row, int D, int lane) {
+    const uint32_t nb = (uint32_t)D * 4u;
+    const rsrc_t s0 = make_rsrc(row, nb), s1 = make_rsrc(row + D, nb), s2 = make_rsrc(row + 2 * D, nb);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        q.q0[k] = bload<V>(s0, goff<V>(lane, k));
+        q.q1[k] = bload<V>(s1, goff<V>(lane, k));
+        q.q2[k] = bload<V>(s2, goff<V>(lane, k));
+    }
+    q.na_inv = q.nb_inv = 0.f;
+}
+
+template <int V>
+__device__ __forceinline__ void vstore(float* dst, const vecf<V>& v, bool ok) {
+    if (ok) *reinterpret_cast<vecf<V>*>(dst) = v;
+}
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void bwd_rows_kernel(ScoreParams p) {
+    constexpr int W = G * V * kWave;  // floats per operand per wave image
+    __shared__ float red[kWavesPerBlock][3][W];
+    __shared__ float red_mod[kWavesPerBlock];
+    const int64_t b = blockIdx.x;
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int D = p.D, DV = D / V;
+    Query<FN, CH, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+
+    vecf<V> dq0[G], dq1[G], dq2[G], dca[G], dcb[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) dq0[k] = dq1[k] = dq2[k] = vzero<V>();
+    float dmod = 0.f;
+    const int64_t per = (p.N + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t n_lo = w * per, n_hi = min(p.N, n_lo + per);
+    for (int64_t c0 = n_lo; c0 < n_hi; c0 += kWave) {
+        const int nc = (int)min((int64_t)kWave, n_hi - c0);
+        int64_t my_id = 0;
+        float my_g = 0.f;
+        if (lane < nc) {
+            my_id = p.c_idx ? p.c_idx[b * p.c_stride + c0 + lane] : b * p.c_dense + c0 + lane;
+            my_g = p.d_scores[b * p.d_ld + c0 + lane];
+        }
+        Cand<FN, V, G> x0, x1;
+        bool ok0, ok1;
+        x0.load(cand_row(p, readlane64(my_id, 0), ok0), ok0, D, lane);
+        for (int j = 0; j < nc; ++j) {
+            if (j + 1 < nc) {  // next row in flight while this one is reduced
+                if (j & 1)
+                    x0.load(cand_row(p, readlane64(my_id, j + 1), ok0), ok0, D, lane);
+                else
+                    x1.load(cand_row(p, readlane64(my_id, j + 1), ok1), ok1, D, lane);
+            }
+            const float g = readlanef(my_g, j);
+            if (j & 1)
+                cand_grad<FN, CH, V, G, true, false>(x1, q, g, lane, DV, p, dq0, dq1, dq2, dca, dcb, dmod);
+            else
+                cand_grad<FN, CH, V, G, true, false>(x0, q, g, lane, DV, p, dq0, dq1, dq2, dca, dcb, dmod);
+        }
+    }
+    // combine the four waves' partials in wave order through LDS
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int e = (lane + k * kWave) * V + i;
+            red[w][0][e] = dq0[k].a[i];
+            red[w][1][e] = dq1[k].a[i];
+            red[w][2][e] = dq2[k].a[i];
+        }
+    if (lane == 0) red_mod[w] = dmod;
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int e = (lane + k * kWave) * V + i;
+            float s0 = red[0][0][e], s1 = red[0][1][e], s2 = red[0][2][e];
+#pragma unroll
+            for (int ww = 1; ww < kWavesPerBlock; ++ww) {
+                s0 += red[ww][0][e];
+                s1 += red[ww][1][e];
+                s2 += red[ww][2][e];
+            }
+            dq0[k].a[i] = s0;
+            dq1[k].a[i] = s1;
+            dq2[k].a[i] = s2;
+        }
+    const float* qrow = p.qent + (qok ? qi : 0) * p.q_ld;
+    const float* rrow = p.rel + (rok ? ri : 0) * p.r_ld + p.r_off;
+    vecf<V> gea[G], geb[G], gra[G], grb[G];
+    query_chain<FN, CH, V, G>(q, dq0, dq1, dq2, qrow, qok, rrow, rok, lane, D, p, gea, geb, gra, grb);
+    const int64_t slot = p.slot0 + b;
+    float* qb = p.qbuf + slot * 3 * D;
+    float* ge = p.qg_ent + slot * p.ent_w;
+    float* gr = p.qg_rel + slot * p.rel_w;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const int gi = lane + k * kWave;
+        const bool in = gi < DV;
+        const int e = gi * V;
+        vstore<V>(qb + e, q.q0[k], in);
+        vstore<V>(qb + D + e, q.q1[k], in);
+        vstore<V>(qb + 2 * D + e, q.q2[k], in);
+        // a query row that is out of range (TF zero-fill) receives no gradient
+        vstore<V>(ge + e, qok ? gea[k] : vzero<V>(), in);
+        if constexpr (is_split(FN)) vstore<V>(ge + D + e, qok ? geb[k] : vzero<V>(), in);
+        vstore<V>(gr + e, rok ? gra[k] : vzero<V>(), in);
+        if constexpr (rel_split(FN)) vstore<V>(gr + D + e, rok ? grb[k] : vzero<V>(), in);
+    }
+    if (lane == 0 && p.dmod_part) {
+        float m = red_mod[0];
+        for (int ww = 1; ww < kWavesPerBlock; ++ww) m += red_mod[ww];
+        p.dmod_part[slot] = m;
+    }
+}
+
+// ascending bitonic sort of one int per lane across the wave
+__device__ __forceinline__ int wave_sort_asc(int v, int lane) {
+#pragma unroll
+    for (int k = 2; k <= kWave; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int o = __shfl_xor(v, j, kWave);
+            const bool keep_min = ((lane & k) == 0) == ((lane & j) == 0);
+            v = keep_min ? min(v, o) : max(v, o);
+        }
+    return v;
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+
+template <int FN, bool CH, int V, int G>
+__device__ __forceinline__ void ent_event(const ScoreParams& p, const Cand<FN, V, G>& c, int code, int lane,
+                                          vecf<V> (&acc_a)[G], vecf<V> (&acc_b)[G]) {
+    const int D = p.D, DV = D / V;
+    const int64_t BN = p.Bn * p.Nn;
+    vecf<V> dq0[G], dq1[G], dq2[G], dca[G], dcb[G];
+    float dmod = 0.f;
+    if (code < BN + p.Bn) {
+        // candidate event: negative (slot = row b) or positive (slot = Bn + b, tail formula)
+        const bool neg = code < BN;
+        const int64_t slot = neg ? code / p.Nn : p.Bn + (code - BN);
+        const float g = neg ? p.d_ns[code] : p.d_ps[code - BN];
+        if (neg) {
+            Query<FN, CH, V, G> q;
+            load_prebuilt_query<FN, CH, V, G>(q, p.qbuf + slot * 3 * D, D, lane);
+            cand_grad<FN, CH, V, G, false, true>(c, q, g, lane, DV, p, dq0, dq1, dq2, dca, dcb, dmod);
+        } else {
+            Query<FN, false, V, G> q;
+            load_prebuilt_query<FN, false, V, G>(q, p.qbuf + slot * 3 * D, D, lane);
+            cand_grad<FN, false, V, G, false, true>(c, q, g, lane, DV, p, dq0, dq1, dq2, dca, dcb, dmod);
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                acc_a[k].a[i] += dca[k].a[i];
+                if constexpr (is_split(FN)) acc_b[k].a[i] += dcb[k].a[i];
+            }
+    } else {
+        // row event: a slot's query-entity gradient (negative call's query, then positive's h)
+        const int64_t slot = code - BN - p.Bn;
+        const float* row = p.qg_ent + slot * p.ent_w;
+        const rsrc_t sa = make_rsrc(row, (uint32_t)D * 4u);
+        const rsrc_t sb = make_rsrc(row + D, is_split(FN) ? (uint32_t)D * 4u : 0u);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const vecf<V> a = bload<V>(sa, goff<V>(lane, k)), bb = bload<V>(sb, goff<V>(lane, k));
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                acc_a[k].a[i] += a.a[i];
+                if constexpr (is_split(FN)) acc_b[k].a[i] += bb.a[i];
+            }
+        }
+    }
+}
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
+    const int64_t e = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (e >= p.c_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int D = p.D, DV = D / V;
+    vecf<V> acc_a[G], acc_b[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) acc_a[k] = acc_b[k] = vzero<V>();
+    const int lo = p.ev_off[e], hi = p.ev_off[e + 1];
+    const int n = hi - lo;
+    if (n > 0) {
+        Cand<FN, V, G> c;
+        c.load(p.cent + e * p.c_ld, true, D, lane);
+        if (n <= kWave) {
+            int code = lane < n ? p.ev_code[lo + lane] : INT32_MAX;
+            code = wave_sort_asc(code, lane);
+            for (int j = 0; j < n; ++j)
+                ent_event<FN, CH, V, G>(p, c, __builtin_amdgcn_readlane(code, j), lane, acc_a, acc_b);
+        } else {
+            // large bucket: extract codes in ascending order (O(n^2 / 64), rare for random ids)
+            int last = -1;
+            for (int it = 0; it < n; ++it) {
+                int m = INT32_MAX;
+                for (int i = lo + lane; i < hi; i += kWave) {
+                    const int v = p.ev_code[i];
+                    if (v > last && v < m) m = v;
+                }
+                m = wave_min_i(m);
+                ent_event<FN, CH, V, G>(p, c, m, lane, acc_a, acc_b);
+                last = m;
+            }
+        }
+    }
+    float* out = p.d_out_ent + e * p.c_ld;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const int gi = lane + k * kWave;
+        const bool in = gi < DV;
+        vstore<V>(out + gi * V, acc_a[k], in);
+        if constexpr (is_split(FN)) vstore<V>(out + D + gi * V, acc_b[k], in);
     }
 }
 
@@ -685,6 +979,10 @@ template <int FN, bool CH, int V, int G>
 void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
     if (kind == KIND_BWD)
         hipLaunchKernelGGL((score_bwd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_BWD_ROWS)
+        hipLaunchKernelGGL((bwd_rows_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_BWD_ENT)
+        hipLaunchKernelGGL((bwd_ent_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_FINISH) {
         if constexpr (!CH) hipLaunchKernelGGL((finish_kernel<FN, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     } else

@@ -14,7 +14,7 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kMaxG = 8;  // float4 groups per lane per half-row kept in VGPRs (D <= 2048)
 constexpr int kBwdMaxG = 16;  // dword groups per lane of the backward's atomic-friendly layout (D <= 1024)
 
-enum Kind { KIND_FWD = 0, KIND_BWD = 1, KIND_FINISH = 2 };
+enum Kind { KIND_FWD = 0, KIND_BWD = 1, KIND_FINISH = 2, KIND_BWD_ROWS = 3, KIND_BWD_ENT = 4 };
 
 // Parameters of one scoring launch. Rows are addressed as base + row * ld (floats).
 //   query entity row of batch row b:  q_idx ? q_idx[b * q_stride] : b
@@ -56,6 +56,20 @@ struct ScoreParams {
     float* out_neg;      // [B] reduced negative branch
     float* out_pos_raw;  // [B] raw positive score (may be null)
     float* out_pos_ls;   // [B] logsigmoid(positive score)
+    // deterministic two-phase backward (kge_step_backward). A "slot" is one query side: slots
+    // [0, Bn) are the negative call's batch rows, [Bn, 2 Bn) the positive (single) call's.
+    float* qbuf;          // [slots, 3 D] query operands q0 | q1 | q2 (phase 1 writes, phase 2 reads)
+    float* qg_ent;        // [slots, ent_w] gradient of each slot's raw query-entity row
+    float* qg_rel;        // [slots, rel_w] gradient of each slot's used relation part
+    float* dmod_part;     // [slots] pRotatE modulus gradient partials
+    int64_t slot0;        // first slot of a phase-1 launch
+    int64_t ent_w, rel_w; // floats per entity row / per used relation part
+    const int* ev_off;    // [E + 1] bucket offsets of the per-entity gradient events (phase 2)
+    const int* ev_code;   // event codes, grouped by entity (order inside a bucket: arbitrary)
+    const float* d_ns;    // [Bn, N] dL/d(negative score), contiguous
+    const float* d_ps;    // [Bn] dL/d(positive score)
+    int64_t Bn, Nn;       // negative batch rows and candidates per row
+    float* d_out_ent;     // [E, c_ld] entity gradient table, fully overwritten by phase 2
 };
 
 // per-score-function launchers (one translation unit each, see kge_fn_*.hip)

@@ -340,30 +340,28 @@ class _StepForward(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, d_neg, d_pos):
+        """kge_step_backward: deterministic two-phase backward (no float atomics); it overwrites
+        every row of the gradient tables, so they are allocated uninitialised."""
         ent, rel, pos, neg, ns, ps = ctx.saved_tensors
         (fn, mode, rel_off, D, gamma, emb_range, modulus, temperature, adversarial, detach,
          mod_shape) = ctx.cfg
         lib = _lib.load()
-        st = _stream(ent.device)
         B, N = ns.shape
-        d_ent = torch.zeros_like(ent)
-        d_rel = torch.zeros_like(rel)
-        d_mod = torch.zeros(1, dtype=torch.float32, device=ent.device) if mod_shape is not None else None
-        if d_neg is not None:
-            d_neg = d_neg.contiguous()
-            d_ns = torch.empty_like(ns)
-            check(lib.kge_neg_reduce_bwd(ns.data_ptr(), B, N, ns.stride(0), float(temperature),
-                                         int(bool(adversarial)), int(bool(detach)), d_neg.data_ptr(),
-                                         d_ns.data_ptr(), d_ns.stride(0), st), "kge_neg_reduce_bwd")
-            score_indexed_bwd_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus,
-                                  d_ns, d_ent, d_rel, d_mod)
-        if d_pos is not None:
-            d_pos = d_pos.contiguous()
-            d_ps = torch.empty_like(ps)
-            check(lib.kge_log_sigmoid_bwd(ps.data_ptr(), d_pos.data_ptr(), B, d_ps.data_ptr(), st),
-                  "kge_log_sigmoid_bwd")
-            score_indexed_bwd_raw(fn, SINGLE, ent, rel, rel_off, pos, None, D, gamma, emb_range,
-                                  modulus, d_ps.view(B, 1), d_ent, d_rel, d_mod)
+        dev = ent.device
+        d_neg = torch.zeros(B, device=dev) if d_neg is None else d_neg.contiguous()
+        d_pos = torch.zeros(B, device=dev) if d_pos is None else d_pos.contiguous()
+        d_ent = torch.empty_like(ent)
+        d_rel = torch.empty_like(rel)
+        d_mod = torch.empty(1, dtype=torch.float32, device=dev) if mod_shape is not None else None
+        nbytes = lib.kge_step_backward_workspace_size(fn, ent.shape[0], B, N, D)
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        rc = lib.kge_step_backward(
+            fn, mode, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0),
+            rel_off, pos.data_ptr(), neg.data_ptr(), neg.stride(0), B, N, D, float(gamma), float(emb_range),
+            float(modulus), float(temperature), int(bool(adversarial)), int(bool(detach)), ns.data_ptr(),
+            ns.stride(0), ps.data_ptr(), d_neg.data_ptr(), d_pos.data_ptr(), d_ent.data_ptr(), d_rel.data_ptr(),
+            ctypes_ptr(d_mod), ws.data_ptr(), ws.numel(), _stream(dev))
+        check(rc, "kge_step_backward")
         if d_mod is not None:
             d_mod = d_mod.view(mod_shape)
         return (d_ent, d_rel, d_mod) + (None,) * 11

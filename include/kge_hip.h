@@ -205,6 +205,28 @@ int kge_neg_reduce_bwd(const float* scores, int64_t B, int64_t N, int64_t ld,
 int kge_log_sigmoid_bwd(const float* x, const float* d_out, int64_t n, float* d_x, void* stream);
 
 /*
+ * Deterministic backward of kge_step_forward (supervisor.py:25 tape.gradient through both calls),
+ * given dL/d(out_neg) and dL/d(out_pos) [B]. OVERWRITES every row of d_ent [nentity, ent_ld] and
+ * d_rel [nrelation, rel_ld] (no memset needed) and *d_modulus (pRotatE; may be NULL). No float
+ * atomics: phase 1 reduces each batch row's query-side gradient inside one block; phase 2 walks,
+ * for every entity row, the gradient events bucketed to it (counting sort) in a fixed order, so
+ * the result is bitwise reproducible. detach != 0: upstream's detached self-adversarial weights.
+ * workspace: device scratch of kge_step_backward_workspace_size(fn, nentity, B, N, D) bytes.
+ */
+int64_t kge_step_backward_workspace_size(int fn, int64_t nentity, int64_t B, int64_t N, int64_t D);
+int kge_step_backward(int fn, int mode,
+                      const float* ent, int64_t nentity, int64_t ent_ld,
+                      const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off,
+                      const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                      int64_t B, int64_t N, int64_t D,
+                      float gamma, float emb_range, float modulus,
+                      float temperature, int adversarial, int detach,
+                      const float* neg_scores, int64_t ns_ld, const float* pos_scores,
+                      const float* d_out_neg, const float* d_out_pos,
+                      float* d_ent, float* d_rel, float* d_modulus,
+                      void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
  * Dense Adam step over n floats (supervisor.py:26 `optimizer.apply_gradients`, run.py:111 Keras Adam).
  *   keras != 0: Keras Adam  (m += (g-m)(1-b1); v += (g^2-v)(1-b2);
  *                            p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t))

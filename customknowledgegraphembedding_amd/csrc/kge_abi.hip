@@ -199,30 +199,59 @@ __global__ __launch_bounds__(kBlock) void ev_count_kernel(EvArgs a, int* __restr
     if (k >= 0 && k < a.E) atomicAdd(&count[k], 1);
 }
 
-// exclusive scan of count[0..E) -> off[0..E], cursor = off; one block of 1024 threads
-__global__ __launch_bounds__(1024) void ev_scan_kernel(const int* __restrict__ count, int64_t E, int* __restrict__ off,
-                                                       int* __restrict__ cursor) {
-    __shared__ int part[1024];
+// exclusive scan of count[0..E) -> off[0..E] (and cursor = off), three launches:
+//   tiles of 1024 (block scan, tile totals) -> scan of the tile totals (one block) -> add prefix
+constexpr int kScanTile = 1024;
+
+__device__ __forceinline__ int block_exclusive_scan_1024(int v, int* part, int& total) {
     const int t = threadIdx.x;
-    const int64_t per = (E + 1023) / 1024;
-    const int64_t lo = t * per, hi = min(E, lo + per);
-    int s = 0;
-    for (int64_t i = lo; i < hi; ++i) s += count[i];
-    part[t] = s;
+    part[t] = v;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-        const int v = t >= o ? part[t - o] : 0;
+    for (int o = 1; o < kScanTile; o <<= 1) {  // Hillis-Steele inclusive scan in LDS
+        const int u = t >= o ? part[t - o] : 0;
         __syncthreads();
-        part[t] += v;
+        part[t] += u;
         __syncthreads();
     }
-    int run = part[t] - s;
-    for (int64_t i = lo; i < hi; ++i) {
-        off[i] = run;
-        cursor[i] = run;
-        run += count[i];
+    total = part[kScanTile - 1];
+    return part[t] - v;
+}
+
+__global__ __launch_bounds__(kScanTile) void scan_tiles_kernel(const int* __restrict__ count, int64_t E,
+                                                               int* __restrict__ off, int* __restrict__ tile_sum) {
+    __shared__ int part[kScanTile];
+    const int64_t i = (int64_t)blockIdx.x * kScanTile + threadIdx.x;
+    const int v = i < E ? count[i] : 0;
+    int total;
+    const int ex = block_exclusive_scan_1024(v, part, total);
+    if (i < E) off[i] = ex;
+    if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanTile) void scan_sums_kernel(int* __restrict__ tile_sum, int ntiles,
+                                                              int* __restrict__ off_end) {
+    __shared__ int part[kScanTile];
+    int carry = 0;
+    for (int base = 0; base < ntiles; base += kScanTile) {  // ntiles > 1024 loops (E > 1M rows)
+        const int i = base + threadIdx.x;
+        const int v = i < ntiles ? tile_sum[i] : 0;
+        int total;
+        const int ex = block_exclusive_scan_1024(v, part, total);
+        __syncthreads();
+        if (i < ntiles) tile_sum[i] = carry + ex;
+        carry += total;
+        __syncthreads();
     }
-    if (t == 1023) off[E] = part[1023];
+    if (threadIdx.x == 0) *off_end = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void scan_add_kernel(int* __restrict__ off, int* __restrict__ cursor, int64_t E,
+                                                          const int* __restrict__ tile_sum) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= E) return;
+    const int v = off[i] + tile_sum[i / kScanTile];
+    off[i] = v;
+    cursor[i] = v;
 }
 
 __global__ __launch_bounds__(kBlock) void ev_scatter_kernel(EvArgs a, int* __restrict__ cursor, int* __restrict__ code) {
@@ -232,48 +261,52 @@ __global__ __launch_bounds__(kBlock) void ev_scatter_kernel(EvArgs a, int* __res
     if (k >= 0 && k < a.E) code[atomicAdd(&cursor[k], 1)] = i;
 }
 
-// relation gradient: one wave per relation row; the slots that use it are found 64 at a time by a
-// ballot and added in slot order (deterministic). Lane l owns columns l, l+64, ... (<= 4096).
-constexpr int kRelCols = 64;  // columns per lane -> rel_w <= 4096
+// Relation gradient: one wave per (relation, 64-column chunk). The wave finds the slots that use
+// the relation 64 at a time (ballot) and adds their rows in slot order, 8 rows' loads in flight.
 __global__ __launch_bounds__(kBlock) void bwd_rel_kernel(const int64_t* __restrict__ pos, int64_t B, int64_t R,
                                                          const float* __restrict__ qg_rel, int64_t rel_w,
                                                          int64_t rel_off, float* __restrict__ d_rel, int64_t rel_ld,
                                                          int64_t rel_dim, const float* __restrict__ dmod_part,
                                                          float* __restrict__ d_mod) {
-    const int64_t rho = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int64_t wid = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (blockIdx.x == 0 && threadIdx.x == 0 && d_mod && dmod_part) {
         float m = 0.f;
         for (int64_t s = 0; s < 2 * B; ++s) m += dmod_part[s];
         *d_mod = m;
     }
+    const int64_t chunks = (rel_dim + kWave - 1) / kWave;
+    const int64_t rho = wid / chunks;
     if (rho >= R) return;
-    float acc[kRelCols];
+    const int64_t c = (wid - rho * chunks) * kWave + lane;  // column of the full relation row
+    float* out = d_rel + rho * rel_ld;
+    const bool used = c >= rel_off && c < rel_off + rel_w;
+    const int64_t cu = c - rel_off;
+    float acc = 0.f;
+    if (__ballot(used)) {
+        for (int64_t s0 = 0; s0 < 2 * B; s0 += kWave) {
+            const int64_t s = s0 + lane;
+            unsigned long long m = __ballot(s < 2 * B && pos[(s % B) * 3 + 1] == rho);  // slot s: row s % B
+            while (m) {
+                float v[8];
+                int nv = 0;
 #pragma unroll
-    for (int j = 0; j < kRelCols; ++j) acc[j] = 0.f;
-    for (int64_t s0 = 0; s0 < 2 * B; s0 += kWave) {
-        const int64_t s = s0 + lane;
-        const bool hit = s < 2 * B && pos[(s % B) * 3 + 1] == rho;  // slot s: row s % B of either call
-        unsigned long long m = __ballot(hit);
-        while (m) {
-            const int bit = __builtin_ctzll(m);
-            m &= m - 1;
-            const float* row = qg_rel + (s0 + bit) * rel_w;
+                for (int u = 0; u < 8; ++u) {
+                    v[u] = 0.f;
+                    if (m) {
+                        const int bit = __builtin_ctzll(m);
+                        m &= m - 1;
+                        v[u] = used ? qg_rel[(s0 + bit) * rel_w + cu] : 0.f;
+                        ++nv;
+                    }
+                }
 #pragma unroll
-            for (int j = 0; j < kRelCols; ++j) {
-                const int64_t c = lane + (int64_t)j * kWave;
-                if (c < rel_w) acc[j] += row[c];
+                for (int u = 0; u < 8; ++u)
+                    if (u < nv) acc += v[u];
             }
         }
     }
-    float* out = d_rel + rho * rel_ld;
-    for (int64_t c = lane; c < rel_dim; c += kWave)
-        if (c < rel_off || c >= rel_off + rel_w) out[c] = 0.f;  // parts no score function reads
-#pragma unroll
-    for (int j = 0; j < kRelCols; ++j) {
-        const int64_t c = lane + (int64_t)j * kWave;
-        if (c < rel_w) out[rel_off + c] = acc[j];
-    }
+    if (c < rel_dim) out[c] = used ? acc : 0.f;  // parts no score function reads get 0
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -735,7 +768,7 @@ int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq
 // ---------------------------------------------------------------------------------------------
 struct StepWs {
     float *d_ns, *d_ps, *qbuf, *qg_ent, *qg_rel, *dmod;
-    int *count, *off, *cursor, *code;
+    int *count, *off, *cursor, *code, *tiles;
     int64_t bytes;
 };
 
@@ -759,6 +792,7 @@ static StepWs step_ws_layout(char* base, int64_t E, int64_t B, int64_t N, int64_
     w.off = (int*)take((E + 1) * 4);
     w.cursor = (int*)take(E * 4);
     w.code = (int*)take((B * N + 3 * B) * 4);
+    w.tiles = (int*)take(((E + 1023) / 1024 + 1) * 4);
     w.bytes = o;
     return w;
 }
@@ -819,7 +853,6 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
         return fail(KGE_EINVAL, "null pointer");
     if (B * N + 3 * B >= (int64_t)INT32_MAX || nentity >= (int64_t)INT32_MAX)
         return fail(KGE_EINVAL, "too many gradient events for 32-bit codes");
-    if (rel_width(fn, D) > (int64_t)kRelCols * kWave) return fail(KGE_ENOTSUP, "relation part wider than 4096");
     const int64_t ent_w = ent_width(fn, D), rel_w = rel_width(fn, D);
     const int64_t rel_dim = rel_ld;  // rows are written over their full stride (padding included)
     StepWs w = step_ws_layout((char*)workspace, nentity, B, N, D, ent_w, rel_w);
@@ -879,7 +912,14 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
     if (hipMemsetAsync(w.count, 0, (size_t)(nentity * 4), st) != hipSuccess) return check_launch("memset");
     const unsigned eb = (unsigned)((a.total + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
-    hipLaunchKernelGGL(ev_scan_kernel, dim3(1), dim3(1024), 0, st, w.count, nentity, w.off, w.cursor);
+    if (nentity > 0) {
+        const int ntiles = (int)((nentity + kScanTile - 1) / kScanTile);
+        hipLaunchKernelGGL(scan_tiles_kernel, dim3(ntiles), dim3(kScanTile), 0, st, w.count, nentity, w.off,
+                           w.tiles);
+        hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanTile), 0, st, w.tiles, ntiles, w.off + nentity);
+        hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((nentity + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                           w.off, w.cursor, nentity, w.tiles);
+    }
     hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
     rc = check_launch("kge_step_backward events");
     if (rc) return rc;
@@ -903,7 +943,8 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
     }
     // 5. relation rows (slot order) and the pRotatE modulus
     if (nrelation > 0 || d_modulus) {
-        const int64_t rb = std::max<int64_t>(1, (nrelation + kWavesPerBlock - 1) / kWavesPerBlock);
+        const int64_t rwaves = nrelation * ((rel_dim + kWave - 1) / kWave);
+        const int64_t rb = std::max<int64_t>(1, (rwaves + kWavesPerBlock - 1) / kWavesPerBlock);
         hipLaunchKernelGGL(bwd_rel_kernel, dim3((unsigned)rb), dim3(kBlock), 0, st, pos, B, nrelation, w.qg_rel, rel_w,
                            rel_off, d_rel, rel_ld, rel_dim, w.dmod, d_modulus);
     }

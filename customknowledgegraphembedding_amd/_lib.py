@@ -85,6 +85,13 @@ SIGNATURES = {
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p,
          _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p],
     ),
+    "kge_step_backward_adam_workspace_size": (_c_i64, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
+    "kge_step_backward_adam": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_p, _c_f, _c_f, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p,
+         _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_i64, _c_p],
+    ),
     "kge_score_bwd_workspace_size": (_c_i64, [_c_i, _c_i, _c_i64, _c_i64, _c_i64]),
     "kge_score_indexed_bwd": (
         _c_i,

@@ -84,22 +84,8 @@ __global__ __launch_bounds__(kBlock) void log_sigmoid_bwd_kernel(const float* __
 //          p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
 // HBM-bound elementwise pass: 16-B loads/stores, grid-stride; optionally zeroes the gradient.
 // ---------------------------------------------------------------------------------------------
-struct AdamArgs {
-    float b1, b2, eps, alpha, step_size, bc2_sqrt;
-    int keras, zero_grad;
-};
-
 __device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v, const AdamArgs& a) {
-    const float gg = g;
-    if (a.keras) {
-        m += (gg - m) * (1.f - a.b1);
-        v += (gg * gg - v) * (1.f - a.b2);
-        p -= (m * a.alpha) / (sqrtf(v) + a.eps);
-    } else {
-        m = m + (1.f - a.b1) * (gg - m);
-        v = v * a.b2 + (1.f - a.b2) * gg * gg;
-        p -= a.step_size * m / (sqrtf(v) / a.bc2_sqrt + a.eps);
-    }
+    adam_update(p, g, m, v, a.b1, a.b2, a.eps, a.alpha, a.step_size, a.bc2_sqrt, a.keras);
     if (a.zero_grad) g = 0.f;
 }
 
@@ -839,17 +825,20 @@ int64_t kge_step_backward_workspace_size(int fn, int64_t nentity, int64_t B, int
     return step_ws_layout(nullptr, nentity, B, N, D, ent_width(fn, D), rel_width(fn, D)).bytes;
 }
 
-int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
-                      int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
-                      int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
-                      float temperature, int adversarial, int detach, const float* neg_scores, int64_t ns_ld,
-                      const float* pos_scores, const float* d_out_neg, const float* d_out_pos, float* d_ent,
-                      float* d_rel, float* d_modulus, void* workspace, int64_t workspace_bytes, void* stream) {
+static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                              int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos,
+                              const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma,
+                              float emb_range, float modulus, float temperature, int adversarial, int detach,
+                              const float* neg_scores, int64_t ns_ld, const float* pos_scores, const float* d_out_neg,
+                              const float* d_out_pos, float* d_ent, float* d_rel, float* d_modulus, void* workspace,
+                              int64_t workspace_bytes, void* stream, const AdamArgs* adam, float* m_ent,
+                              float* v_ent) {
     int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
     if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_backward needs a negative mode (0 or 1)");
     if (B < 0 || N <= 0 || D <= 0 || nentity < 0 || nrelation < 0) return fail(KGE_EINVAL, "bad shape");
-    if (!ent || !rel || !pos || !neg || !neg_scores || !pos_scores || !d_out_neg || !d_out_pos || !d_ent || !d_rel)
+    if (!ent || !rel || !pos || !neg || !neg_scores || !pos_scores || !d_out_neg || !d_out_pos || !d_rel ||
+        (!adam && !d_ent) || (adam && (!m_ent || !v_ent)))
         return fail(KGE_EINVAL, "null pointer");
     if (B * N + 3 * B >= (int64_t)INT32_MAX || nentity >= (int64_t)INT32_MAX)
         return fail(KGE_EINVAL, "too many gradient events for 32-bit codes");
@@ -858,7 +847,7 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
     StepWs w = step_ws_layout((char*)workspace, nentity, B, N, D, ent_w, rel_w);
     if (!workspace || workspace_bytes < w.bytes) return fail(KGE_EINVAL, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
-    if (B == 0) {
+    if (B == 0 && !adam) {
         if (hipMemsetAsync(d_ent, 0, (size_t)(nentity * ent_ld * 4), st) != hipSuccess ||
             hipMemsetAsync(d_rel, 0, (size_t)(nrelation * rel_ld * 4), st) != hipSuccess)
             return check_launch("kge_step_backward memset");
@@ -911,7 +900,7 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
     a.total = (int)(B * N + 3 * B);
     if (hipMemsetAsync(w.count, 0, (size_t)(nentity * 4), st) != hipSuccess) return check_launch("memset");
     const unsigned eb = (unsigned)((a.total + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
+    if (a.total > 0) hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
     if (nentity > 0) {
         const int ntiles = (int)((nentity + kScanTile - 1) / kScanTile);
         hipLaunchKernelGGL(scan_tiles_kernel, dim3(ntiles), dim3(kScanTile), 0, st, w.count, nentity, w.off,
@@ -920,7 +909,7 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
         hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((nentity + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                            w.off, w.cursor, nentity, w.tiles);
     }
-    hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
+    if (a.total > 0) hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
     rc = check_launch("kge_step_backward events");
     if (rc) return rc;
     // 4. phase 2: one wave per entity row, events in code order -> every row of d_ent written
@@ -937,6 +926,18 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
     q.Nn = N;
     q.ent_w = ent_w;
     q.d_out_ent = d_ent;
+    if (adam) {
+        q.adam.on = 1;
+        q.adam.m = m_ent;
+        q.adam.v = v_ent;
+        q.adam.b1 = adam->b1;
+        q.adam.b2 = adam->b2;
+        q.adam.eps = adam->eps;
+        q.adam.alpha = adam->alpha;
+        q.adam.step_size = adam->step_size;
+        q.adam.bc2_sqrt = adam->bc2_sqrt;
+        q.adam.keras = adam->keras;
+    }
     if (nentity > 0) {
         rc = run_score(fn, mode, q, KIND_BWD_ENT, stream);
         if (rc) return rc;
@@ -949,6 +950,68 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
                            rel_off, d_rel, rel_ld, rel_dim, w.dmod, d_modulus);
     }
     return check_launch("kge_step_backward");
+}
+
+int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                      int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                      int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
+                      float temperature, int adversarial, int detach, const float* neg_scores, int64_t ns_ld,
+                      const float* pos_scores, const float* d_out_neg, const float* d_out_pos, float* d_ent,
+                      float* d_rel, float* d_modulus, void* workspace, int64_t workspace_bytes, void* stream) {
+    return step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
+                              D, gamma, emb_range, modulus, temperature, adversarial, detach, neg_scores, ns_ld,
+                              pos_scores, d_out_neg, d_out_pos, d_ent, d_rel, d_modulus, workspace, workspace_bytes,
+                              stream, nullptr, nullptr, nullptr);
+}
+
+int64_t kge_step_backward_adam_workspace_size(int fn, int64_t nentity, int64_t nrelation, int64_t rel_ld, int64_t B,
+                                              int64_t N, int64_t D) {
+    const int64_t base = kge_step_backward_workspace_size(fn, nentity, B, N, D);
+    if (base < 0 || nrelation < 0 || rel_ld < 0) return -1;
+    return base + align256(nrelation * rel_ld * 4) + 256;
+}
+
+int kge_step_backward_adam(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld, float* rel,
+                           int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                           int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range,
+                           float* modulus_param, float modulus, float temperature, int adversarial, int detach,
+                           const float* neg_scores, int64_t ns_ld, const float* pos_scores, const float* d_out_neg,
+                           const float* d_out_pos, float* m_ent, float* v_ent, float* m_rel, float* v_rel,
+                           float* m_mod, float* v_mod, float lr, float beta1, float beta2, float eps, int64_t step,
+                           int keras, void* workspace, int64_t workspace_bytes, void* stream) {
+    if (step < 1) return fail(KGE_EINVAL, "step is 1-based");
+    if (!m_rel || !v_rel || (modulus_param && (!m_mod || !v_mod))) return fail(KGE_EINVAL, "null optimizer state");
+    const int64_t base = kge_step_backward_workspace_size(fn, nentity, B, N, D);
+    if (base < 0) return fail(KGE_EINVAL, "bad shape");
+    if (!workspace || workspace_bytes < kge_step_backward_adam_workspace_size(fn, nentity, nrelation, rel_ld, B, N, D))
+        return fail(KGE_EINVAL, "workspace too small");
+    float* d_rel = (float*)((char*)workspace + base);
+    float* d_mod = (float*)((char*)workspace + base + align256(nrelation * rel_ld * 4));
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    AdamArgs a;
+    a.b1 = beta1;
+    a.b2 = beta2;
+    a.eps = eps;
+    a.alpha = (float)((double)lr * std::sqrt(bc2) / bc1);
+    a.step_size = (float)((double)lr / bc1);
+    a.bc2_sqrt = (float)std::sqrt(bc2);
+    a.keras = keras;
+    a.zero_grad = 0;
+    int rc = step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B,
+                                N, D, gamma, emb_range, modulus, temperature, adversarial, detach, neg_scores, ns_ld,
+                                pos_scores, d_out_neg, d_out_pos, nullptr, d_rel, modulus_param ? d_mod : nullptr,
+                                workspace, base, stream, &a, m_ent, v_ent);
+    if (rc) return rc;
+    // the relation table (and the pRotatE modulus) are small: their gradients go through the dense
+    // optimizer kernel, with the same adam_update as the fused entity rows
+    rc = kge_adam_update(rel, d_rel, m_rel, v_rel, nrelation * rel_ld, lr, beta1, beta2, eps, step, keras, 0, stream);
+    if (rc) return rc;
+    if (modulus_param) {
+        rc = kge_adam_update(modulus_param, d_mod, m_mod, v_mod, 1, lr, beta1, beta2, eps, step, keras, 0, stream);
+        if (rc) return rc;
+    }
+    return ok();
 }
 
 }  // extern "C"

@@ -132,6 +132,23 @@ __device__ __forceinline__ float sigmoidf(float x) {
     return e / (1.f + e);
 }
 
+// One Adam update (supervisor.py:26; run.py:111 Keras Adam, or torch.optim.Adam), shared by the
+// dense optimizer kernel and the fused backward so both give bitwise-identical results.
+//   keras: m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2); p -= m * alpha / (sqrt(v) + eps)
+//   torch: m = lerp(m, g, 1 - b1); v = v b2 + (1 - b2) g^2; p -= step_size m / (sqrt(v) / bc2_sqrt + eps)
+__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, float b1, float b2, float eps,
+                                            float alpha, float step_size, float bc2_sqrt, int keras) {
+    if (keras) {
+        m += (g - m) * (1.f - b1);
+        v += (g * g - v) * (1.f - b2);
+        p -= (m * alpha) / (sqrtf(v) + eps);
+    } else {
+        m = m + (1.f - b1) * (g - m);
+        v = v * b2 + (1.f - b2) * g * g;
+        p -= step_size * m / (sqrtf(v) / bc2_sqrt + eps);
+    }
+}
+
 constexpr bool is_split(int fn) { return fn == KGE_COMPLEX || fn == KGE_ROTATE || fn == KGE_INTERHT; }
 constexpr bool rel_split(int fn) { return fn == KGE_COMPLEX; }
 
@@ -939,9 +956,9 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
     for (int k = 0; k < G; ++k) acc_a[k] = acc_b[k] = vzero<V>();
     const int lo = p.ev_off[e], hi = p.ev_off[e + 1];
     const int n = hi - lo;
+    Cand<FN, V, G> c;
+    if (n > 0 || p.adam.on) c.load(p.cent + e * p.c_ld, true, D, lane);
     if (n > 0) {
-        Cand<FN, V, G> c;
-        c.load(p.cent + e * p.c_ld, true, D, lane);
         if (n <= kWave) {
             int code = lane < n ? p.ev_code[lo + lane] : INT32_MAX;
             code = wave_sort_asc(code, lane);
@@ -961,6 +978,34 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
                 last = m;
             }
         }
+    }
+    if (p.adam.on) {
+        // fused optimizer: row e of the table (already in registers) and its Adam moments
+        float* prow = const_cast<float*>(p.cent) + e * p.c_ld;
+        float* mrow = p.adam.m + e * p.c_ld;
+        float* vrow = p.adam.v + e * p.c_ld;
+        const rsrc_t sm = make_rsrc(mrow, (uint32_t)p.ent_w * 4u), sv = make_rsrc(vrow, (uint32_t)p.ent_w * 4u);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int gi = lane + k * kWave;
+            const bool in = gi < DV;
+#pragma unroll
+            for (int h = 0; h < (is_split(FN) ? 2 : 1); ++h) {
+                const uint32_t off = (uint32_t)(h * D * 4) + goff<V>(lane, k);
+                vecf<V> mm = bload<V>(sm, off), vv = bload<V>(sv, off);
+                vecf<V> pp = h ? c.cb[k] : c.ca[k];
+                const vecf<V>& gg = h ? acc_b[k] : acc_a[k];
+#pragma unroll
+                for (int i = 0; i < V; ++i)
+                    adam_update(pp.a[i], gg.a[i], mm.a[i], vv.a[i], p.adam.b1, p.adam.b2, p.adam.eps, p.adam.alpha,
+                                p.adam.step_size, p.adam.bc2_sqrt, p.adam.keras);
+                const int64_t col = (int64_t)h * D + gi * V;
+                vstore<V>(prow + col, pp, in);
+                vstore<V>(mrow + col, mm, in);
+                vstore<V>(vrow + col, vv, in);
+            }
+        }
+        return;
     }
     float* out = p.d_out_ent + e * p.c_ld;
 #pragma unroll

@@ -70,6 +70,19 @@ struct ScoreParams {
     const float* d_ps;    // [Bn] dL/d(positive score)
     int64_t Bn, Nn;       // negative batch rows and candidates per row
     float* d_out_ent;     // [E, c_ld] entity gradient table, fully overwritten by phase 2
+    // fused optimizer in phase 2 (kge_step_backward_adam): row e of the table is updated in place
+    struct {
+        float* m;   // [E, c_ld] first moment
+        float* v;   // [E, c_ld] second moment
+        float b1, b2, eps, alpha, step_size, bc2_sqrt;
+        int keras, on;
+    } adam;
+};
+
+// Adam coefficients of step t (1-based), computed on the host in double
+struct AdamArgs {
+    float b1, b2, eps, alpha, step_size, bc2_sqrt;
+    int keras, zero_grad;
 };
 
 // per-score-function launchers (one translation unit each, see kge_fn_*.hip)

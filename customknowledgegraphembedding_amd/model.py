@@ -158,6 +158,61 @@ class TFKGEModel(_KGEBase):
         return neg.unsqueeze(1), pos.unsqueeze(1)
 
 
+    def train_step_fused(self, positive_sample, negative_sample, subsampling_weight, mode, optimizer):
+        """supervisor.py:15-26 entirely in HIP: fused forward (kge_step_forward), the loss of
+        supervisor.py:19-23, and kge_step_backward_adam — the deterministic backward with the
+        optimizer applied to each entity row inside the entity-major pass (no dense gradient is
+        materialised). Needs `optimizer` = customknowledgegraphembedding_amd.optim.Adam over this
+        model's parameters. Returns the loss (0-dim tensor)."""
+        from .optim import Adam
+        from . import _lib
+
+        if not isinstance(optimizer, Adam):
+            raise TypeError("train_step_fused needs customknowledgegraphembedding_amd.optim.Adam")
+        m = ops.mode_id(mode)
+        fn = FN_IDS[self.model_name]
+        ent, rel = self.entity_embedding, self.relation_embedding
+        is_p = self.model_name == "pRotatE"
+        modulus = float(self.modulus.reshape(-1)[0]) if is_p else 0.0
+        out_neg, out_pos, ns, ps = ops.step_forward_raw(fn, m, ent.detach(), rel.detach(), self._rel_off,
+                                                        positive_sample, negative_sample, self._D, self._gamma_f,
+                                                        self._range_f, modulus)
+        w = subsampling_weight.reshape(-1).to(out_neg.dtype)
+        sw = torch.sum(w)
+        loss = (-torch.sum(w * out_pos) / sw - torch.sum(w * out_neg) / sw) / 2
+        d_out = ((-0.5 / sw) * w).contiguous()  # the op order autograd uses for this loss
+        group = optimizer.param_groups[0]
+        lr = group["lr"]() if callable(group["lr"]) else group["lr"]
+        b1, b2 = group["betas"]
+        params = [ent, rel] + ([self.modulus] if is_p else [])
+        for prm in params:
+            st = optimizer.state[prm]
+            if not st:
+                st["step"] = 0
+                st["exp_avg"] = torch.zeros_like(prm)
+                st["exp_avg_sq"] = torch.zeros_like(prm)
+            st["step"] += 1
+        step = optimizer.state[ent]["step"]
+        B, N = ns.shape
+        lib = _lib.load()
+        nbytes = lib.kge_step_backward_adam_workspace_size(fn, ent.shape[0], rel.shape[0], rel.stride(0), B, N,
+                                                           self._D)
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=ent.device)
+        sm = optimizer.state[self.modulus] if is_p else None
+        rc = lib.kge_step_backward_adam(
+            fn, m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0),
+            self._rel_off, positive_sample.data_ptr(), negative_sample.data_ptr(), negative_sample.stride(0), B, N,
+            self._D, self._gamma_f, self._range_f, self.modulus.data_ptr() if is_p else None, modulus, 1.0, 1, 0,
+            ns.data_ptr(), ns.stride(0), ps.data_ptr(), d_out.data_ptr(), d_out.data_ptr(),
+            optimizer.state[ent]["exp_avg"].data_ptr(), optimizer.state[ent]["exp_avg_sq"].data_ptr(),
+            optimizer.state[rel]["exp_avg"].data_ptr(), optimizer.state[rel]["exp_avg_sq"].data_ptr(),
+            sm["exp_avg"].data_ptr() if is_p else None, sm["exp_avg_sq"].data_ptr() if is_p else None,
+            float(lr), float(b1), float(b2), float(group["eps"]), int(step), int(group["semantics"] == "keras"),
+            ws.data_ptr(), ws.numel(), torch.cuda.current_stream(ent.device).cuda_stream)
+        _lib.check(rc, "kge_step_backward_adam")
+        return loss.detach()
+
+
 class KGEModel(_KGEBase):
     """Drop-in for the upstream PyTorch ``KGEModel`` (KnowledgeGraphEmbedding/codes/model.py)."""
 

@@ -70,12 +70,21 @@ class Sum:
 class Trainer:
     """supervisor.py:5-58."""
 
-    def __init__(self, strategy, dataloader, model, optimizer, metrics):
+    def __init__(self, strategy, dataloader, model, optimizer, metrics, fused=None):
         self.dataloader = dataloader
         self.model = model
         self.optimizer = optimizer
         self.metrics = metrics
         self.strategy = strategy
+        if fused is None:
+            # the fused optimizer never materialises gradients, so it needs a single replica and
+            # this package's Adam over exactly the model's parameters in one group
+            from .optim import Adam
+            fused = (isinstance(optimizer, Adam) and strategy.num_replicas_in_sync == 1
+                     and hasattr(model, "train_step_fused") and len(optimizer.param_groups) == 1
+                     and {id(p) for p in optimizer.param_groups[0]["params"]} == {id(p) for p in model.parameters()
+                                                                                   if p.requires_grad})
+        self.fused = bool(fused)
 
     def loss(self, positive_sample, negative_sample, subsampling_weight, mode):
         """supervisor.py:17-23 — both calls fused, then the weighted loss."""
@@ -94,6 +103,12 @@ class Trainer:
             negative_sample = negative_sample.to(dev, non_blocking=True)
             subsampling_weight = subsampling_weight.to(dev, non_blocking=True)
             mode = mode.cpu() if torch.is_tensor(mode) else mode
+            if self.fused:
+                # forward + loss + deterministic backward with Adam fused into the entity pass
+                loss = self.model.train_step_fused(positive_sample, negative_sample, subsampling_weight, mode[0],
+                                                   self.optimizer)
+                self.metrics.update_state(loss * self.strategy.num_replicas_in_sync)
+                return loss
             self.optimizer.zero_grad(set_to_none=True)
             loss = self.loss(positive_sample, negative_sample, subsampling_weight, mode)
             loss.backward()                                                    # :25

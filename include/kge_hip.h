@@ -227,6 +227,30 @@ int kge_step_backward(int fn, int mode,
                       void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
+ * The whole train step's update (supervisor.py:25-26) with the optimizer FUSED into the backward:
+ * the deterministic backward of kge_step_backward, where the entity-major phase applies Adam
+ * (keras != 0: Keras rule, else torch.optim.Adam) to each entity row as it finishes its
+ * gradient, in place on `ent` / m_ent / v_ent; then Adam on the relation table (and on the
+ * pRotatE modulus if modulus_param != NULL). Bitwise identical to kge_step_backward followed by
+ * kge_adam_update on every table, without materialising the entity gradient.
+ * workspace: kge_step_backward_adam_workspace_size(...) bytes.
+ */
+int64_t kge_step_backward_adam_workspace_size(int fn, int64_t nentity, int64_t nrelation, int64_t rel_ld,
+                                              int64_t B, int64_t N, int64_t D);
+int kge_step_backward_adam(int fn, int mode,
+                           float* ent, int64_t nentity, int64_t ent_ld,
+                           float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off,
+                           const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                           int64_t B, int64_t N, int64_t D,
+                           float gamma, float emb_range, float* modulus_param, float modulus,
+                           float temperature, int adversarial, int detach,
+                           const float* neg_scores, int64_t ns_ld, const float* pos_scores,
+                           const float* d_out_neg, const float* d_out_pos,
+                           float* m_ent, float* v_ent, float* m_rel, float* v_rel, float* m_mod, float* v_mod,
+                           float lr, float beta1, float beta2, float eps, int64_t step, int keras,
+                           void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
  * Dense Adam step over n floats (supervisor.py:26 `optimizer.apply_gradients`, run.py:111 Keras Adam).
  *   keras != 0: Keras Adam  (m += (g-m)(1-b1); v += (g^2-v)(1-b2);
  *                            p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t))

@@ -124,3 +124,39 @@ def test_step_backward_deterministic_and_matches_atomic_path(name, mode):
         assert torch.equal(x, y)  # bitwise reproducible
         scale = float(z.abs().max().clamp_min(1e-12))
         assert float((x - z).abs().max()) <= 1e-5 * scale + 1e-7, name
+
+
+@pytest.mark.parametrize("name", ["InterHT", "DistMult", "RotatE", "pRotatE"])
+@pytest.mark.parametrize("semantics", ["keras", "torch"])
+def test_fused_train_step_equals_autograd_path(name, semantics):
+    """Trainer with the optimizer fused into the backward (kge_step_backward_adam) leaves tables,
+    Adam moments and losses bitwise equal to the autograd path (kge_step_backward + kge_adam_update)."""
+    cfg = {"InterHT": (True, False, True), "DistMult": (False, False, False), "RotatE": (True, False, False),
+           "pRotatE": (False, False, False)}
+    de, dr, tr = cfg[name]
+    E, R, d, B, N = 300, 6, 32, 48, 40
+
+    def make():
+        return kge.TFKGEModel(name, E, R, d, 10.0, de, dr, tr, device=DEV, seed=21)
+
+    g = np.random.RandomState(3)
+    data = []
+    for i in range(4):
+        pos = torch.from_numpy(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1))
+        neg = torch.from_numpy(g.randint(E, size=(B, N)))
+        w = torch.from_numpy(g.uniform(0.1, 1, size=(B, 1))).float()
+        data.append((pos, neg, w, torch.tensor([i % 2] * B)))
+    runs = []
+    for fused in (True, False):
+        m = make()
+        opt = Adam(m.parameters(), lr=2e-3, semantics=semantics)
+        tr_ = Trainer(Strategy(), data, m, opt, Sum(), fused=fused)
+        assert tr_.fused == fused
+        it = iter(data)
+        losses = [float(tr_.train_step(it)) for _ in range(4)]
+        runs.append((losses, [p.detach().clone() for p in m.parameters()],
+                     [opt.state[p]["exp_avg_sq"].clone() for p in m.parameters()]))
+    (la, pa, va), (lb, pb, vb) = runs
+    assert la == lb
+    for x, y in zip(pa + va, pb + vb):
+        assert torch.equal(x, y)

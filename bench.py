@@ -234,8 +234,10 @@ def train_step_bench(m, batches, steps, warmup):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     N = batches[0][1].shape[1]
-    return {"ms_per_step": dt * 1e3, "triples_per_s": (B * N + B) / dt, "steps": steps,
-            "what": "fwd (kge_step_forward) + loss + bwd (HIP, fp32 atomics) + Keras Adam (HIP) on both tables"}
+    return {"ms_per_step": dt * 1e3, "triples_per_s": (B * N + B) / dt, "steps": steps, "fused": tr.fused,
+            "what": "supervisor.py:13-30: fwd (kge_step_forward) + loss + deterministic bwd with Keras Adam "
+                    "fused into the entity pass (kge_step_backward_adam)" if tr.fused else
+                    "fwd + loss + deterministic bwd (kge_step_backward) + Keras Adam (kge_adam_update)"}
 
 
 def cpu_baseline(w, budget_s=15.0, rows=64):

@@ -92,6 +92,10 @@ SIGNATURES = {
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_p, _c_f, _c_f, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p,
          _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_i64, _c_p],
     ),
+    "kge_sampler_create": (_c_p, [_c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i]),
+    "kge_sampler_seed": (_c_i, [_c_p, ctypes.c_uint32]),
+    "kge_sampler_get": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p, _c_p]),
+    "kge_sampler_destroy": (None, [_c_p]),
     "kge_score_bwd_workspace_size": (_c_i64, [_c_i, _c_i, _c_i64, _c_i64, _c_i64]),
     "kge_score_indexed_bwd": (
         _c_i,

@@ -478,6 +478,8 @@ void fill_dense(ScoreParams& p, int fn, int mode, const float* head, int64_t hea
 bool empty(int64_t B, int64_t N) { return B == 0 || N == 0; }
 
 }  // namespace
+
+int set_error(int code, const char* msg) { return fail(code, msg); }
 }  // namespace kge_impl
 
 using namespace kge_impl;

@@ -251,6 +251,23 @@ int kge_step_backward_adam(int fn, int mode,
                            void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
+ * Negative sampler of the training batches (host memory, no GPU): the upstream KnowledgeGraphEmbedding
+ * TrainDataset (call sites compress_data/main.py:64-73), bit-exact with its numpy code for the same RNG
+ * state: negatives from numpy's legacy MT19937 `randint` (seeded like np.random.seed(seed)), filtered by
+ * `np.in1d(..., assume_unique=True, invert=True)` exactly as numpy 2.2.6 evaluates it, weights
+ * sqrt(1 / (count(h,r) + count(t,-r-1))) with count start 4.
+ *   triples [T,3] int64 (h, r, t) training triples; mode KGE_HEAD_BATCH or KGE_TAIL_BATCH
+ *   kge_sampler_get: for each idx[b] in order: pos[b] = triples[idx[b]], neg[b] [N], weight[b]
+ */
+typedef struct kge_sampler kge_sampler;
+kge_sampler* kge_sampler_create(const int64_t* triples, int64_t ntriples, int64_t nentity, int64_t nrelation,
+                                int64_t negative_sample_size, int mode);
+int kge_sampler_seed(kge_sampler* sampler, uint32_t seed);
+int kge_sampler_get(kge_sampler* sampler, const int64_t* idx, int64_t B, int64_t* pos, int64_t* neg,
+                    float* weight);
+void kge_sampler_destroy(kge_sampler* sampler);
+
+/*
  * Dense Adam step over n floats (supervisor.py:26 `optimizer.apply_gradients`, run.py:111 Keras Adam).
  *   keras != 0: Keras Adam  (m += (g-m)(1-b1); v += (g^2-v)(1-b2);
  *                            p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t))

@@ -322,3 +322,44 @@ def eval_ranks(name, ent, rel, pos, mode, all_true, gamma, embedding_range=None,
         slot = h if mode == "head-batch" else t
         ranks.append(int((order == slot).nonzero()[0, 0]) + 1)
     return torch.tensor(ranks, dtype=torch.int64)
+
+
+# ------------------------------------------------------------------------------------------------
+# negative sampler: upstream TrainDataset.__getitem__ with numpy itself (the reference's own RNG and
+# set-membership code, so this part of the oracle is pinned by numpy, not restated)
+# ------------------------------------------------------------------------------------------------
+def upstream_train_dataset(triples, nentity, negative_sample_size, mode):
+    """Returns getitem(idx) -> (positive_sample, negative_sample, subsampling_weight) computed
+    exactly as upstream TrainDataset does, drawing from numpy's GLOBAL RandomState."""
+    import numpy as np
+
+    triples = [tuple(map(int, t)) for t in triples]
+    count = {}
+    for h, r, t in triples:  # count_frequency(start=4)
+        count[(h, r)] = count.get((h, r), 3) + 1
+        count[(t, -r - 1)] = count.get((t, -r - 1), 3) + 1
+    true_head, true_tail = {}, {}
+    for h, r, t in triples:  # get_true_head_and_tail
+        true_tail.setdefault((h, r), []).append(t)
+        true_head.setdefault((r, t), []).append(h)
+    true_head = {k: np.array(list(set(v))) for k, v in true_head.items()}
+    true_tail = {k: np.array(list(set(v))) for k, v in true_tail.items()}
+
+    def getitem(idx):
+        head, relation, tail = triples[idx]
+        w = count[(head, relation)] + count[(tail, -relation - 1)]
+        w = torch.sqrt(1 / torch.Tensor([w]))
+        lst, size = [], 0
+        while size < negative_sample_size:
+            neg = np.random.randint(nentity, size=negative_sample_size * 2)
+            if mode == "head-batch":
+                mask = np.in1d(neg, true_head[(relation, tail)], assume_unique=True, invert=True)
+            else:
+                mask = np.in1d(neg, true_tail[(head, relation)], assume_unique=True, invert=True)
+            neg = neg[mask]
+            lst.append(neg)
+            size += neg.size
+        neg = np.concatenate(lst)[:negative_sample_size]
+        return np.array([head, relation, tail]), neg, w.numpy()
+
+    return getitem

@@ -96,6 +96,15 @@ SIGNATURES = {
     "kge_sampler_seed": (_c_i, [_c_p, ctypes.c_uint32]),
     "kge_sampler_get": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p, _c_p]),
     "kge_sampler_destroy": (None, [_c_p]),
+    "kge_crc32c": (ctypes.c_uint32, [_c_p, _c_i64]),
+    "kge_tfrecord_open": (_c_p, [_c_p, _c_i64, _c_i]),
+    "kge_tfrecord_next": (_c_i, [_c_p, _c_p]),
+    "kge_tfrecord_copy": (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p]),
+    "kge_tfrecord_rewind": (_c_i, [_c_p]),
+    "kge_tfrecord_close": (None, [_c_p]),
+    "kge_tfrecord_writer_open": (_c_p, [ctypes.c_char_p]),
+    "kge_tfrecord_write_example": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64]),
+    "kge_tfrecord_writer_close": (_c_i, [_c_p]),
     "kge_score_bwd_workspace_size": (_c_i64, [_c_i, _c_i, _c_i64, _c_i64, _c_i64]),
     "kge_score_indexed_bwd": (
         _c_i,

@@ -268,6 +268,32 @@ int kge_sampler_get(kge_sampler* sampler, const int64_t* idx, int64_t B, int64_t
 void kge_sampler_destroy(kge_sampler* sampler);
 
 /*
+ * TFRecord IO of the reference's on-disk training batches (host memory, no GPU). One
+ * tf.train.Example per batch with Int64List "positive_sample" [B*3], "negative_sample" [B*N],
+ * FloatList "subsampling_weight" [B], Int64List "mode" [B]:
+ *   writer = compress_data/main.py:117-131 + compress_data/utils.py:35-42 (create_example);
+ *   reader = tensorflow_codes/run.py:40-51 (parse_tfrecord_fn, VarLenFeature + to_dense) over
+ *            tf.data.TFRecordDataset(paths) (run.py:87), files read in order.
+ * Framing and CRC-32C (masked) as TFRecord; CRCs are verified when verify_crc != 0.
+ * kge_tfrecord_next: 1 = a record was parsed and counts[4] = {npos, nneg, nw, nmode}; 0 = end of the
+ * last file; < 0 = error (truncated, CRC mismatch, malformed proto, wrong list type).
+ */
+typedef struct kge_tfrecord_reader kge_tfrecord_reader;
+typedef struct kge_tfrecord_writer kge_tfrecord_writer;
+uint32_t kge_crc32c(const void* data, int64_t n);
+kge_tfrecord_reader* kge_tfrecord_open(const char* const* paths, int64_t npaths, int verify_crc);
+int kge_tfrecord_next(kge_tfrecord_reader* reader, int64_t* counts);
+int kge_tfrecord_copy(kge_tfrecord_reader* reader, int64_t* positive_sample, int64_t* negative_sample,
+                      float* subsampling_weight, int64_t* mode);
+int kge_tfrecord_rewind(kge_tfrecord_reader* reader);
+void kge_tfrecord_close(kge_tfrecord_reader* reader);
+kge_tfrecord_writer* kge_tfrecord_writer_open(const char* path);
+int kge_tfrecord_write_example(kge_tfrecord_writer* writer, const int64_t* positive_sample, int64_t npos,
+                               const int64_t* negative_sample, int64_t nneg, const float* subsampling_weight,
+                               int64_t nw, const int64_t* mode, int64_t nmode);
+int kge_tfrecord_writer_close(kge_tfrecord_writer* writer);
+
+/*
  * Dense Adam step over n floats (supervisor.py:26 `optimizer.apply_gradients`, run.py:111 Keras Adam).
  *   keras != 0: Keras Adam  (m += (g-m)(1-b1); v += (g^2-v)(1-b2);
  *                            p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t))

@@ -56,6 +56,11 @@ WORKLOADS = {
     "c5": dict(name="FB15k filtered eval DistMult d=1000, 1024 queries/step vs all 14951 entities",
                fn="DistMult", nentity=14951, nrelation=1345, hidden_dim=1000, gamma=24.0, de=False, tr=False,
                dr=False, B=1024, N=14951, eval=True),
+    # TranSparse (model.py:226-235; in the reference's model_func dict, not in a BASELINE config):
+    # WN18RR-sized graph, d=500, head-batch (the only mode whose scores depend on the negatives, Q9)
+    "c6": dict(name="WN18RR-sized TranSparse d=500 gamma=12 n_neg=256 bz=512 head-batch", fn="TranSparse",
+               nentity=40943, nrelation=11, hidden_dim=500, gamma=12.0, de=False, tr=False, dr=False,
+               B=512, N=256, transparse=True),
     "c4s": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512/rank, row-sharded owner-computes",
                 fn="DistMult", nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False,
                 dr=False, B=512, N=1024, sharded=True),
@@ -209,6 +214,76 @@ def eval_bench(w, a, device):
             "filtered_metrics": met}
 
 
+def transparse_bench(w, a, device):
+    """c6: TranSparse scoring step = head-batch negatives ([B, N], kge_transparse_score on the fp32
+    MFMA, events around it) + the positives (single, [B, 1]) + the row reductions; plus the
+    autograd train step (deterministic backward + HIP Adam) as a side measurement."""
+    from customknowledgegraphembedding_amd.model import TFKGEModel
+    from customknowledgegraphembedding_amd.optim import Adam
+    from customknowledgegraphembedding_amd.supervisor import Strategy, Sum, Trainer
+    m = TFKGEModel("TranSparse", w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"], device=device, seed=0)
+    E, R, B, N, d = w["nentity"], w["nrelation"], w["B"], w["N"], w["hidden_dim"]
+    batches = []
+    for i in range(4):
+        g = np.random.RandomState(1 + i)
+        pos = np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1)
+        neg = np.random.RandomState(2 + i).randint(E, size=(B, N))
+        batches.append((torch.from_numpy(pos).to(device), torch.from_numpy(neg).to(device)))
+    ent, rel, W, mask = m.entity_embedding.detach(), m.relation_embedding.detach(), m.W.detach(), m.mask
+
+    def step(b, ev=None):
+        pos, neg = b
+        if ev is not None:
+            ev[0].record()
+        ns = ops.transparse_score_raw(0, ent, rel, W, mask, pos, neg, m._gamma_f)
+        if ev is not None:
+            ev[1].record()
+        ps = ops.transparse_score_raw(3, ent, rel, W, mask, pos, None, m._gamma_f)
+        return ops.neg_reduce_raw(ns), ops.log_sigmoid_raw(ps.reshape(-1))
+
+    for i in range(a.warmup):
+        step(batches[i % 4])
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(batches[i % 4], evs[i])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    k_s = statistics.mean(e0.elapsed_time(e1) for e0, e1 in evs) / 1e3
+    flops = 2.0 * B * N * d * d
+    train = None
+    if a.train_steps > 0:
+        wts = torch.ones(B, 1, device=device)
+        data = [(pos, neg, wts, torch.tensor([0])) for pos, neg in batches]
+
+        def cycle():
+            while True:
+                yield from data
+
+        tr = Trainer(Strategy(), data, m, Adam([p for p in m.parameters() if p.requires_grad], lr=5e-5), Sum())
+        it = cycle()
+        tr.train_step(it)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(a.train_steps):
+            tr.train_step(it)
+        torch.cuda.synchronize()
+        tdt = (time.perf_counter() - t1) / a.train_steps
+        train = {"ms_per_step": tdt * 1e3, "triples_per_s": (B * N + B) / tdt, "steps": a.train_steps,
+                 "what": "supervisor.py:13-30 with TranSparse: fwd (MFMA) + loss + deterministic MFMA backward "
+                         "(kge_transparse_score_bwd) + Keras Adam (kge_adam_update) over E, R and W"}
+    return {"metric": f"scored triples/sec (pos+neg, one fused scoring step), {w['name']}",
+            "value": (B * N + B) * a.steps / dt, "unit": "triples/s", "n_gpus": 1, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (random tables, uniform random ids)",
+            "config": {"workload": w["name"], "global_batch": B, "n_neg": N, "d": d},
+            "roofline": {"bound": "mfma", "achieved": flops / k_s / 1e12, "peak": 157.3, "unit": "TFLOP/s",
+                         "frac": flops / k_s / 1e12 / 157.3, "traffic": None,
+                         "kernel": "ts_rows_kernel<TS_FWD> (v_mfma_f32_32x32x2_f32)", "kernel_avg_us": k_s * 1e6},
+            "train_step": train}
+
+
 def train_step_bench(m, batches, steps, warmup):
     """supervisor.py:13-30 train step (fused forward, HIP backward, HIP Keras Adam) on the same
     workload: reported beside the scoring metric, never as `value`."""
@@ -320,10 +395,10 @@ def main():
     torch.cuda.set_device(device)
 
     w = WORKLOADS[a.workload]
-    fn = FN_IDS[w["fn"]]
+    fn = FN_IDS.get(w["fn"])
     B, N = w["B"], w["N"]
-    if w.get("eval"):
-        line = eval_bench(w, a, device)
+    if w.get("eval") or w.get("transparse"):
+        line = eval_bench(w, a, device) if w.get("eval") else transparse_bench(w, a, device)
         if rank == 0:
             print(json.dumps(line), flush=True)
         if dist:

@@ -8,6 +8,7 @@
 #include <string>
 
 #include "kge_device.h"
+#include "kge_scan.h"
 
 namespace kge_impl {
 namespace {
@@ -183,61 +184,6 @@ __global__ __launch_bounds__(kBlock) void ev_count_kernel(EvArgs a, int* __restr
     if (i >= a.total) return;
     const int64_t k = ev_key(a, i);
     if (k >= 0 && k < a.E) atomicAdd(&count[k], 1);
-}
-
-// exclusive scan of count[0..E) -> off[0..E] (and cursor = off), three launches:
-//   tiles of 1024 (block scan, tile totals) -> scan of the tile totals (one block) -> add prefix
-constexpr int kScanTile = 1024;
-
-__device__ __forceinline__ int block_exclusive_scan_1024(int v, int* part, int& total) {
-    const int t = threadIdx.x;
-    part[t] = v;
-    __syncthreads();
-    for (int o = 1; o < kScanTile; o <<= 1) {  // Hillis-Steele inclusive scan in LDS
-        const int u = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += u;
-        __syncthreads();
-    }
-    total = part[kScanTile - 1];
-    return part[t] - v;
-}
-
-__global__ __launch_bounds__(kScanTile) void scan_tiles_kernel(const int* __restrict__ count, int64_t E,
-                                                               int* __restrict__ off, int* __restrict__ tile_sum) {
-    __shared__ int part[kScanTile];
-    const int64_t i = (int64_t)blockIdx.x * kScanTile + threadIdx.x;
-    const int v = i < E ? count[i] : 0;
-    int total;
-    const int ex = block_exclusive_scan_1024(v, part, total);
-    if (i < E) off[i] = ex;
-    if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kScanTile) void scan_sums_kernel(int* __restrict__ tile_sum, int ntiles,
-                                                              int* __restrict__ off_end) {
-    __shared__ int part[kScanTile];
-    int carry = 0;
-    for (int base = 0; base < ntiles; base += kScanTile) {  // ntiles > 1024 loops (E > 1M rows)
-        const int i = base + threadIdx.x;
-        const int v = i < ntiles ? tile_sum[i] : 0;
-        int total;
-        const int ex = block_exclusive_scan_1024(v, part, total);
-        __syncthreads();
-        if (i < ntiles) tile_sum[i] = carry + ex;
-        carry += total;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *off_end = carry;
-}
-
-__global__ __launch_bounds__(kBlock) void scan_add_kernel(int* __restrict__ off, int* __restrict__ cursor, int64_t E,
-                                                          const int* __restrict__ tile_sum) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= E) return;
-    const int v = off[i] + tile_sum[i / kScanTile];
-    off[i] = v;
-    cursor[i] = v;
 }
 
 __global__ __launch_bounds__(kBlock) void ev_scatter_kernel(EvArgs a, int* __restrict__ cursor, int* __restrict__ code) {
@@ -903,14 +849,7 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
     if (hipMemsetAsync(w.count, 0, (size_t)(nentity * 4), st) != hipSuccess) return check_launch("memset");
     const unsigned eb = (unsigned)((a.total + kBlock - 1) / kBlock);
     if (a.total > 0) hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
-    if (nentity > 0) {
-        const int ntiles = (int)((nentity + kScanTile - 1) / kScanTile);
-        hipLaunchKernelGGL(scan_tiles_kernel, dim3(ntiles), dim3(kScanTile), 0, st, w.count, nentity, w.off,
-                           w.tiles);
-        hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanTile), 0, st, w.tiles, ntiles, w.off + nentity);
-        hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((nentity + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                           w.off, w.cursor, nentity, w.tiles);
-    }
+    launch_exclusive_scan(w.count, nentity, w.off, w.cursor, w.tiles, st);
     if (a.total > 0) hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
     rc = check_launch("kge_step_backward events");
     if (rc) return rc;

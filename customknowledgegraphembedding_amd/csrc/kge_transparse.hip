@@ -1,0 +1,885 @@
+// kge_transparse.hip — TranSparse score function on the fp32 matrix cores,
+// forward and deterministic backward.
+//
+// Reference: tensorflow_codes/model.py:226-235 with its call sites :139-142 (single), :161-164
+// (head-batch), :187-190 (tail-batch) and the tables of :96-106:
+//   M_r     = mask[r] * W[r]                        ([d, d], mask is a fixed 0/1 pattern)
+//   p_head  = normalize(head @ M_r)                 (no epsilon, Q7)
+//   p_tail  = normalize(head @ M_r)                 (Q9: computed from the HEAD, tail unused)
+//   rel     = normalize(relation)
+//   score   = gamma - || p_head * rel - p_tail ||_1 = gamma - sum_j |p_j c_j| / P,
+//             P = ||p||, u = r / ||r||, c = u - 1
+// Shapes follow the reference: head-batch head = E[neg] -> [B, N]; single and tail-batch head = E[pos_h]
+// -> [B, 1] (Q9 makes the tail-batch score independent of the negatives).
+//
+// A "row" is one head vector to project. Two row sources share every kernel:
+//   * per batch row  (head-batch): block = (b, 128 negatives); all rows share relation pos[b,1];
+//   * per relation   (single/tail): block = (r, 128-row chunk of the batch rows with pos[b,1] == r),
+//     found by an ordered ballot scan of pos[:,1]; bucket r = nrel collects out-of-range relations
+//     (zero rows -> NaN scores, like TF-GPU gather).
+//
+// Forward (ts_rows_kernel<TS_FWD>): P[128, d] = H . M_r on v_mfma_f32_32x32x2_f32, block tile 128 x 128
+// over the column tiles (2 x 2 waves of 64 x 64, K chunks of 16 double-buffered through LDS, the mask
+// product fused into the M_r tile load). P never leaves registers: each column tile folds into per-row
+// sums of p^2 and |p c|; optional per-row stats (P^2, sum |p c|) are kept for the backward.
+//
+// Backward of the raw scores, with G = dL/ds of a row:
+//   dL/dp_j = (G / P) (p_j * S / P^2 - sign(p_j c_j) c_j),   S = sum_j |p_j c_j|
+//   dL/du_j = -sign(c_j) sum_rows (G / P) |p_j|   ->  dL/dr = (g_u - u (u . g_u)) / ||r||
+//   dL/dh   = dL/dp . M_r^T,      dL/dW_r = mask_r * sum_rows h^T dL/dp
+// Kernels: (1) ts_rows_kernel<TS_GP> recomputes P tiles and writes dL/dp rows plus per-block column
+// partials of g_u; (2) ts_rows_kernel<TS_DH> = dL/dp . M_r^T -> dH rows; (3) ts_dw_kernel: per
+// (relation, 128 x 128 tile of dW, K split) MFMA over the relation's rows (relation CSR built by
+// ordered compaction), split partials reduced in order; (4) entity buckets (count, scan, scatter,
+// rank-sort by row id) and a wave per entity adding its dH rows in row order; (5) ts_drel_kernel per
+// relation adds the g_u partials in block order. Every output element is produced by one thread in a
+// fixed order: the backward is bitwise deterministic. Gradients ACCUMULATE into d_ent, d_rel, d_W.
+#include <math.h>
+
+#include <string>
+
+#include "kge_device.h"
+#include "kge_scan.h"
+
+namespace kge_impl {
+int set_error(int code, const char* msg);  // kge_abi.hip
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TBM = 128, TBN = 128, TBK = 16;
+constexpr int TLD = TBN + 4;
+constexpr int kMaxTsDim = 8192;
+enum TsOp { TS_FWD = 0, TS_GP = 1, TS_DH = 2 };
+
+struct TsParams {
+    const float* ent;
+    int64_t nent, ent_ld;
+    const float* rel;
+    int64_t nrel, rel_ld;
+    const float* W;     // [R, d, d]
+    const float* mask;  // [R, d, d]
+    const int64_t* pos;
+    const int64_t* neg;
+    int64_t neg_ld;
+    int64_t B, N;  // N = rows per batch row (1 for the grouped source)
+    int d;
+    float gamma;
+    float* out;
+    int64_t out_ld;
+    float2* stats;  // [B * N] (P^2, sum |p c|) per row, row id = b * N + n
+    int nchunk;
+    bool grouped;
+    // backward
+    const float* d_scores;
+    int64_t d_ld;
+    float* gp;    // [rows, d]  dL/dp
+    float* dh;    // [rows, d]  dL/dh
+    float* upart;  // [blocks, d] per-block column sums of (G / P) |p|
+    const int* rcnt;   // [R + 1] rows (batch rows) per relation bucket
+    const int* roff;   // [R + 2]
+    const int* rlist;  // [B] batch rows grouped by relation, ascending within a relation
+    float* d_ent;
+    float* d_rel;
+    float* d_W;
+    float* pdw;  // [S, R, d, d] split partials (S > 1)
+    int S, T;
+};
+
+__device__ __forceinline__ int64_t row_entity(const TsParams& p, int64_t b, int64_t n) {
+    return p.grouped ? p.pos[b * 3] : p.neg[b * p.neg_ld + n];
+}
+
+template <int VEC>
+__device__ __forceinline__ float4 ld4(const float* base, int64_t off, int lim) {
+    // lim: number of valid elements starting at off (<= 0: none)
+    if constexpr (VEC == 4) {
+        return lim > 0 ? *reinterpret_cast<const float4*>(base + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+        float4 v;
+        v.x = lim > 0 ? base[off] : 0.f;
+        v.y = lim > 1 ? base[off + 1] : 0.f;
+        v.z = lim > 2 ? base[off + 2] : 0.f;
+        v.w = lim > 3 ? base[off + 3] : 0.f;
+        return v;
+    }
+}
+
+__device__ __forceinline__ float4 mul4(float4 a, float4 b) {
+    return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+}
+
+// one K chunk of the 2 x 2-wave 128 x 128 MFMA tile from the LDS images (k-major)
+__device__ __forceinline__ void mfma_chunk(const float (*As)[TLD], const float (*Bs)[TLD], int wm, int wn, int half,
+                                           int col, f32x16 (&acc)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < TBK / 2; ++s) {
+        const int kk = 2 * s + half;
+        float a[2], bv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = As[kk][wm * 64 + i * 32 + col];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = Bs[kk][wn * 64 + j * 32 + col];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+// C/D map of the 32 x 32 MFMA: row within the wave tile for (i, register r, half-wave)
+__device__ __forceinline__ int acc_row(int wm, int i, int r, int half) {
+    return wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row-block kernel: forward scores (TS_FWD), dL/dp rows (TS_GP) or dL/dh rows (TS_DH).
+// ---------------------------------------------------------------------------------------------
+template <int OP, int VEC>
+__global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
+    __shared__ __attribute__((aligned(16))) float As[2][TBK][TLD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][TBK][TLD];
+    __shared__ const float* rowp[TBM];
+    __shared__ int rb[TBM], rn[TBM];  // (b, n) of each row; rb = -1 for padding rows
+    __shared__ float2 red[2][TBM];
+    __shared__ float sa[TBM], sbv[TBM];
+    __shared__ float wsum[kWavesPerBlock];
+    __shared__ int wcnt[kWavesPerBlock];
+    __shared__ int s_rows;
+    extern __shared__ float cs[];  // u - 1, d floats
+
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int half = lane >> 5, col = lane & 31;
+    const int d = p.d;
+    const int64_t blk = blockIdx.x;
+    const int64_t grp = blk / p.nchunk;
+    const int chunk = (int)(blk % p.nchunk);
+
+    // ---- rows of this block + its relation -----------------------------------------------------
+    int64_t r;
+    if (!p.grouped) {
+        const int64_t b = grp;
+        r = p.pos[b * 3 + 1];
+        const int64_t n0 = (int64_t)chunk * TBM;
+        const int nrows = (int)min<int64_t>(TBM, p.N - n0);
+        if (t < TBM) {
+            rb[t] = t < nrows ? (int)b : -1;
+            rn[t] = (int)(n0 + t);
+        }
+        if (t == 0) s_rows = nrows;
+    } else {
+        r = grp;  // == nrel: the out-of-range bucket
+        const int64_t skip = (int64_t)chunk * TBM;
+        int64_t seen = 0;
+        if (t < TBM) {
+            rb[t] = -1;
+            rn[t] = 0;
+        }
+        for (int64_t s = 0; s < p.B; s += kBlock) {
+            const int64_t b = s + t;
+            bool m = false;
+            if (b < p.B) {
+                const int64_t rr = p.pos[b * 3 + 1];
+                m = (r < p.nrel) ? (rr == r) : !(rr >= 0 && rr < p.nrel);
+            }
+            const uint64_t bal = __ballot(m);
+            if (lane == 0) wcnt[wave] = __popcll(bal);
+            __syncthreads();
+            int before = 0, total = 0;
+            for (int w = 0; w < kWavesPerBlock; ++w) {
+                before += (w < wave) ? wcnt[w] : 0;
+                total += wcnt[w];
+            }
+            if (m) {
+                const int64_t k = seen + before + __popcll(bal & ((1ull << lane) - 1ull)) - skip;
+                if (k >= 0 && k < TBM) rb[k] = (int)b;
+            }
+            seen += total;
+            __syncthreads();
+            if (seen >= skip + TBM) break;
+        }
+        const int64_t nrows = min<int64_t>(TBM, seen - skip);
+        if (nrows <= 0) return;  // uniform: every thread computed the same `seen`
+        if (t == 0) s_rows = (int)nrows;
+    }
+    __syncthreads();
+    const bool rok = r >= 0 && r < p.nrel;
+    if (t < TBM) {
+        const float* rp = nullptr;
+        float a = 0.f, bsc = 0.f;
+        if (rb[t] >= 0) {
+            const int64_t b = rb[t], n = rn[t];
+            const int64_t row = b * p.N + n;
+            if constexpr (OP == TS_DH) {
+                rp = p.gp + row * d;
+            } else {
+                const int64_t id = row_entity(p, b, n);
+                if (id >= 0 && id < p.nent) rp = p.ent + id * p.ent_ld;
+            }
+            if constexpr (OP == TS_GP) {
+                const float2 st = p.stats[row];
+                const float P = sqrtf(st.x);
+                a = p.d_scores[b * p.d_ld + (p.grouped ? 0 : n)] / P;
+                bsc = st.y / (P * P);
+            }
+        }
+        rowp[t] = rp;
+        sa[t] = a;
+        sbv[t] = bsc;
+    }
+
+    // ---- u - 1 for the relation row ------------------------------------------------------------
+    if constexpr (OP != TS_DH) {
+        float ss = 0.f;
+        for (int j = t; j < d; j += kBlock) {
+            const float v = rok ? p.rel[r * p.rel_ld + j] : 0.f;
+            cs[j] = v;
+            ss += v * v;
+        }
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, kWave);
+        if (lane == 0) wsum[wave] = ss;
+        __syncthreads();
+        const float rnorm = sqrtf(wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+        for (int j = t; j < d; j += kBlock) cs[j] = cs[j] / rnorm - 1.f;
+    }
+    const float* Wr = rok ? p.W + r * (int64_t)d * d : nullptr;
+    const float* Mr = rok ? p.mask + r * (int64_t)d * d : nullptr;
+    __syncthreads();
+
+    // ---- staging --------------------------------------------------------------------------------
+    // A (rows): 128 rows x 16 k, 2 float4 per thread, transposed into As[k][row].
+    // B: FWD/GP: M_r[k][col] row segments (natural k-major); DH: M_r[col][k] (transposed like A).
+    const float* arow[2];
+    int akq[2], ar[2], bkr[2], bjq[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int f = t + u * kBlock;
+        ar[u] = f >> 2;
+        akq[u] = (f & 3) * 4;
+        arow[u] = rowp[ar[u]];
+        bkr[u] = f >> 5;
+        bjq[u] = (f & 31) * 4;
+    }
+    float4 ra[2], rbv[2];
+    auto gload = [&](int ct, int k0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int ka = k0 + akq[u];
+            ra[u] = arow[u] ? ld4<VEC>(arow[u], ka, d - ka) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (OP == TS_DH) {
+                const int c = ct * TBN + ar[u];
+                if (Wr && c < d) {
+                    const int64_t off = (int64_t)c * d + ka;
+                    rbv[u] = mul4(ld4<VEC>(Wr, off, d - ka), ld4<VEC>(Mr, off, d - ka));
+                } else {
+                    rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            } else {
+                const int kb = k0 + bkr[u], j = ct * TBN + bjq[u];
+                if (Wr && kb < d) {
+                    const int64_t off = (int64_t)kb * d + j;
+                    rbv[u] = mul4(ld4<VEC>(Wr, off, d - j), ld4<VEC>(Mr, off, d - j));
+                } else {
+                    rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            As[buf][akq[u] + 0][ar[u]] = ra[u].x;
+            As[buf][akq[u] + 1][ar[u]] = ra[u].y;
+            As[buf][akq[u] + 2][ar[u]] = ra[u].z;
+            As[buf][akq[u] + 3][ar[u]] = ra[u].w;
+            if constexpr (OP == TS_DH) {
+                Bs[buf][akq[u] + 0][ar[u]] = rbv[u].x;
+                Bs[buf][akq[u] + 1][ar[u]] = rbv[u].y;
+                Bs[buf][akq[u] + 2][ar[u]] = rbv[u].z;
+                Bs[buf][akq[u] + 3][ar[u]] = rbv[u].w;
+            } else {
+                *reinterpret_cast<float4*>(&Bs[buf][bkr[u]][bjq[u]]) = rbv[u];
+            }
+        }
+    };
+
+    f32x16 acc[2][2];
+    float sq[2][16], ab[2][16];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r2 = 0; r2 < 16; ++r2) {
+            sq[i][r2] = 0.f;
+            ab[i][r2] = 0.f;
+            acc[i][0][r2] = 0.f;
+            acc[i][1][r2] = 0.f;
+        }
+
+    const int nrows = s_rows;
+    const int nk = (d + TBK - 1) / TBK, nct = (d + TBN - 1) / TBN;
+    const int iters = nk * nct;
+    gload(0, 0);
+    sstore(0);
+    __syncthreads();
+    for (int it = 0; it < iters; ++it) {
+        const int buf = it & 1;
+        const int ct = it / nk, kc = it - ct * nk;
+        if (it + 1 < iters) {
+            const int ct1 = (it + 1) / nk;
+            gload(ct1, ((it + 1) - ct1 * nk) * TBK);
+        }
+        mfma_chunk(As[buf], Bs[buf], wm, wn, half, col, acc);
+        if (kc == nk - 1) {
+            if constexpr (OP == TS_FWD) {
+                // fold the column tile into the per-row sums
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int cg = ct * TBN + wn * 64 + j * 32 + col;
+                    const float c = cg < d ? cs[cg] : 0.f;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int r2 = 0; r2 < 16; ++r2) {
+                            const float v = acc[i][j][r2];
+                            sq[i][r2] = fmaf(v, v, sq[i][r2]);
+                            ab[i][r2] += fabsf(v * c);
+                            acc[i][j][r2] = 0.f;
+                        }
+                }
+            } else if constexpr (OP == TS_GP) {
+                float up[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int cg = ct * TBN + wn * 64 + j * 32 + col;
+                    const bool cin = cg < d;
+                    const float c = cin ? cs[cg] : 0.f;
+                    up[j] = 0.f;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int r2 = 0; r2 < 16; ++r2) {
+                            const int m = acc_row(wm, i, r2, half);
+                            const float v = acc[i][j][r2];
+                            const float a = sa[m];
+                            if (cin && m < nrows)
+                                p.gp[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = a * (v * sbv[m] - sgnf(v * c) * c);
+                            up[j] += a * fabsf(v);
+                            acc[i][j][r2] = 0.f;
+                        }
+                    up[j] += __shfl_xor(up[j], 32, kWave);
+                }
+                if (half == 0) {
+                    red[wm][wn * 64 + col].x = up[0];
+                    red[wm][wn * 64 + 32 + col].x = up[1];
+                }
+                __syncthreads();
+                if (t < TBN && ct * TBN + t < d) p.upart[blk * d + ct * TBN + t] = red[0][t].x + red[1][t].x;
+            } else {  // TS_DH
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int cg = ct * TBN + wn * 64 + j * 32 + col;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int r2 = 0; r2 < 16; ++r2) {
+                            const int m = acc_row(wm, i, r2, half);
+                            if (cg < d && m < nrows) p.dh[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = acc[i][j][r2];
+                            acc[i][j][r2] = 0.f;
+                        }
+                }
+            }
+        }
+        if (it + 1 < iters) {
+            sstore(buf ^ 1);
+            __syncthreads();
+        }
+    }
+
+    if constexpr (OP == TS_FWD) {
+        // row reductions: the 32 lanes of a half-wave hold the columns of the same rows
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) {
+                float a = sq[i][r2], b = ab[i][r2];
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) {
+                    a += __shfl_xor(a, o, kWave);
+                    b += __shfl_xor(b, o, kWave);
+                }
+                if (col == 0) red[wn][acc_row(wm, i, r2, half)] = make_float2(a, b);
+            }
+        __syncthreads();
+        if (t < nrows) {
+            const float2 x = red[0][t], y = red[1][t];
+            const float s2 = x.x + y.x, l1 = x.y + y.y;
+            const int64_t b = rb[t], n = rn[t];
+            p.out[b * p.out_ld + n] = p.gamma - l1 / sqrtf(s2);
+            if (p.stats) p.stats[b * p.N + n] = make_float2(s2, l1);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Relation CSR of the batch rows: count (one block per bucket), scan (one block), ordered list.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool in_bucket(const TsParams& p, int64_t b, int64_t r) {
+    const int64_t rr = p.pos[b * 3 + 1];
+    return r < p.nrel ? rr == r : !(rr >= 0 && rr < p.nrel);
+}
+
+__global__ __launch_bounds__(kBlock) void ts_rel_count_kernel(TsParams p, int* __restrict__ cnt) {
+    __shared__ int wc[kWavesPerBlock];
+    const int64_t r = blockIdx.x;
+    int c = 0;
+    for (int64_t b = threadIdx.x; b < p.B; b += kBlock) c += in_bucket(p, b, r) ? 1 : 0;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, kWave);
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[r] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+__global__ __launch_bounds__(kBlock) void ts_rel_list_kernel(TsParams p, const int* __restrict__ off,
+                                                             int* __restrict__ list) {
+    __shared__ int wcnt[kWavesPerBlock];
+    const int64_t r = blockIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int base = off[r];
+    for (int64_t s = 0; s < p.B; s += kBlock) {
+        const int64_t b = s + t;
+        const bool m = b < p.B && in_bucket(p, b, r);
+        const uint64_t bal = __ballot(m);
+        if (lane == 0) wcnt[wave] = __popcll(bal);
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) {
+            before += (w < wave) ? wcnt[w] : 0;
+            total += wcnt[w];
+        }
+        if (m) list[base + before + __popcll(bal & ((1ull << lane) - 1ull))] = (int)b;
+        base += total;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dW: block = (relation r, tile (ti, tj) of dM_r, split s); dM_r[i][j] = sum_rows h[i] gp[j] over the
+// rows of the relation (its batch rows x N), the split's contiguous part of that row list.
+// ---------------------------------------------------------------------------------------------
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void ts_dw_kernel(TsParams p) {
+    __shared__ __attribute__((aligned(16))) float As[2][TBK][TLD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][TBK][TLD];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int half = lane >> 5, col = lane & 31;
+    const int d = p.d, T = p.T, S = p.S;
+    int64_t blk = blockIdx.x;
+    const int s = (int)(blk % S);
+    blk /= S;
+    const int tj = (int)(blk % T);
+    blk /= T;
+    const int ti = (int)(blk % T);
+    const int64_t r = blk / T;
+    const int cnt = p.rcnt[r];
+    if (cnt == 0) return;
+    const int* lst = p.rlist + p.roff[r];
+    const int64_t K = (int64_t)cnt * p.N;
+    const int64_t q0 = K * s / S, q1 = K * (s + 1) / S;
+
+    int kr[2], cq[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int f = t + u * kBlock;
+        kr[u] = f >> 5;
+        cq[u] = (f & 31) * 4;
+    }
+    float4 ra[2], rbv[2];
+    auto gload = [&](int64_t k0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int64_t q = k0 + kr[u];
+            ra[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < q1) {
+                const int64_t b = lst[q / p.N], n = q % p.N;
+                const int64_t id = row_entity(p, b, n);
+                const int i = ti * TBM + cq[u], j = tj * TBN + cq[u];
+                if (id >= 0 && id < p.nent) ra[u] = ld4<VEC>(p.ent + id * p.ent_ld, i, d - i);
+                rbv[u] = ld4<VEC>(p.gp + (b * p.N + n) * d, j, d - j);
+            }
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            *reinterpret_cast<float4*>(&As[buf][kr[u]][cq[u]]) = ra[u];
+            *reinterpret_cast<float4*>(&Bs[buf][kr[u]][cq[u]]) = rbv[u];
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r2 = 0; r2 < 16; ++r2) {
+            acc[i][0][r2] = 0.f;
+            acc[i][1][r2] = 0.f;
+        }
+    const int64_t nk = (q1 - q0 + TBK - 1) / TBK;
+    if (nk > 0) {
+        gload(q0);
+        sstore(0);
+        __syncthreads();
+        for (int64_t kc = 0; kc < nk; ++kc) {
+            const int buf = (int)(kc & 1);
+            if (kc + 1 < nk) gload(q0 + (kc + 1) * TBK);
+            mfma_chunk(As[buf], Bs[buf], wm, wn, half, col, acc);
+            if (kc + 1 < nk) {
+                sstore(buf ^ 1);
+                __syncthreads();
+            }
+        }
+    }
+    const int64_t dd = (int64_t)d * d;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int gj = tj * TBN + wn * 64 + j * 32 + col;
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) {
+                const int gi = ti * TBM + acc_row(wm, i, r2, half);
+                if (gi < d && gj < d) {
+                    const int64_t e = (int64_t)gi * d + gj;
+                    if (S == 1) {
+                        if (r < p.nrel) p.d_W[r * dd + e] += p.mask[r * dd + e] * acc[i][j][r2];
+                    } else {
+                        p.pdw[((int64_t)s * (p.nrel + 1) + r) * dd + e] = acc[i][j][r2];
+                    }
+                }
+            }
+        }
+}
+
+__global__ __launch_bounds__(kBlock) void ts_dw_reduce_kernel(TsParams p) {
+    const int64_t dd = (int64_t)p.d * p.d;
+    const int64_t total = p.nrel * dd;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += (int64_t)gridDim.x * kBlock) {
+        const int64_t r = e / dd;
+        if (p.rcnt[r] == 0) continue;
+        float v = 0.f;
+        for (int s = 0; s < p.S; ++s) v += p.pdw[((int64_t)s * (p.nrel + 1)) * dd + e];
+        p.d_W[e] += p.mask[e] * v;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// d_rel: one block per relation; g_u = sum of the block partials of the relation's row blocks in
+// block order, then the normalisation backward (g_u - u (u . g_u)) / ||r||.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void ts_drel_kernel(TsParams p) {
+    extern __shared__ float gu[];  // d floats
+    __shared__ float wsum[2][kWavesPerBlock];
+    const int64_t r = blockIdx.x;
+    const int cnt = p.rcnt[r];
+    if (cnt == 0) return;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int d = p.d;
+    const float* rr = p.rel + r * p.rel_ld;
+    float ss = 0.f, dot = 0.f;
+    for (int j = t; j < d; j += kBlock) {
+        float g = 0.f;
+        if (p.grouped) {
+            const int nb = (cnt + TBM - 1) / TBM;
+            for (int c = 0; c < nb; ++c) g += p.upart[(r * p.nchunk + c) * d + j];
+        } else {
+            const int* lst = p.rlist + p.roff[r];
+            for (int q = 0; q < cnt; ++q) {
+                const int64_t b = lst[q];
+                for (int c = 0; c < p.nchunk; ++c) g += p.upart[(b * p.nchunk + c) * d + j];
+            }
+        }
+        const float v = rr[j];
+        gu[j] = g;
+        ss += v * v;
+    }
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, kWave);
+    if (lane == 0) wsum[0][wave] = ss;
+    __syncthreads();
+    const float rn = sqrtf(wsum[0][0] + wsum[0][1] + wsum[0][2] + wsum[0][3]);
+    for (int j = t; j < d; j += kBlock) {
+        const float u = rr[j] / rn;
+        const float g = -sgnf(u - 1.f) * gu[j];
+        gu[j] = g;
+        dot += u * g;
+    }
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o, kWave);
+    if (lane == 0) wsum[1][wave] = dot;
+    __syncthreads();
+    const float ug = wsum[1][0] + wsum[1][1] + wsum[1][2] + wsum[1][3];
+    for (int j = t; j < d; j += kBlock) {
+        const float u = rr[j] / rn;
+        p.d_rel[r * p.rel_ld + j] += (gu[j] - u * ug) / rn;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// d_ent: rows bucketed by entity (count, scan, scatter), each bucket rank-sorted by row id, then one
+// wave per (entity, 256 columns) adds the bucket's dH rows in row order.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void ts_ent_count_kernel(TsParams p, int* __restrict__ count) {
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= p.B * p.N) return;
+    const int64_t id = row_entity(p, q / p.N, q % p.N);
+    if (id >= 0 && id < p.nent) atomicAdd(&count[id], 1);
+}
+
+__global__ __launch_bounds__(kBlock) void ts_ent_scatter_kernel(TsParams p, int* __restrict__ cursor,
+                                                                int* __restrict__ code) {
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= p.B * p.N) return;
+    const int64_t id = row_entity(p, q / p.N, q % p.N);
+    if (id >= 0 && id < p.nent) code[atomicAdd(&cursor[id], 1)] = (int)q;
+}
+
+__global__ __launch_bounds__(kBlock) void ts_ent_sort_kernel(int64_t E, const int* __restrict__ off,
+                                                             const int* __restrict__ code, int* __restrict__ sorted) {
+    const int64_t e = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (e >= E) return;
+    const int lane = threadIdx.x & 63;
+    const int lo = off[e], n = off[e + 1] - lo;
+    for (int i = lane; i < n; i += kWave) {  // codes are distinct: rank = # smaller
+        const int v = code[lo + i];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) rank += code[lo + j] < v ? 1 : 0;
+        sorted[lo + rank] = v;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void ts_dent_kernel(TsParams p, const int* __restrict__ off,
+                                                         const int* __restrict__ sorted) {
+    const int d = p.d;
+    const int64_t chunks = (d + 255) / 256;
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int64_t e = w / chunks;
+    if (e >= p.nent) return;
+    const int lane = threadIdx.x & 63;
+    const int c0 = (int)(w % chunks) * 256 + lane;
+    const int lo = off[e], hi = off[e + 1];
+    if (lo == hi) return;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = lo; k < hi; ++k) {
+        const float* row = p.dh + (int64_t)sorted[k] * d;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (c0 + 64 * u < d) acc[u] += row[c0 + 64 * u];
+    }
+    float* out = p.d_ent + e * p.ent_ld;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (c0 + 64 * u < d) out[c0 + 64 * u] += acc[u];
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+int check(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(KGE_EHIP, (std::string(what) + ": " + hipGetErrorString(e)).c_str());
+    return 0;
+}
+
+bool use_v4(const TsParams& p) {
+    return p.d % 4 == 0 && p.ent_ld % 4 == 0 && ((uintptr_t)p.ent & 15) == 0 && ((uintptr_t)p.W & 15) == 0 &&
+           ((uintptr_t)p.mask & 15) == 0;
+}
+
+int fill(TsParams& p, int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
+         int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+         int64_t B, int64_t N, int64_t d, float gamma) {
+    if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH && mode != KGE_SINGLE)
+        return set_error(KGE_EINVAL, "TranSparse: mode must be 0, 1 or 3");
+    if (B < 0 || N < 0 || d <= 0 || nent < 0 || nrel < 0) return set_error(KGE_EINVAL, "TranSparse: bad shape");
+    if (d > kMaxTsDim) return set_error(KGE_ENOTSUP, "TranSparse: d > 8192");
+    if (B > INT32_MAX / 4 || B * (N > 0 ? N : 1) > INT32_MAX) return set_error(KGE_EINVAL, "TranSparse: batch too large");
+    p = TsParams{};
+    p.ent = ent;
+    p.nent = nent;
+    p.ent_ld = ent_ld;
+    p.rel = rel;
+    p.nrel = nrel;
+    p.rel_ld = rel_ld;
+    p.W = W;
+    p.mask = mask;
+    p.pos = pos;
+    p.neg = neg;
+    p.neg_ld = neg_ld;
+    p.B = B;
+    p.grouped = mode != KGE_HEAD_BATCH;
+    p.N = p.grouped ? 1 : N;
+    p.d = (int)d;
+    p.gamma = gamma;
+    p.nchunk = (int)((p.grouped ? B : N) + TBM - 1) / TBM;
+    if (p.nchunk == 0) p.nchunk = 1;
+    return 0;
+}
+
+int64_t row_blocks(const TsParams& p) { return p.grouped ? (p.nrel + 1) * p.nchunk : p.B * p.nchunk; }
+
+template <int OP>
+void launch_rows(const TsParams& p, hipStream_t st) {
+    const unsigned blocks = (unsigned)row_blocks(p);
+    const size_t lds = OP == TS_DH ? 0 : (size_t)p.d * sizeof(float);
+    if (use_v4(p))
+        hipLaunchKernelGGL((ts_rows_kernel<OP, 4>), dim3(blocks), dim3(kBlock), lds, st, p);
+    else
+        hipLaunchKernelGGL((ts_rows_kernel<OP, 1>), dim3(blocks), dim3(kBlock), lds, st, p);
+}
+
+size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct TsWs {
+    float *gp, *dh, *upart, *pdw;
+    int *rcnt, *roff, *rcur, *rtiles, *rlist, *ecount, *eoff, *ecursor, *etiles, *ecode, *esorted;
+    int S;
+};
+
+int pick_splits(int64_t nrel, int T) {
+    const int64_t base = (nrel + 1) * (int64_t)T * T;
+    int S = (int)((1024 + base - 1) / base);
+    return S < 1 ? 1 : (S > 16 ? 16 : S);
+}
+
+size_t ws_layout(const TsParams& p, TsWs* w, char* base) {
+    const int64_t rows = p.B * p.N, d = p.d, E = p.nent, R = p.nrel;
+    const int T = (p.d + TBM - 1) / TBM;
+    const int S = pick_splits(R, T);
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        char* ptr = base ? base + o : nullptr;
+        o += al(bytes);
+        return ptr;
+    };
+    TsWs x;
+    x.gp = (float*)take((size_t)rows * d * 4);
+    x.dh = (float*)take((size_t)rows * d * 4);
+    x.upart = (float*)take((size_t)row_blocks(p) * d * 4);
+    x.pdw = S > 1 ? (float*)take((size_t)S * (R + 1) * d * d * 4) : nullptr;
+    x.rcnt = (int*)take((size_t)(R + 1) * 4);
+    x.roff = (int*)take((size_t)(R + 2) * 4);
+    x.rcur = (int*)take((size_t)(R + 1) * 4);
+    x.rtiles = (int*)take((size_t)((R + 1 + 1023) / 1024 + 1) * 4);
+    x.rlist = (int*)take((size_t)(p.B > 0 ? p.B : 1) * 4);
+    x.ecount = (int*)take((size_t)(E > 0 ? E : 1) * 4);
+    x.eoff = (int*)take((size_t)(E + 1) * 4);
+    x.ecursor = (int*)take((size_t)(E > 0 ? E : 1) * 4);
+    x.etiles = (int*)take((size_t)((E + 1023) / 1024 + 1) * 4);
+    x.ecode = (int*)take((size_t)(rows > 0 ? rows : 1) * 4);
+    x.esorted = (int*)take((size_t)(rows > 0 ? rows : 1) * 4);
+    x.S = S;
+    if (w) *w = x;
+    return o;
+}
+
+}  // namespace
+}  // namespace kge_impl
+
+using namespace kge_impl;
+
+extern "C" {
+
+int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
+                         int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
+                         int64_t neg_ld, int64_t B, int64_t N, int64_t d, float gamma, float* out, int64_t out_ld,
+                         float* stats, void* stream) {
+    TsParams p;
+    int rc = fill(p, mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d, gamma);
+    if (rc) return rc;
+    if (B == 0 || (!p.grouped && N == 0)) return 0;
+    if (!ent || !rel || !W || !mask || !pos || !out || (!p.grouped && !neg))
+        return set_error(KGE_EINVAL, "kge_transparse_score: null pointer");
+    if (row_blocks(p) > INT32_MAX) return set_error(KGE_EINVAL, "kge_transparse_score: grid too large");
+    p.out = out;
+    p.out_ld = out_ld;
+    p.stats = reinterpret_cast<float2*>(stats);
+    launch_rows<TS_FWD>(p, (hipStream_t)stream);
+    return check("kge_transparse_score");
+}
+
+size_t kge_transparse_bwd_workspace_size(int mode, int64_t nent, int64_t nrel, int64_t B, int64_t N, int64_t d) {
+    TsParams p;
+    if (fill(p, mode, nullptr, nent, 0, nullptr, nrel, 0, nullptr, nullptr, nullptr, nullptr, 0, B, N, d, 0.f))
+        return 0;
+    return ws_layout(p, nullptr, nullptr);
+}
+
+int kge_transparse_score_bwd(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel,
+                             int64_t nrel, int64_t rel_ld, const float* W, const float* mask, const int64_t* pos,
+                             const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t d, const float* stats,
+                             const float* d_scores, int64_t d_ld, float* d_ent, float* d_rel, float* d_W,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+    TsParams p;
+    int rc = fill(p, mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d, 0.f);
+    if (rc) return rc;
+    if (B == 0 || (!p.grouped && N == 0)) return 0;
+    if (!ent || !rel || !W || !mask || !pos || (!p.grouped && !neg) || !stats || !d_scores || !d_ent || !d_rel ||
+        !d_W || !workspace)
+        return set_error(KGE_EINVAL, "kge_transparse_score_bwd: null pointer");
+    TsWs w;
+    const size_t need = ws_layout(p, &w, (char*)workspace);
+    if (workspace_bytes < need) return set_error(KGE_EINVAL, "kge_transparse_score_bwd: workspace too small");
+    if (row_blocks(p) > INT32_MAX) return set_error(KGE_EINVAL, "kge_transparse_score_bwd: grid too large");
+    hipStream_t st = (hipStream_t)stream;
+    p.stats = reinterpret_cast<float2*>(const_cast<float*>(stats));
+    p.d_scores = d_scores;
+    p.d_ld = d_ld;
+    p.gp = w.gp;
+    p.dh = w.dh;
+    p.upart = w.upart;
+    p.pdw = w.pdw;
+    p.rcnt = w.rcnt;
+    p.roff = w.roff;
+    p.rlist = w.rlist;
+    p.d_ent = d_ent;
+    p.d_rel = d_rel;
+    p.d_W = d_W;
+    p.S = w.S;
+    p.T = (p.d + TBM - 1) / TBM;
+    const int64_t rows = p.B * p.N;
+    // relation CSR
+    hipLaunchKernelGGL(ts_rel_count_kernel, dim3((unsigned)(nrel + 1)), dim3(kBlock), 0, st, p, w.rcnt);
+    launch_exclusive_scan(w.rcnt, nrel + 1, w.roff, w.rcur, w.rtiles, st);
+    hipLaunchKernelGGL(ts_rel_list_kernel, dim3((unsigned)(nrel + 1)), dim3(kBlock), 0, st, p, w.roff, w.rlist);
+    // dL/dp rows + g_u partials, then dL/dh rows
+    launch_rows<TS_GP>(p, st);
+    launch_rows<TS_DH>(p, st);
+    // dW
+    const int64_t dwb = (nrel + 1) * (int64_t)p.T * p.T * p.S;
+    if (dwb > INT32_MAX) return set_error(KGE_EINVAL, "kge_transparse_score_bwd: dW grid too large");
+    if (use_v4(p))
+        hipLaunchKernelGGL(ts_dw_kernel<4>, dim3((unsigned)dwb), dim3(kBlock), 0, st, p);
+    else
+        hipLaunchKernelGGL(ts_dw_kernel<1>, dim3((unsigned)dwb), dim3(kBlock), 0, st, p);
+    if (p.S > 1) hipLaunchKernelGGL(ts_dw_reduce_kernel, dim3(2048), dim3(kBlock), 0, st, p);
+    // d_rel
+    hipLaunchKernelGGL(ts_drel_kernel, dim3((unsigned)nrel), dim3(kBlock), (size_t)p.d * 4, st, p);
+    // d_ent
+    if (nent > 0) {
+        if (hipMemsetAsync(w.ecount, 0, (size_t)nent * 4, st) != hipSuccess) return check("memset");
+        const unsigned rb = (unsigned)((rows + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(ts_ent_count_kernel, dim3(rb), dim3(kBlock), 0, st, p, w.ecount);
+        launch_exclusive_scan(w.ecount, nent, w.eoff, w.ecursor, w.etiles, st);
+        hipLaunchKernelGGL(ts_ent_scatter_kernel, dim3(rb), dim3(kBlock), 0, st, p, w.ecursor, w.ecode);
+        hipLaunchKernelGGL(ts_ent_sort_kernel, dim3((unsigned)((nent + kWavesPerBlock - 1) / kWavesPerBlock)),
+                           dim3(kBlock), 0, st, nent, w.eoff, w.ecode, w.esorted);
+        const int64_t waves = nent * ((p.d + 255) / 256);
+        hipLaunchKernelGGL(ts_dent_kernel, dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)),
+                           dim3(kBlock), 0, st, p, w.eoff, w.esorted);
+    }
+    return check("kge_transparse_score_bwd");
+}
+
+}  // extern "C"

@@ -55,6 +55,17 @@ def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor
     if out is None:
         out = torch.empty((B, E), dtype=torch.float32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
+    if model.model_name == "TranSparse":
+        # head-batch: every entity as the head (stride-0 candidate rows); tail-batch scores do not
+        # depend on the tail (Q9), so the [B, 1] score is broadcast to every candidate
+        if m == HEAD_BATCH:
+            cand = torch.arange(E, device=dev, dtype=torch.int64).unsqueeze(0).expand(B, E)
+            return ops.transparse_score_raw(m, ent, rel, model.W.detach(), model.mask, positive_sample, cand,
+                                            model._gamma_f, out=out)
+        s = ops.transparse_score_raw(m, ent, rel, model.W.detach(), model.mask, positive_sample, None,
+                                     model._gamma_f)
+        out.copy_(s.expand(B, E))
+        return out
     if model.model_name in MFMA_FNS:
         K = ent.shape[1]
         Q = torch.empty((B, K), dtype=torch.float32, device=dev)

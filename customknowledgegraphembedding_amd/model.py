@@ -46,7 +46,10 @@ def _dims_for(model_name, entity_dim, relation_dim):
             raise ValueError("InterHT needs -de and -tr (entity 2d, relation 3d)")
         return entity_dim // 2, entity_dim // 2
     if model_name == "TranSparse":
-        raise NotImplementedError("TranSparse (model.py:226-235) has no HIP kernel yet")
+        # model.py:227: head [.., d] @ (mask * W)[d, d] and the relation row of width d
+        if entity_dim != relation_dim:
+            raise ValueError("TranSparse needs entity_dim == relation_dim")
+        return entity_dim, 0
     raise ValueError(f"model {model_name} not supported")
 
 
@@ -59,13 +62,16 @@ class _KGEBase(nn.Module):
         rel = torch.empty(nrelation, relation_dim).uniform_(-init_range, init_range, generator=g)
         self.entity_embedding = nn.Parameter(ent.to(device))
         self.relation_embedding = nn.Parameter(rel.to(device))
+        return g
 
     def _make_model_func(self):
         def plugin(name):
-            fn = FN_IDS[name]
+            fn = FN_IDS.get(name)
 
             def model_func(head, relation, tail, mode, *extra):
                 m = ops.mode_id(mode)
+                if name == "TranSparse":
+                    return self._transparse_dense(head, relation, m, *extra)
                 ew = head.shape[-1]
                 D = ew // 2 if name in SPLIT_ENTITY else ew
                 rel_off = D if name == "InterHT" else 0
@@ -76,10 +82,35 @@ class _KGEBase(nn.Module):
             model_func.__name__ = name
             return model_func
 
-        return {name: plugin(name) for name in FN_IDS}
+        return {name: plugin(name) for name in list(FN_IDS) + ["TranSparse"]}
+
+    def _transparse_dense(self, head, relation, mode, weight, mask):
+        """model_func['TranSparse'](head, relation, tail, mode, weight, mask) on pre-gathered rows
+        (model.py:226-235): the gathered tensors become the kernel's tables, indexed 0..rows-1."""
+        B, d = head.shape[0], head.shape[-1]
+        dev = head.device
+        ar = torch.arange(B, device=dev, dtype=torch.int64)
+        pos = torch.stack([ar, ar, ar], dim=1)
+        rel = relation.reshape(B, d)
+        if mode == HEAD_BATCH:
+            N = head.shape[1]
+            ent = head.reshape(B * N, d)
+            neg = torch.arange(B * N, device=dev, dtype=torch.int64).view(B, N)
+        else:
+            ent = head.reshape(B, d)
+            neg = None
+        return ops.transparse_score(mode, ent.contiguous(), rel.contiguous(), weight.contiguous(),
+                                    mask.contiguous().to(torch.float32), pos, neg, self._gamma_f)
 
     # fused gather + score (no [B, N, d] tensor is ever built)
+    @property
+    def supports_fused_step(self):
+        return self.model_name in FN_IDS
+
     def score(self, mode, positive_sample, negative_sample=None):
+        if self.model_name == "TranSparse":
+            return ops.transparse_score(mode, self.entity_embedding, self.relation_embedding, self.W, self.mask,
+                                        positive_sample, negative_sample, self._gamma_f)
         fn = FN_IDS[self.model_name]
         modulus = self.modulus if self.model_name == "pRotatE" else None
         return ops.score_indexed(fn, mode, self.entity_embedding, self.relation_embedding,
@@ -122,7 +153,14 @@ class TFKGEModel(_KGEBase):
         self.entity_dim, self.relation_dim = entity_dim, relation_dim
 
         # model.py:86-91 (Q8): U(-(gamma+2)/d, (gamma+2)/d) for both tables (torch RNG, seeded)
-        self._init_tables(nentity, nrelation, entity_dim, relation_dim, float(rng[0]), device, seed)
+        g = self._init_tables(nentity, nrelation, entity_dim, relation_dim, float(rng[0]), device, seed)
+        if model_name == "TranSparse":
+            # model.py:96-106: per relation a fixed 0/1 mask (uniform[1, 100) >= int(0.5 * 100)) and a
+            # trainable W [R, rd, rd] drawn with the same initializer (torch RNG, seeded)
+            prob = torch.empty(nrelation, relation_dim, relation_dim).uniform_(1.0, 100.0, generator=g)
+            self.register_buffer("mask", (prob >= 50).to(torch.float32).to(device))
+            W = torch.empty(nrelation, relation_dim, relation_dim).uniform_(-float(rng[0]), float(rng[0]), generator=g)
+            self.W = nn.Parameter(W.to(device))
         if model_name == "InterHT":
             self.u = 1  # model.py:94-95 (the kernel hard-codes u = 1)
         if model_name == "pRotatE":
@@ -150,6 +188,8 @@ class TFKGEModel(_KGEBase):
         m = ops.mode_id(mode)
         if m == SINGLE:
             raise ValueError("step_forward needs the batch's negative mode")
+        if self.model_name == "TranSparse":
+            return self(((positive_sample, negative_sample), m)), self(((positive_sample, negative_sample), SINGLE))
         modulus = self.modulus if self.model_name == "pRotatE" else None
         neg, pos = ops.step_forward(FN_IDS[self.model_name], m, self.entity_embedding,
                                     self.relation_embedding, positive_sample, negative_sample,
@@ -169,6 +209,8 @@ class TFKGEModel(_KGEBase):
 
         if not isinstance(optimizer, Adam):
             raise TypeError("train_step_fused needs customknowledgegraphembedding_amd.optim.Adam")
+        if not self.supports_fused_step:
+            raise NotImplementedError(f"{self.model_name} has no fused train step; use the autograd path")
         m = ops.mode_id(mode)
         fn = FN_IDS[self.model_name]
         ent, rel = self.entity_embedding, self.relation_embedding

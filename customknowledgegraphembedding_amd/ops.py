@@ -224,6 +224,55 @@ def log_sigmoid_raw(x):
     return out
 
 
+
+def transparse_score_raw(mode, ent, rel, W, mask, pos, neg, gamma, stats=None, out=None):
+    """TranSparse raw scores (model.py:226-235): [B, N] for head-batch, [B, 1] for single and
+    tail-batch (Q9). `stats` (optional [rows, 2] fp32) receives the per-row backward statistics."""
+    _need_gpu(ent, rel, W, mask, pos, neg)
+    for t, n in ((ent, "ent"), (rel, "rel"), (W, "W"), (mask, "mask")):
+        _fp32(t, n)
+    _i64(pos, "pos")
+    if not (W.is_contiguous() and mask.is_contiguous()):
+        raise ValueError("W and mask must be contiguous [R, d, d]")
+    m = mode_id(mode)
+    B, d = pos.shape[0], ent.shape[1]
+    if rel.shape[1] != d or tuple(W.shape) != (rel.shape[0], d, d) or W.shape != mask.shape:
+        raise ValueError("TranSparse needs entity_dim == relation_dim == d and W, mask [R, d, d]")
+    if pos.stride(1) != 1 or pos.stride(0) != 3:
+        pos = pos.contiguous()
+    head = m == HEAD_BATCH
+    N = neg.shape[1] if head else 1
+    if head:
+        _i64(neg, "neg")
+        if neg.stride(1) != 1:
+            neg = neg.contiguous()
+    if out is None:
+        out = torch.empty((B, N), dtype=torch.float32, device=ent.device)
+    rc = _lib.load().kge_transparse_score(
+        m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), W.data_ptr(),
+        mask.data_ptr(), pos.data_ptr(), neg.data_ptr() if head else None, neg.stride(0) if head else 0, B, N, d,
+        float(gamma), out.data_ptr(), out.stride(0), None if stats is None else stats.data_ptr(), _stream(ent.device))
+    check(rc, "kge_transparse_score")
+    return out
+
+
+def transparse_score_bwd_raw(mode, ent, rel, W, mask, pos, neg, stats, d_scores, d_ent, d_rel, d_W):
+    """Accumulates the TranSparse gradients into d_ent, d_rel, d_W (deterministic)."""
+    m = mode_id(mode)
+    B, d = pos.shape[0], ent.shape[1]
+    head = m == HEAD_BATCH
+    N = neg.shape[1] if head else 1
+    d_scores = d_scores.contiguous() if d_scores.stride(-1) != 1 else d_scores
+    lib = _lib.load()
+    nbytes = lib.kge_transparse_bwd_workspace_size(m, ent.shape[0], rel.shape[0], B, N, d)
+    ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=ent.device)
+    rc = lib.kge_transparse_score_bwd(
+        m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), W.data_ptr(),
+        mask.data_ptr(), pos.data_ptr(), neg.data_ptr() if head else None, neg.stride(0) if head else 0, B, N, d,
+        stats.data_ptr(), d_scores.data_ptr(), d_scores.stride(0), d_ent.data_ptr(), d_rel.data_ptr(),
+        d_W.data_ptr(), ws.data_ptr(), ws.numel(), _stream(ent.device))
+    check(rc, "kge_transparse_score_bwd")
+
 # ----------------------------------------------------------------------------------------------
 # autograd
 # ----------------------------------------------------------------------------------------------
@@ -365,6 +414,35 @@ class _StepForward(torch.autograd.Function):
         if d_mod is not None:
             d_mod = d_mod.view(mod_shape)
         return (d_ent, d_rel, d_mod) + (None,) * 11
+
+
+class _TranSparse(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ent, rel, W, mask, pos, neg, mode, gamma):
+        m = mode_id(mode)
+        pos = pos.contiguous()
+        neg = neg.contiguous() if (m == HEAD_BATCH) else None
+        rows = pos.shape[0] * (neg.shape[1] if neg is not None else 1)
+        stats = torch.empty((rows, 2), dtype=torch.float32, device=ent.device)
+        out = transparse_score_raw(m, ent, rel, W, mask, pos, neg, gamma, stats=stats)
+        ctx.save_for_backward(ent, rel, W, mask, pos, neg if neg is not None else pos, stats)
+        ctx.cfg = (m, neg is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_scores):
+        ent, rel, W, mask, pos, neg, stats = ctx.saved_tensors
+        m, has_neg = ctx.cfg
+        d_ent, d_rel, d_W = torch.zeros_like(ent), torch.zeros_like(rel), torch.zeros_like(W)
+        transparse_score_bwd_raw(m, ent, rel, W, mask, pos, neg if has_neg else None, stats, d_scores, d_ent, d_rel,
+                                 d_W)
+        return d_ent, d_rel, d_W, None, None, None, None, None
+
+
+def transparse_score(mode, ent, rel, W, mask, pos, neg, gamma):
+    """TranSparse gather + score (model.py:139-142,161-164,187-190,226-235), differentiable w.r.t.
+    ent, rel and W -> [B, N] (head-batch) or [B, 1] (single / tail-batch)."""
+    return _TranSparse.apply(ent, rel, W, mask, pos, neg, mode, float(gamma))
 
 
 def step_forward(fn, mode, ent, rel, pos, neg, D, gamma, emb_range, rel_off=0, modulus=None,

@@ -81,7 +81,8 @@ class Trainer:
             # this package's Adam over exactly the model's parameters in one group
             from .optim import Adam
             fused = (isinstance(optimizer, Adam) and strategy.num_replicas_in_sync == 1
-                     and hasattr(model, "train_step_fused") and len(optimizer.param_groups) == 1
+                     and hasattr(model, "train_step_fused") and getattr(model, "supports_fused_step", False)
+                     and len(optimizer.param_groups) == 1
                      and {id(p) for p in optimizer.param_groups[0]["params"] if p.requires_grad}
                      == {id(p) for p in model.parameters() if p.requires_grad})
         self.fused = bool(fused)

@@ -251,6 +251,35 @@ int kge_step_backward_adam(int fn, int mode,
                            void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
+ * TranSparse scores (tensorflow_codes/model.py:226-235, gathers at :139-142, :161-164, :187-190; tables
+ * :96-106) on the fp32 matrix cores. W and mask are [nrel, d, d] row-major contiguous; the score reads the
+ * whole relation row (d floats, rel_ld stride) and needs entity_dim == relation_dim == d.
+ *   mode KGE_HEAD_BATCH: out[b*out_ld + n] for n < N, head = E[neg[b*neg_ld + n]], relation pos[b,1]
+ *   mode KGE_SINGLE / KGE_TAIL_BATCH: out[b*out_ld] only (the reference's [B, 1]: Q9 makes the score
+ *        depend on the head alone, so tail-batch ignores the negatives); neg may be NULL.
+ * Out-of-range ids read zero rows (scores NaN from the zero-norm normalisation, as on TF-GPU).
+ * stats (may be NULL): per row float2 (||p||^2, sum_j |p_j c_j|) for the backward.
+ * d <= 8192. Deterministic (no atomics).
+ */
+int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
+                         int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
+                         int64_t neg_ld, int64_t B, int64_t N, int64_t d, float gamma, float* out, int64_t out_ld,
+                         float* stats, void* stream);
+/*
+ * Backward of kge_transparse_score's raw scores (autograd of model.py:226-235 through the gathers).
+ *   stats     [B*N] (head-batch) or [B] (single/tail) float2 written by the forward (stats != NULL)
+ *   d_scores  dL/dscore, row b at d_scores + b*d_ld (column 0 only for single/tail)
+ *   d_ent [nent, ent_ld], d_rel [nrel, rel_ld], d_W [nrel, d, d]: gradients are ADDED (+=)
+ * Bitwise deterministic (no float atomics). Workspace: kge_transparse_bwd_workspace_size bytes.
+ */
+size_t kge_transparse_bwd_workspace_size(int mode, int64_t nent, int64_t nrel, int64_t B, int64_t N, int64_t d);
+int kge_transparse_score_bwd(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
+                             int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
+                             int64_t neg_ld, int64_t B, int64_t N, int64_t d, const float* stats, const float* d_scores,
+                             int64_t d_ld, float* d_ent, float* d_rel, float* d_W, void* workspace,
+                             size_t workspace_bytes, void* stream);
+
+/*
  * Negative sampler of the training batches (host memory, no GPU): the upstream KnowledgeGraphEmbedding
  * TrainDataset (call sites compress_data/main.py:64-73), bit-exact with its numpy code for the same RNG
  * state: negatives from numpy's legacy MT19937 `randint` (seeded like np.random.seed(seed)), filtered by

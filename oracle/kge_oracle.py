@@ -181,6 +181,26 @@ def score(name, ent, rel, pos, neg, mode, gamma, embedding_range=None, modulus=N
     return model_func(name, head, relation, tail, mode, gamma, embedding_range, modulus)
 
 
+def transparse_score(ent, rel, W, mask, pos, neg, mode, gamma):
+    """TranSparse branches of TFKGEModel (model.py:127-192 with the W/mask gathers of :139-142,
+    :161-164, :187-190): raw scores [B, N] (head-batch) or [B, 1] (single, tail-batch: Q9)."""
+    head, relation, tail = gather_rows(ent, rel, pos, neg, mode)
+    b_W = W[pos[:, 1]]
+    b_mask = mask[pos[:, 1]]
+    return transparse(head, relation, tail, mode, gamma, b_W, b_mask)
+
+
+def tf_call_transparse(ent, rel, W, mask, pos, neg, mode, gamma):
+    """TFKGEModel.call for TranSparse, all three branches blended as model.py:114-125 does."""
+    p_score = F.logsigmoid(transparse_score(ent, rel, W, mask, pos, neg, 3, gamma))
+    head_score = adv_reduce(transparse_score(ent, rel, W, mask, pos, neg, 0, gamma))
+    tail_score = adv_reduce(transparse_score(ent, rel, W, mask, pos, neg, 1, gamma))
+    negative_condition = 1.0 if mode == 0 else 0.0
+    n_score = head_score * negative_condition + tail_score * (1 - negative_condition)
+    condition = 1.0 if mode == 3 else 0.0
+    return p_score * condition + n_score * (1 - condition)
+
+
 def adv_reduce(s, temperature=1.0):
     """model.py:168-171 / 195-198 (Q3): sum softmax(s*T) * logsigmoid(-s), keepdims."""
     return torch.sum(torch.softmax(s * temperature, dim=1) * F.logsigmoid(-s), dim=1, keepdim=True)

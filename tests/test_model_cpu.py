@@ -47,7 +47,25 @@ def test_upstream_model_validation():
 def test_dims_for_errors():
     with pytest.raises(ValueError):
         _dims_for("TransE", 10, 20)
-    with pytest.raises(NotImplementedError):
-        _dims_for("TranSparse", 10, 10)
+    assert _dims_for("TranSparse", 10, 10) == (10, 0)
+    with pytest.raises(ValueError):
+        _dims_for("TranSparse", 20, 10)
     with pytest.raises(ValueError):
         _dims_for("Nope", 10, 10)
+
+
+def test_transparse_tables_cpu():
+    """model.py:96-106: mask [R, d, d] of 0/1 with rate 0.5, W [R, d, d] trainable; d_ent == d_rel."""
+    from customknowledgegraphembedding_amd.model import TFKGEModel
+
+    m = TFKGEModel("TranSparse", 20, 3, 16, 12.0, device="cpu", seed=0)
+    assert m.W.shape == (3, 16, 16) and m.W.requires_grad
+    assert m.mask.shape == (3, 16, 16) and not m.mask.requires_grad
+    assert set(m.mask.unique().tolist()) <= {0.0, 1.0}
+    rng = (12.0 + 2.0) / 16
+    assert float(m.W.abs().max()) <= rng
+    assert not m.supports_fused_step
+    assert "TranSparse" in m.model_func
+    import pytest
+    with pytest.raises(ValueError):
+        TFKGEModel("TranSparse", 20, 3, 16, 12.0, double_entity_embedding=True, device="cpu")

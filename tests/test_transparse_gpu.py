@@ -1,0 +1,156 @@
+"""TranSparse (tensorflow_codes/model.py:96-106,139-142,161-164,187-190,226-235) on the GPU: the MFMA
+forward and the deterministic backward through the C-ABI against the fp64 oracle (torch autograd on
+the same fp32 inputs). Scores: |got - ref| <= 1e-4 * max(1, |ref|). Gradients: |got - ref| <=
+1e-4 * max|ref| per tensor (fp32 sums over up to d * N terms)."""
+import numpy as np
+import pytest
+import torch
+
+from customknowledgegraphembedding_amd import ops
+from customknowledgegraphembedding_amd.model import TFKGEModel
+from oracle import kge_oracle as O
+from tests.conftest import rel_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tables(E, R, d, seed=0, gamma=12.0):
+    g = torch.Generator().manual_seed(seed)
+    rng = (gamma + 2.0) / d
+    ent = torch.empty(E, d).uniform_(-rng, rng, generator=g)
+    rel = torch.empty(R, d).uniform_(-rng, rng, generator=g)
+    W = torch.empty(R, d, d).uniform_(-rng, rng, generator=g)
+    mask = (torch.empty(R, d, d).uniform_(1, 100, generator=g) >= 50).float()
+    return ent, rel, W, mask
+
+
+def _batch(E, R, B, N, seed=1):
+    g = np.random.RandomState(seed)
+    pos = np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1).astype(np.int64)
+    neg = g.randint(E, size=(B, N)).astype(np.int64)
+    return torch.from_numpy(pos), torch.from_numpy(neg)
+
+
+def _oracle(ent, rel, W, mask, pos, neg, mode, gamma, grad=None):
+    t = [x.double().requires_grad_(True) for x in (ent, rel, W)]
+    s = O.transparse_score(t[0], t[1], t[2], mask.double(), pos, neg, mode, gamma)
+    if grad is None:
+        return s.detach().numpy(), None
+    (s * grad.double()).sum().backward()
+    return s.detach().numpy(), [x.grad.numpy() for x in t]
+
+
+CASES = [  # (E, R, d, B, N)
+    (97, 3, 8, 4, 16),
+    (61, 2, 50, 5, 7),       # d % 4 != 0: scalar loads
+    (200, 5, 130, 6, 200),   # partial K/column tiles, 2 row chunks per batch row
+    (300, 2, 256, 300, 3),   # > 128 batch rows per relation: grouped chunks
+]
+
+
+@pytest.mark.parametrize("E,R,d,B,N", CASES)
+@pytest.mark.parametrize("mode", [0, 1, 3])
+def test_forward_parity(E, R, d, B, N, mode):
+    gamma = 12.0
+    ent, rel, W, mask = _tables(E, R, d)
+    pos, neg = _batch(E, R, B, N)
+    ref, _ = _oracle(ent, rel, W, mask, pos, neg, mode, gamma)
+    got = ops.transparse_score_raw(mode, ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV), pos.to(DEV),
+                                   neg.to(DEV), gamma)
+    torch.cuda.synchronize()
+    got = got.cpu().numpy()
+    assert got.shape == ref.shape
+    assert rel_close(got, ref) <= 1e-4
+
+
+@pytest.mark.parametrize("E,R,d,B,N", CASES)
+@pytest.mark.parametrize("mode", [0, 1, 3])
+def test_backward_parity_and_determinism(E, R, d, B, N, mode):
+    gamma = 12.0
+    ent, rel, W, mask = _tables(E, R, d, seed=3)
+    pos, neg = _batch(E, R, B, N, seed=4)
+    Nc = N if mode == 0 else 1
+    grad = torch.from_numpy(np.random.RandomState(5).randn(B, Nc).astype(np.float32))
+    _, ref = _oracle(ent, rel, W, mask, pos, neg, mode, gamma, grad)
+    outs = []
+    for _ in range(2):
+        t = [x.to(DEV).requires_grad_(True) for x in (ent, rel, W)]
+        s = ops.transparse_score(mode, t[0], t[1], t[2], mask.to(DEV), pos.to(DEV), neg.to(DEV), gamma)
+        s.backward(grad.to(DEV))
+        torch.cuda.synchronize()
+        outs.append([x.grad.cpu().numpy() for x in t])
+    for name, g, r in zip(("d_ent", "d_rel", "d_W"), outs[0], ref):
+        scale = max(np.abs(r).max(), 1e-30)
+        assert np.abs(g - r).max() <= 1e-4 * scale, name
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)  # bitwise deterministic
+
+
+def test_out_of_range_ids_give_nan_rows():
+    E, R, d, B, N = 50, 3, 16, 4, 5
+    ent, rel, W, mask = _tables(E, R, d)
+    pos, neg = _batch(E, R, B, N)
+    neg[1, 2] = E + 5        # zero entity row -> NaN score
+    pos[2, 1] = R + 1        # zero relation -> NaN row
+    got = ops.transparse_score_raw(0, ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV), pos.to(DEV), neg.to(DEV),
+                                   12.0).cpu().numpy()
+    assert np.isnan(got[1, 2]) and np.isnan(got[2]).all()
+    ok = np.ones_like(got, dtype=bool)
+    ok[1, 2] = False
+    ok[2] = False
+    assert np.isfinite(got[ok]).all()
+    got1 = ops.transparse_score_raw(3, ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV), pos.to(DEV), None,
+                                    12.0).cpu().numpy()
+    assert np.isnan(got1[2, 0]) and np.isfinite(np.delete(got1, 2, 0)).all()
+
+
+def test_model_call_and_plugin_match_oracle():
+    E, R, hd, B, N = 120, 4, 32, 6, 10
+    m = TFKGEModel("TranSparse", E, R, hd, 12.0, device=DEV, seed=7)
+    assert m.W.shape == (R, hd, hd) and 0.4 < float(m.mask.mean()) < 0.6
+    pos, neg = _batch(E, R, B, N, seed=9)
+    pd, nd = pos.to(DEV), neg.to(DEV)
+    ent, rel, W, mask = (x.detach().cpu() for x in (m.entity_embedding, m.relation_embedding, m.W, m.mask))
+    for mode in (0, 1, 3):
+        got = m(((pd, nd), mode)).detach().cpu().numpy()
+        ref = O.tf_call_transparse(ent.double(), rel.double(), W.double(), mask.double(), pos, neg, mode, 12.0)
+        assert rel_close(got, ref.numpy()) <= 1e-4
+    # model_func plugin on pre-gathered tensors (model.py:161-164)
+    head = m.entity_embedding[nd]
+    relation = m.relation_embedding[pd[:, 1]].unsqueeze(1)
+    tail = m.entity_embedding[pd[:, 2]].unsqueeze(1)
+    s = m.model_func["TranSparse"](head, relation, tail, 0, m.W[pd[:, 1]], m.mask[pd[:, 1]])
+    ref = O.transparse(head.detach().cpu().double(), relation.detach().cpu().double(), None, "head-batch", 12.0,
+                       W[pos[:, 1]].double(), mask[pos[:, 1]].double())
+    assert rel_close(s.detach().cpu().numpy(), ref.numpy()) <= 1e-4
+
+
+def test_trainer_step_matches_oracle_loss():
+    from customknowledgegraphembedding_amd.optim import Adam
+    from customknowledgegraphembedding_amd.supervisor import Strategy, Sum, Trainer
+
+    E, R, hd, B, N = 90, 3, 24, 8, 12
+    m = TFKGEModel("TranSparse", E, R, hd, 12.0, device=DEV, seed=11)
+    ent, rel, W, mask = (x.detach().cpu().double() for x in (m.entity_embedding, m.relation_embedding, m.W, m.mask))
+    pos, neg = _batch(E, R, B, N, seed=13)
+    w = torch.rand(B, 1, generator=torch.Generator().manual_seed(1))
+    mode = torch.zeros(B, dtype=torch.int64)
+    opt = Adam([m.entity_embedding, m.relation_embedding, m.W], lr=1e-3)
+    tr = Trainer(Strategy(), None, m, opt, Sum())
+    assert not tr.fused
+    loss = tr.train_step(iter([(pos, neg, w, mode)]))
+    t = [x.clone().requires_grad_(True) for x in (ent, rel, W)]
+    wd = w.double().reshape(-1, 1)
+    ns = O.tf_call_transparse(t[0], t[1], t[2], mask, pos, neg, 0, 12.0)
+    ps = O.tf_call_transparse(t[0], t[1], t[2], mask, pos, neg, 3, 12.0)
+    ref = (-(wd * ps).sum() / wd.sum() - (wd * ns).sum() / wd.sum()) / 2
+    assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+    ref.backward()
+    # one Keras Adam step from zero moments: every touched coordinate moves by ~lr * sign(g)
+    for p0, prm, g in zip((ent, rel, W), (m.entity_embedding, m.relation_embedding, m.W), (t[0].grad, t[1].grad,
+                                                                                            t[2].grad)):
+        exp, _, _ = O.keras_adam_step(p0, g, torch.zeros_like(p0), torch.zeros_like(p0), 1, 1e-3)
+        got = prm.detach().cpu().double()
+        big = g.abs() > 1e-6 * float(g.abs().max())
+        assert torch.allclose(got[big], exp[big], atol=1e-6)

@@ -233,12 +233,13 @@ def transparse_bench(w, a, device):
 
     def step(b, ev=None):
         pos, neg = b
+        M = ops.transparse_premul(W, mask) if ops._want_premul(W, pos, neg, 0) else None
         if ev is not None:
             ev[0].record()
-        ns = ops.transparse_score_raw(0, ent, rel, W, mask, pos, neg, m._gamma_f)
+        ns = ops.transparse_score_raw(0, ent, rel, W, mask, pos, neg, m._gamma_f, M=M)
         if ev is not None:
             ev[1].record()
-        ps = ops.transparse_score_raw(3, ent, rel, W, mask, pos, None, m._gamma_f)
+        ps = ops.transparse_score_raw(3, ent, rel, W, mask, pos, None, m._gamma_f, M=M)
         return ops.neg_reduce_raw(ns), ops.log_sigmoid_raw(ps.reshape(-1))
 
     for i in range(a.warmup):

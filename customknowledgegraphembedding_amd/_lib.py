@@ -99,7 +99,8 @@ SIGNATURES = {
     "kge_transparse_score": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_i64,
                                     _c_i64, _c_i64, _c_i64, _c_f, _c_p, _c_i64, _c_p, _c_p]),
     "kge_transparse_bwd_workspace_size": (ctypes.c_size_t, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
-    "kge_transparse_score_bwd": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p,
+    "kge_transparse_premul": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p]),
+    "kge_transparse_score_bwd": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p,
                                         _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p,
                                         ctypes.c_size_t, _c_p]),
     "kge_crc32c": (ctypes.c_uint32, [_c_p, _c_i64]),

@@ -48,7 +48,8 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int TBM = 128, TBN = 128, TBK = 16;
+constexpr int TBM = 128, TBN = 128, TBK = 32;
+constexpr int NU = TBK / 8;  // float4 per thread per operand and K chunk
 constexpr int TLD = TBN + 4;
 constexpr int kMaxTsDim = 8192;
 enum TsOp { TS_FWD = 0, TS_GP = 1, TS_DH = 2 };
@@ -60,6 +61,7 @@ struct TsParams {
     int64_t nrel, rel_ld;
     const float* W;     // [R, d, d]
     const float* mask;  // [R, d, d]
+    const float* Mpre;  // [R, d, d] mask * W precomputed, or null (then the product is fused in the loads)
     const int64_t* pos;
     const int64_t* neg;
     int64_t neg_ld;
@@ -142,7 +144,8 @@ __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
     __shared__ __attribute__((aligned(16))) float Bs[2][TBK][TLD];
     __shared__ const float* rowp[TBM];
     __shared__ int rb[TBM], rn[TBM];  // (b, n) of each row; rb = -1 for padding rows
-    __shared__ float2 red[2][TBM];
+    __shared__ float2 red[TBM];
+    __shared__ float colred[kWavesPerBlock][TBN];
     __shared__ float sa[TBM], sbv[TBM];
     __shared__ float wsum[kWavesPerBlock];
     __shared__ int wcnt[kWavesPerBlock];
@@ -150,7 +153,6 @@ __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
     extern __shared__ float cs[];  // u - 1, d floats
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
     const int half = lane >> 5, col = lane & 31;
     const int d = p.d;
     const int64_t blk = blockIdx.x;
@@ -244,43 +246,37 @@ __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
         const float rnorm = sqrtf(wsum[0] + wsum[1] + wsum[2] + wsum[3]);
         for (int j = t; j < d; j += kBlock) cs[j] = cs[j] / rnorm - 1.f;
     }
-    const float* Wr = rok ? p.W + r * (int64_t)d * d : nullptr;
-    const float* Mr = rok ? p.mask + r * (int64_t)d * d : nullptr;
+    const float* Wr = rok ? (p.Mpre ? p.Mpre : p.W) + r * (int64_t)d * d : nullptr;
+    const float* Mr = (rok && !p.Mpre) ? p.mask + r * (int64_t)d * d : nullptr;
     __syncthreads();
 
     // ---- staging --------------------------------------------------------------------------------
-    // A (rows): 128 rows x 16 k, 2 float4 per thread, transposed into As[k][row].
+    // A (rows): 128 rows x TBK k, NU float4 per thread, transposed into As[k][row].
     // B: FWD/GP: M_r[k][col] row segments (natural k-major); DH: M_r[col][k] (transposed like A).
-    const float* arow[2];
-    int akq[2], ar[2], bkr[2], bjq[2];
+    // thread t, unit u: A row = (t >> 3) + 32 u, k offset (t & 7) * 4; B k row = (t >> 5) + 8 u, col (t & 31) * 4
+    const int akq = (t & 7) * 4, bjq = (t & 31) * 4;
+    const float* arow[NU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int f = t + u * kBlock;
-        ar[u] = f >> 2;
-        akq[u] = (f & 3) * 4;
-        arow[u] = rowp[ar[u]];
-        bkr[u] = f >> 5;
-        bjq[u] = (f & 31) * 4;
-    }
-    float4 ra[2], rbv[2];
+    for (int u = 0; u < NU; ++u) arow[u] = rowp[(t >> 3) + 32 * u];
+    float4 ra[NU], rbv[NU];
     auto gload = [&](int ct, int k0) {
+        const int ka = k0 + akq;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int ka = k0 + akq[u];
+        for (int u = 0; u < NU; ++u) {
             ra[u] = arow[u] ? ld4<VEC>(arow[u], ka, d - ka) : make_float4(0.f, 0.f, 0.f, 0.f);
             if constexpr (OP == TS_DH) {
-                const int c = ct * TBN + ar[u];
+                const int c = ct * TBN + (t >> 3) + 32 * u;
                 if (Wr && c < d) {
                     const int64_t off = (int64_t)c * d + ka;
-                    rbv[u] = mul4(ld4<VEC>(Wr, off, d - ka), ld4<VEC>(Mr, off, d - ka));
+                    rbv[u] = Mr ? mul4(ld4<VEC>(Wr, off, d - ka), ld4<VEC>(Mr, off, d - ka)) : ld4<VEC>(Wr, off, d - ka);
                 } else {
                     rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
             } else {
-                const int kb = k0 + bkr[u], j = ct * TBN + bjq[u];
+                const int kb = k0 + (t >> 5) + 8 * u, j = ct * TBN + bjq;
                 if (Wr && kb < d) {
                     const int64_t off = (int64_t)kb * d + j;
-                    rbv[u] = mul4(ld4<VEC>(Wr, off, d - j), ld4<VEC>(Mr, off, d - j));
+                    rbv[u] = Mr ? mul4(ld4<VEC>(Wr, off, d - j), ld4<VEC>(Mr, off, d - j)) : ld4<VEC>(Wr, off, d - j);
                 } else {
                     rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
@@ -289,33 +285,35 @@ __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
     };
     auto sstore = [&](int buf) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            As[buf][akq[u] + 0][ar[u]] = ra[u].x;
-            As[buf][akq[u] + 1][ar[u]] = ra[u].y;
-            As[buf][akq[u] + 2][ar[u]] = ra[u].z;
-            As[buf][akq[u] + 3][ar[u]] = ra[u].w;
+        for (int u = 0; u < NU; ++u) {
+            const int ar = (t >> 3) + 32 * u;
+            As[buf][akq + 0][ar] = ra[u].x;
+            As[buf][akq + 1][ar] = ra[u].y;
+            As[buf][akq + 2][ar] = ra[u].z;
+            As[buf][akq + 3][ar] = ra[u].w;
             if constexpr (OP == TS_DH) {
-                Bs[buf][akq[u] + 0][ar[u]] = rbv[u].x;
-                Bs[buf][akq[u] + 1][ar[u]] = rbv[u].y;
-                Bs[buf][akq[u] + 2][ar[u]] = rbv[u].z;
-                Bs[buf][akq[u] + 3][ar[u]] = rbv[u].w;
+                Bs[buf][akq + 0][ar] = rbv[u].x;
+                Bs[buf][akq + 1][ar] = rbv[u].y;
+                Bs[buf][akq + 2][ar] = rbv[u].z;
+                Bs[buf][akq + 3][ar] = rbv[u].w;
             } else {
-                *reinterpret_cast<float4*>(&Bs[buf][bkr[u]][bjq[u]]) = rbv[u];
+                *reinterpret_cast<float4*>(&Bs[buf][(t >> 5) + 8 * u][bjq]) = rbv[u];
             }
         }
     };
 
-    f32x16 acc[2][2];
-    float sq[2][16], ab[2][16];
+    // wave w: rows [32 w, 32 w + 32) x all 128 columns of the tile (four 32 x 32 MFMA accumulators);
+    // C/D map: row = 32 w + (r & 3) + 8 (r >> 2) + 4 (lane >> 5), column = 32 j + (lane & 31)
+    f32x16 acc[4];
+    float sq[16], ab[16];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int r2 = 0; r2 < 16; ++r2) {
+        sq[r2] = 0.f;
+        ab[r2] = 0.f;
 #pragma unroll
-        for (int r2 = 0; r2 < 16; ++r2) {
-            sq[i][r2] = 0.f;
-            ab[i][r2] = 0.f;
-            acc[i][0][r2] = 0.f;
-            acc[i][1][r2] = 0.f;
-        }
+        for (int j = 0; j < 4; ++j) acc[j][r2] = 0.f;
+    }
+    auto row_of = [&](int r2) { return wave * 32 + (r2 & 3) + 8 * (r2 >> 2) + 4 * half; };
 
     const int nrows = s_rows;
     const int nk = (d + TBK - 1) / TBK, nct = (d + TBN - 1) / TBN;
@@ -330,64 +328,64 @@ __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
             const int ct1 = (it + 1) / nk;
             gload(ct1, ((it + 1) - ct1 * nk) * TBK);
         }
-        mfma_chunk(As[buf], Bs[buf], wm, wn, half, col, acc);
+#pragma unroll
+        for (int s2 = 0; s2 < TBK / 2; ++s2) {
+            const int kk = 2 * s2 + half;
+            const float a = As[buf][kk][wave * 32 + col];
+            float bv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bv[j] = Bs[buf][kk][j * 32 + col];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv[j], acc[j], 0, 0, 0);
+        }
         if (kc == nk - 1) {
             if constexpr (OP == TS_FWD) {
                 // fold the column tile into the per-row sums
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int cg = ct * TBN + wn * 64 + j * 32 + col;
+                for (int j = 0; j < 4; ++j) {
+                    const int cg = ct * TBN + j * 32 + col;
                     const float c = cg < d ? cs[cg] : 0.f;
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int r2 = 0; r2 < 16; ++r2) {
-                            const float v = acc[i][j][r2];
-                            sq[i][r2] = fmaf(v, v, sq[i][r2]);
-                            ab[i][r2] += fabsf(v * c);
-                            acc[i][j][r2] = 0.f;
-                        }
+                    for (int r2 = 0; r2 < 16; ++r2) {
+                        const float v = acc[j][r2];
+                        sq[r2] = fmaf(v, v, sq[r2]);
+                        ab[r2] += fabsf(v * c);
+                        acc[j][r2] = 0.f;
+                    }
                 }
             } else if constexpr (OP == TS_GP) {
-                float up[2];
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int cg = ct * TBN + wn * 64 + j * 32 + col;
+                for (int j = 0; j < 4; ++j) {
+                    const int cg = ct * TBN + j * 32 + col;
                     const bool cin = cg < d;
                     const float c = cin ? cs[cg] : 0.f;
-                    up[j] = 0.f;
+                    float up = 0.f;
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int r2 = 0; r2 < 16; ++r2) {
-                            const int m = acc_row(wm, i, r2, half);
-                            const float v = acc[i][j][r2];
-                            const float a = sa[m];
-                            if (cin && m < nrows)
-                                p.gp[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = a * (v * sbv[m] - sgnf(v * c) * c);
-                            up[j] += a * fabsf(v);
-                            acc[i][j][r2] = 0.f;
-                        }
-                    up[j] += __shfl_xor(up[j], 32, kWave);
-                }
-                if (half == 0) {
-                    red[wm][wn * 64 + col].x = up[0];
-                    red[wm][wn * 64 + 32 + col].x = up[1];
+                    for (int r2 = 0; r2 < 16; ++r2) {
+                        const int m = row_of(r2);
+                        const float v = acc[j][r2];
+                        const float a = sa[m];
+                        if (cin && m < nrows)
+                            p.gp[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = a * (v * sbv[m] - sgnf(v * c) * c);
+                        up += a * fabsf(v);
+                        acc[j][r2] = 0.f;
+                    }
+                    up += __shfl_xor(up, 32, kWave);
+                    if (half == 0) colred[wave][j * 32 + col] = up;
                 }
                 __syncthreads();
-                if (t < TBN && ct * TBN + t < d) p.upart[blk * d + ct * TBN + t] = red[0][t].x + red[1][t].x;
+                if (t < TBN && ct * TBN + t < d)
+                    p.upart[blk * d + ct * TBN + t] = (colred[0][t] + colred[1][t]) + (colred[2][t] + colred[3][t]);
             } else {  // TS_DH
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int cg = ct * TBN + wn * 64 + j * 32 + col;
+                for (int j = 0; j < 4; ++j) {
+                    const int cg = ct * TBN + j * 32 + col;
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int r2 = 0; r2 < 16; ++r2) {
-                            const int m = acc_row(wm, i, r2, half);
-                            if (cg < d && m < nrows) p.dh[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = acc[i][j][r2];
-                            acc[i][j][r2] = 0.f;
-                        }
+                    for (int r2 = 0; r2 < 16; ++r2) {
+                        const int m = row_of(r2);
+                        if (cg < d && m < nrows) p.dh[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = acc[j][r2];
+                        acc[j][r2] = 0.f;
+                    }
                 }
             }
         }
@@ -400,26 +398,29 @@ __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
     if constexpr (OP == TS_FWD) {
         // row reductions: the 32 lanes of a half-wave hold the columns of the same rows
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int r2 = 0; r2 < 16; ++r2) {
+            float a = sq[r2], b = ab[r2];
 #pragma unroll
-            for (int r2 = 0; r2 < 16; ++r2) {
-                float a = sq[i][r2], b = ab[i][r2];
-#pragma unroll
-                for (int o = 16; o > 0; o >>= 1) {
-                    a += __shfl_xor(a, o, kWave);
-                    b += __shfl_xor(b, o, kWave);
-                }
-                if (col == 0) red[wn][acc_row(wm, i, r2, half)] = make_float2(a, b);
+            for (int o = 16; o > 0; o >>= 1) {
+                a += __shfl_xor(a, o, kWave);
+                b += __shfl_xor(b, o, kWave);
             }
+            if (col == 0) red[row_of(r2)] = make_float2(a, b);
+        }
         __syncthreads();
         if (t < nrows) {
-            const float2 x = red[0][t], y = red[1][t];
-            const float s2 = x.x + y.x, l1 = x.y + y.y;
+            const float2 x = red[t];
             const int64_t b = rb[t], n = rn[t];
-            p.out[b * p.out_ld + n] = p.gamma - l1 / sqrtf(s2);
-            if (p.stats) p.stats[b * p.N + n] = make_float2(s2, l1);
+            p.out[b * p.out_ld + n] = p.gamma - x.y / sqrtf(x.x);
+            if (p.stats) p.stats[b * p.N + n] = x;
         }
     }
+}
+
+__global__ __launch_bounds__(kBlock) void ts_premul_kernel(const float4* __restrict__ W, const float4* __restrict__ mask,
+                                                          float4* __restrict__ M, int64_t n4) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock)
+        M[i] = mul4(W[i], mask[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -489,24 +490,19 @@ __global__ __launch_bounds__(kBlock) void ts_dw_kernel(TsParams p) {
     const int64_t K = (int64_t)cnt * p.N;
     const int64_t q0 = K * s / S, q1 = K * (s + 1) / S;
 
-    int kr[2], cq[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int f = t + u * kBlock;
-        kr[u] = f >> 5;
-        cq[u] = (f & 31) * 4;
-    }
-    float4 ra[2], rbv[2];
+    // thread t, unit u: k row (t >> 5) + 8 u of the chunk, columns (t & 31) * 4 .. + 3
+    const int cq = (t & 31) * 4;
+    float4 ra[NU], rbv[NU];
     auto gload = [&](int64_t k0) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int64_t q = k0 + kr[u];
+        for (int u = 0; u < NU; ++u) {
+            const int64_t q = k0 + (t >> 5) + 8 * u;
             ra[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (q < q1) {
                 const int64_t b = lst[q / p.N], n = q % p.N;
                 const int64_t id = row_entity(p, b, n);
-                const int i = ti * TBM + cq[u], j = tj * TBN + cq[u];
+                const int i = ti * TBM + cq, j = tj * TBN + cq;
                 if (id >= 0 && id < p.nent) ra[u] = ld4<VEC>(p.ent + id * p.ent_ld, i, d - i);
                 rbv[u] = ld4<VEC>(p.gp + (b * p.N + n) * d, j, d - j);
             }
@@ -514,9 +510,9 @@ __global__ __launch_bounds__(kBlock) void ts_dw_kernel(TsParams p) {
     };
     auto sstore = [&](int buf) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            *reinterpret_cast<float4*>(&As[buf][kr[u]][cq[u]]) = ra[u];
-            *reinterpret_cast<float4*>(&Bs[buf][kr[u]][cq[u]]) = rbv[u];
+        for (int u = 0; u < NU; ++u) {
+            *reinterpret_cast<float4*>(&As[buf][(t >> 5) + 8 * u][cq]) = ra[u];
+            *reinterpret_cast<float4*>(&Bs[buf][(t >> 5) + 8 * u][cq]) = rbv[u];
         }
     };
 
@@ -694,7 +690,7 @@ int check(const char* what) {
 
 bool use_v4(const TsParams& p) {
     return p.d % 4 == 0 && p.ent_ld % 4 == 0 && ((uintptr_t)p.ent & 15) == 0 && ((uintptr_t)p.W & 15) == 0 &&
-           ((uintptr_t)p.mask & 15) == 0;
+           ((uintptr_t)p.mask & 15) == 0 && ((uintptr_t)p.Mpre & 15) == 0;
 }
 
 int fill(TsParams& p, int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
@@ -799,8 +795,9 @@ int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_l
     int rc = fill(p, mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d, gamma);
     if (rc) return rc;
     if (B == 0 || (!p.grouped && N == 0)) return 0;
-    if (!ent || !rel || !W || !mask || !pos || !out || (!p.grouped && !neg))
+    if (!ent || !rel || !W || !pos || !out || (!p.grouped && !neg))
         return set_error(KGE_EINVAL, "kge_transparse_score: null pointer");
+    if (!mask) p.Mpre = W;  // W already holds mask * W
     if (row_blocks(p) > INT32_MAX) return set_error(KGE_EINVAL, "kge_transparse_score: grid too large");
     p.out = out;
     p.out_ld = out_ld;
@@ -816,8 +813,23 @@ size_t kge_transparse_bwd_workspace_size(int mode, int64_t nent, int64_t nrel, i
     return ws_layout(p, nullptr, nullptr);
 }
 
+int kge_transparse_premul(const float* W, const float* mask, int64_t n, float* M, void* stream) {
+    if (n < 0) return set_error(KGE_EINVAL, "kge_transparse_premul: bad size");
+    if (n == 0) return 0;
+    if (!W || !mask || !M || n % 4 || ((uintptr_t)W & 15) || ((uintptr_t)mask & 15) || ((uintptr_t)M & 15))
+        return set_error(KGE_EINVAL, "kge_transparse_premul: needs 16-byte aligned buffers and n % 4 == 0");
+    const int64_t n4 = n / 4;
+    const int64_t nb = (n4 + kBlock - 1) / kBlock;
+    const unsigned blocks = (unsigned)(nb < 4096 ? nb : 4096);
+    hipLaunchKernelGGL(ts_premul_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(W), reinterpret_cast<const float4*>(mask),
+                       reinterpret_cast<float4*>(M), n4);
+    return check("kge_transparse_premul");
+}
+
 int kge_transparse_score_bwd(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel,
-                             int64_t nrel, int64_t rel_ld, const float* W, const float* mask, const int64_t* pos,
+                             int64_t nrel, int64_t rel_ld, const float* W, const float* mask, const float* M,
+                             const int64_t* pos,
                              const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t d, const float* stats,
                              const float* d_scores, int64_t d_ld, float* d_ent, float* d_rel, float* d_W,
                              void* workspace, size_t workspace_bytes, void* stream) {
@@ -833,6 +845,7 @@ int kge_transparse_score_bwd(int mode, const float* ent, int64_t nent, int64_t e
     if (workspace_bytes < need) return set_error(KGE_EINVAL, "kge_transparse_score_bwd: workspace too small");
     if (row_blocks(p) > INT32_MAX) return set_error(KGE_EINVAL, "kge_transparse_score_bwd: grid too large");
     hipStream_t st = (hipStream_t)stream;
+    p.Mpre = M;
     p.stats = reinterpret_cast<float2*>(const_cast<float*>(stats));
     p.d_scores = d_scores;
     p.d_ld = d_ld;

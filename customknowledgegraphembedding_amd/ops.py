@@ -225,9 +225,27 @@ def log_sigmoid_raw(x):
 
 
 
-def transparse_score_raw(mode, ent, rel, W, mask, pos, neg, gamma, stats=None, out=None):
+def transparse_premul(W, mask):
+    """M = mask * W (kge_transparse_premul)."""
+    M = torch.empty_like(W)
+    check(_lib.load().kge_transparse_premul(W.data_ptr(), mask.data_ptr(), W.numel(), M.data_ptr(),
+                                            _stream(W.device)), "kge_transparse_premul")
+    return M
+
+
+def _want_premul(W, pos, neg, mode):
+    """Premultiply the relation matrices when there are fewer of them than row blocks: one pass over
+    R*d*d floats then saves every block the mask reads."""
+    if W.numel() % 4 or W.data_ptr() % 16:
+        return False
+    rows = pos.shape[0] * (neg.shape[1] if (mode_id(mode) == HEAD_BATCH and neg is not None) else 1)
+    return W.shape[0] * 4 <= max(1, rows // 128)
+
+
+def transparse_score_raw(mode, ent, rel, W, mask, pos, neg, gamma, stats=None, out=None, M=None):
     """TranSparse raw scores (model.py:226-235): [B, N] for head-batch, [B, 1] for single and
-    tail-batch (Q9). `stats` (optional [rows, 2] fp32) receives the per-row backward statistics."""
+    tail-batch (Q9). `stats` (optional [rows, 2] fp32) receives the per-row backward statistics.
+    `M` (optional) = transparse_premul(W, mask), used instead of forming mask * W in the loads."""
     _need_gpu(ent, rel, W, mask, pos, neg)
     for t, n in ((ent, "ent"), (rel, "rel"), (W, "W"), (mask, "mask")):
         _fp32(t, n)
@@ -256,7 +274,7 @@ def transparse_score_raw(mode, ent, rel, W, mask, pos, neg, gamma, stats=None, o
     return out
 
 
-def transparse_score_bwd_raw(mode, ent, rel, W, mask, pos, neg, stats, d_scores, d_ent, d_rel, d_W):
+def transparse_score_bwd_raw(mode, ent, rel, W, mask, pos, neg, stats, d_scores, d_ent, d_rel, d_W, M=None):
     """Accumulates the TranSparse gradients into d_ent, d_rel, d_W (deterministic)."""
     m = mode_id(mode)
     B, d = pos.shape[0], ent.shape[1]
@@ -268,8 +286,8 @@ def transparse_score_bwd_raw(mode, ent, rel, W, mask, pos, neg, stats, d_scores,
     ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=ent.device)
     rc = lib.kge_transparse_score_bwd(
         m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), W.data_ptr(),
-        mask.data_ptr(), pos.data_ptr(), neg.data_ptr() if head else None, neg.stride(0) if head else 0, B, N, d,
-        stats.data_ptr(), d_scores.data_ptr(), d_scores.stride(0), d_ent.data_ptr(), d_rel.data_ptr(),
+        mask.data_ptr(), None if M is None else M.data_ptr(), pos.data_ptr(), neg.data_ptr() if head else None,
+        neg.stride(0) if head else 0, B, N, d, stats.data_ptr(), d_scores.data_ptr(), d_scores.stride(0), d_ent.data_ptr(), d_rel.data_ptr(),
         d_W.data_ptr(), ws.data_ptr(), ws.numel(), _stream(ent.device))
     check(rc, "kge_transparse_score_bwd")
 
@@ -424,18 +442,20 @@ class _TranSparse(torch.autograd.Function):
         neg = neg.contiguous() if (m == HEAD_BATCH) else None
         rows = pos.shape[0] * (neg.shape[1] if neg is not None else 1)
         stats = torch.empty((rows, 2), dtype=torch.float32, device=ent.device)
-        out = transparse_score_raw(m, ent, rel, W, mask, pos, neg, gamma, stats=stats)
-        ctx.save_for_backward(ent, rel, W, mask, pos, neg if neg is not None else pos, stats)
-        ctx.cfg = (m, neg is not None)
+        M = transparse_premul(W, mask) if _want_premul(W, pos, neg, m) else None
+        out = transparse_score_raw(m, ent, rel, W, mask, pos, neg, gamma, stats=stats, M=M)
+        ctx.save_for_backward(ent, rel, W, mask, pos, neg if neg is not None else pos, stats,
+                              M if M is not None else stats)
+        ctx.cfg = (m, neg is not None, M is not None)
         return out
 
     @staticmethod
     def backward(ctx, d_scores):
-        ent, rel, W, mask, pos, neg, stats = ctx.saved_tensors
-        m, has_neg = ctx.cfg
+        ent, rel, W, mask, pos, neg, stats, M = ctx.saved_tensors
+        m, has_neg, has_m = ctx.cfg
         d_ent, d_rel, d_W = torch.zeros_like(ent), torch.zeros_like(rel), torch.zeros_like(W)
         transparse_score_bwd_raw(m, ent, rel, W, mask, pos, neg if has_neg else None, stats, d_scores, d_ent, d_rel,
-                                 d_W)
+                                 d_W, M=M if has_m else None)
         return d_ent, d_rel, d_W, None, None, None, None, None
 
 

@@ -259,6 +259,7 @@ int kge_step_backward_adam(int fn, int mode,
  *        depend on the head alone, so tail-batch ignores the negatives); neg may be NULL.
  * Out-of-range ids read zero rows (scores NaN from the zero-norm normalisation, as on TF-GPU).
  * stats (may be NULL): per row float2 (||p||^2, sum_j |p_j c_j|) for the backward.
+ * mask may be NULL: W then already holds mask * W (kge_transparse_premul), which halves the matrix reads.
  * d <= 8192. Deterministic (no atomics).
  */
 int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
@@ -269,12 +270,16 @@ int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_l
  * Backward of kge_transparse_score's raw scores (autograd of model.py:226-235 through the gathers).
  *   stats     [B*N] (head-batch) or [B] (single/tail) float2 written by the forward (stats != NULL)
  *   d_scores  dL/dscore, row b at d_scores + b*d_ld (column 0 only for single/tail)
+ *   M         mask * W from kge_transparse_premul, or NULL (the product is then formed on the fly)
  *   d_ent [nent, ent_ld], d_rel [nrel, rel_ld], d_W [nrel, d, d]: gradients are ADDED (+=)
  * Bitwise deterministic (no float atomics). Workspace: kge_transparse_bwd_workspace_size bytes.
  */
+/* M[i] = mask[i] * W[i] for n floats (n % 4 == 0, 16-byte aligned): the premultiplied relation matrices. */
+int kge_transparse_premul(const float* W, const float* mask, int64_t n, float* M, void* stream);
 size_t kge_transparse_bwd_workspace_size(int mode, int64_t nent, int64_t nrel, int64_t B, int64_t N, int64_t d);
 int kge_transparse_score_bwd(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
-                             int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
+                             int64_t rel_ld, const float* W, const float* mask, const float* M, const int64_t* pos,
+                             const int64_t* neg,
                              int64_t neg_ld, int64_t B, int64_t N, int64_t d, const float* stats, const float* d_scores,
                              int64_t d_ld, float* d_ent, float* d_rel, float* d_W, void* workspace,
                              size_t workspace_bytes, void* stream);

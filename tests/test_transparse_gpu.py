@@ -51,13 +51,15 @@ CASES = [  # (E, R, d, B, N)
 
 @pytest.mark.parametrize("E,R,d,B,N", CASES)
 @pytest.mark.parametrize("mode", [0, 1, 3])
-def test_forward_parity(E, R, d, B, N, mode):
+@pytest.mark.parametrize("premul", [False, True])
+def test_forward_parity(E, R, d, B, N, mode, premul):
     gamma = 12.0
     ent, rel, W, mask = _tables(E, R, d)
     pos, neg = _batch(E, R, B, N)
     ref, _ = _oracle(ent, rel, W, mask, pos, neg, mode, gamma)
-    got = ops.transparse_score_raw(mode, ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV), pos.to(DEV),
-                                   neg.to(DEV), gamma)
+    Wd, md = W.to(DEV), mask.to(DEV)
+    M = ops.transparse_premul(Wd, md) if premul and d % 4 == 0 else None
+    got = ops.transparse_score_raw(mode, ent.to(DEV), rel.to(DEV), Wd, md, pos.to(DEV), neg.to(DEV), gamma, M=M)
     torch.cuda.synchronize()
     got = got.cpu().numpy()
     assert got.shape == ref.shape
@@ -85,6 +87,25 @@ def test_backward_parity_and_determinism(E, R, d, B, N, mode):
         assert np.abs(g - r).max() <= 1e-4 * scale, name
     for a, b in zip(outs[0], outs[1]):
         assert np.array_equal(a, b)  # bitwise deterministic
+
+
+def test_backward_with_premultiplied_matrices_is_identical():
+    E, R, d, B, N = 200, 2, 64, 8, 40
+    ent, rel, W, mask = (x.to(DEV) for x in _tables(E, R, d, seed=21))
+    pos, neg = (x.to(DEV) for x in _batch(E, R, B, N, seed=22))
+    g = torch.randn(B, N, device=DEV)
+    st = torch.empty(B * N, 2, device=DEV)
+    M = ops.transparse_premul(W, mask)
+    s0 = ops.transparse_score_raw(0, ent, rel, W, mask, pos, neg, 12.0, stats=st)
+    s1 = ops.transparse_score_raw(0, ent, rel, W, mask, pos, neg, 12.0, M=M)
+    assert torch.equal(s0, s1)
+    grads = []
+    for MM in (None, M):
+        d = [torch.zeros_like(ent), torch.zeros_like(rel), torch.zeros_like(W)]
+        ops.transparse_score_bwd_raw(0, ent, rel, W, mask, pos, neg, st, g, *d, M=MM)
+        grads.append(d)
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
 
 
 def test_out_of_range_ids_give_nan_rows():

@@ -52,7 +52,10 @@ __global__ __launch_bounds__(kBlock) void eval_query_kernel(ScoreParams p, float
 // LDS images are k-major ([k][m]) so a wave's fragment read (lanes 0-31 one k, 32-63 the next)
 // is 32 consecutive dwords per half-wave: conflict-free ds_read_b32.
 // ---------------------------------------------------------------------------------------------
-constexpr int GBM = 128, GBN = 128, GBK = 16;
+constexpr int GBM = 128, GBN = 128, GBK = 16;  // BK = 32 measured 92 vs 96 TFLOP/s at C5
+constexpr int GNU = GBK / 8;      // float4 per thread per operand and K chunk
+constexpr int GTPR = GBK / 4;     // threads per staged row
+constexpr int GRPP = kBlock / GTPR;  // rows staged per unit
 constexpr int GLD = GBM + 4;  // padded LDS row (floats)
 
 __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
@@ -73,14 +76,15 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __rest
     const int tn = bid / ntm, tm = bid % ntm;
     const int m0 = tm * GBM, n0 = tn * GBN;
 
-    // global -> register staging: 128 rows x 16 floats per operand = 512 float4, 2 per thread
-    float4 ra[2], rb[2];
+    // global -> register staging: 128 rows x GBK floats per operand = GNU float4 per thread
+    // (thread t, unit u: row t / GTPR + GRPP u, k offset (t % GTPR) * 4)
+    float4 ra[GNU], rb[GNU];
+    const int kq = (t % GTPR) * 4;
     auto gload = [&](int k0) {
+        const int ka = k0 + kq;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int f = t + u * kBlock;
-            const int r = f >> 2, kq = (f & 3) * 4;
-            const int ka = k0 + kq;
+        for (int u = 0; u < GNU; ++u) {
+            const int r = t / GTPR + GRPP * u;
             const int gm = m0 + r, gn = n0 + r;
             ra[u] = (gm < M && ka < K) ? *reinterpret_cast<const float4*>(A + (int64_t)gm * lda + ka)
                                        : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -90,9 +94,8 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __rest
     };
     auto sstore = [&](int buf) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int f = t + u * kBlock;
-            const int r = f >> 2, kq = (f & 3) * 4;
+        for (int u = 0; u < GNU; ++u) {
+            const int r = t / GTPR + GRPP * u;
             As[buf][kq + 0][r] = ra[u].x;
             As[buf][kq + 1][r] = ra[u].y;
             As[buf][kq + 2][r] = ra[u].z;

@@ -67,6 +67,22 @@ WORKLOADS = {
 }
 
 
+def pmc_traffic(workload, kernel_prefix):
+    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 --pmc summary of this
+    workload (profiles/pmc_<workload>.json, scripts/pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x 2
+    + WRITE_SIZE, the gfx950 corrections). None when no summary was committed."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"pmc_{workload}.json")
+    try:
+        with open(path) as f:
+            rows = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    for row in rows:
+        if row.get("kernel", "").startswith(kernel_prefix) and "hbm_read_bytes_corrected" in row:
+            return row["hbm_read_bytes_corrected"] + row.get("hbm_write_bytes", 0.0), os.path.relpath(path)
+    return None, None
+
+
 def dims(w):
     d = w["hidden_dim"]
     ent = 2 * d if w["de"] else d
@@ -456,6 +472,7 @@ def main():
         elapsed = float(t.item())
 
     neg_bytes, pos_bytes = algorithmic_bytes(w)
+    traffic, traffic_src = pmc_traffic(a.workload, "score_fwd_kernel")
     kern_avg_s = statistics.mean(kern_ms) / 1e3
     achieved = neg_bytes / kern_avg_s / 1e9
     triples = (B * N + B) * a.steps * world
@@ -477,7 +494,8 @@ def main():
         "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N, "hidden_dim": w["hidden_dim"],
                    "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "traffic_source": traffic_src,
                      "kernel": "score_fwd_kernel (negatives)", "kernel_avg_us": kern_avg_s * 1e6,
                      "algorithmic_bytes_per_launch": neg_bytes},
     }

@@ -8,6 +8,7 @@ import os
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc/c2"
+json_out = sys.argv[2] if len(sys.argv) > 2 else None
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
@@ -32,3 +33,9 @@ for line in out:
     for c, v in line.items():
         if c != "kernel":
             print(f"    {c:28s} {v:,.1f}")
+
+if json_out:
+    import json
+    with open(json_out, "w") as f:
+        json.dump({"source": root, "correction": "FETCH_SIZE kB x 1024 x 2 (gfx950, MI355X_MICROARCH.md HBM); "
+                   "WRITE_SIZE kB x 1024", "kernels": out}, f, indent=1)

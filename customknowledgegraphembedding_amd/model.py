@@ -223,8 +223,11 @@ class TFKGEModel(_KGEBase):
         sw = torch.sum(w)
         loss = (-torch.sum(w * out_pos) / sw - torch.sum(w * out_neg) / sw) / 2
         d_out = ((-0.5 / sw) * w).contiguous()  # the op order autograd uses for this loss
+        from .optim import resolve_lr
+
         group = optimizer.param_groups[0]
-        lr = group["lr"]() if callable(group["lr"]) else group["lr"]
+        st0 = optimizer.state[self.entity_embedding]
+        lr = resolve_lr(group["lr"], st0["step"] if st0 else 0)
         b1, b2 = group["betas"]
         params = [ent, rel] + ([self.modulus] if is_p else [])
         for prm in params:

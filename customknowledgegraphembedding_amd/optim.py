@@ -6,10 +6,47 @@ into the step size; semantics="torch": torch.optim.Adam's update (eps added to s
 """
 from __future__ import annotations
 
+import inspect
+
 import torch
 
 from . import _lib
 from ._lib import check
+
+
+def lrfn(epoch, num_replicas=1):
+    """run.py:69-84: linear warm-up over 5 epochs from 1e-5 to 5e-5 * replicas, then 0.8 ** epoch decay
+    towards 1e-5 (evaluated in float like the @tf.function)."""
+    LR_START, LR_MAX, LR_MIN = 0.00001, 0.00005 * num_replicas, 0.00001
+    LR_RAMPUP_EPOCHS, LR_SUSTAIN_EPOCHS, LR_EXP_DECAY = 5.0, 0.0, 0.8
+    if float(epoch) < LR_RAMPUP_EPOCHS:
+        return (LR_MAX - LR_START) / LR_RAMPUP_EPOCHS * float(epoch) + LR_START
+    if float(epoch) < LR_RAMPUP_EPOCHS + LR_SUSTAIN_EPOCHS:
+        return LR_MAX
+    return (LR_MAX - LR_MIN) * LR_EXP_DECAY ** (float(epoch) - LR_RAMPUP_EPOCHS - LR_SUSTAIN_EPOCHS) + LR_MIN
+
+
+class LRSchedule:
+    """run.py:106-108: `lrfn(epoch=step // steps_per_epoch)` as a Keras LearningRateSchedule; Adam
+    calls it with the number of updates already applied (Keras' `optimizer.iterations`)."""
+
+    def __init__(self, steps_per_epoch, num_replicas=1):
+        self.steps_per_epoch = int(steps_per_epoch)
+        self.num_replicas = int(num_replicas)
+
+    def __call__(self, step):
+        return lrfn(int(step) // self.steps_per_epoch, self.num_replicas)
+
+
+def resolve_lr(lr, iterations):
+    """A float, a zero-argument callable, or a schedule called with the prior update count."""
+    if not callable(lr):
+        return float(lr)
+    try:
+        n = len(inspect.signature(lr).parameters)
+    except (TypeError, ValueError):
+        n = 1
+    return float(lr(iterations) if n else lr())
 
 
 class Adam(torch.optim.Optimizer):
@@ -28,7 +65,8 @@ class Adam(torch.optim.Optimizer):
                 loss = closure()
         lib = _lib.load()
         for group in self.param_groups:
-            lr = group["lr"]() if callable(group["lr"]) else group["lr"]
+            first = next((self.state[q] for q in group["params"] if q.grad is not None and self.state[q]), None)
+            lr = resolve_lr(group["lr"], first["step"] if first else 0)
             b1, b2 = group["betas"]
             for p in group["params"]:
                 if p.grad is None:

@@ -27,3 +27,16 @@ def test_lrfn_schedule_run_py():
     assert abs(O.lrfn(6) - ((5e-5 - 1e-5) * 0.8 + 1e-5)) < 1e-12
     assert abs(O.lrfn(0, num_replicas=8) - 1e-5) < 1e-12
     assert abs(O.lrfn(5, num_replicas=8) - 4e-4) < 1e-12
+
+
+def test_lr_schedule_matches_reference_formula():
+    """run.py:69-84 (lrfn) and :106-108 (LRSchedule: epoch = step // steps_per_epoch)."""
+    from customknowledgegraphembedding_amd.optim import LRSchedule, lrfn, resolve_lr
+    from oracle import kge_oracle as O
+
+    for e in range(12):
+        assert lrfn(e) == O.lrfn(e)
+        assert lrfn(e, 8) == O.lrfn(e, 8)
+    s = LRSchedule(steps_per_epoch=100)
+    assert resolve_lr(s, 0) == lrfn(0) and resolve_lr(s, 250) == lrfn(2)
+    assert resolve_lr(lambda: 0.5, 7) == 0.5 and resolve_lr(0.25, 3) == 0.25

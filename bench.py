@@ -474,6 +474,12 @@ def main():
     neg_bytes, pos_bytes = algorithmic_bytes(w)
     traffic, traffic_src = pmc_traffic(a.workload, "score_fwd_kernel")
     kern_avg_s = statistics.mean(kern_ms) / 1e3
+    # head and tail reported separately (steps alternate head, tail, ...)
+    head_ms, tail_ms = kern_ms[0::2], kern_ms[1::2]
+    # unique-row bytes of one step (row reuse inside a batch; the algorithmic bytes count every gather)
+    ent_dim_, _, _, _ = dims(w)
+    pos0, neg0 = batches[0]
+    uniq = torch.unique(torch.cat([neg0.reshape(-1), pos0[:, 0], pos0[:, 2]])).numel()
     achieved = neg_bytes / kern_avg_s / 1e9
     triples = (B * N + B) * a.steps * world
     value = triples / elapsed
@@ -497,7 +503,11 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                      "traffic_source": traffic_src,
                      "kernel": "score_fwd_kernel (negatives)", "kernel_avg_us": kern_avg_s * 1e6,
-                     "algorithmic_bytes_per_launch": neg_bytes},
+                     "kernel_avg_us_head_batch": statistics.mean(head_ms) * 1e3 if head_ms else None,
+                     "kernel_avg_us_tail_batch": statistics.mean(tail_ms) * 1e3 if tail_ms else None,
+                     "algorithmic_bytes_per_launch": neg_bytes,
+                     "unique_row_bytes_per_step": uniq * ent_dim_ * 4,
+                     "row_reuse": (B * N + 2 * B) / max(1, uniq)},
     }
     if a.train_steps > 0:
         line["train_step"] = train_step_bench(m, batches, a.train_steps, 2)

@@ -398,6 +398,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--train-steps", type=int, default=10, help="train-step side measurement (0 = skip)")
+    ap.add_argument("--sharded-steps", type=int, default=20,
+                    help="side measurement of the YAGO3-10 row-sharded step (c4s) at the same world size (0 = skip)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -511,6 +513,22 @@ def main():
     }
     if a.train_steps > 0:
         line["train_step"] = train_step_bench(m, batches, a.train_steps, 2)
+    if a.sharded_steps > 0 and a.workload == "c2":
+        # the north star's YAGO3-10 row-sharded configuration at this world size (weak scaling:
+        # bz=512 per rank), measured beside the headline replica metric
+        ws = WORKLOADS["c4s"]
+        sa = argparse.Namespace(**{**vars(a), "steps": a.sharded_steps, "warmup": 3})
+        el = sharded_bench(ws, sa, world, rank, device, dist)
+        if dist:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            el = float(t.item())
+        line["yago3_10_rowshard"] = {
+            "workload": ws["name"], "n_gpus": world, "global_batch": ws["B"] * world, "n_neg": ws["N"],
+            "triples_per_s": (ws["B"] * ws["N"] + ws["B"]) * world * sa.steps / el,
+            "ms_per_step": el / sa.steps * 1e3, "steps": sa.steps,
+            "what": "distributed.ShardedKGE.step_forward: entity table row-sharded over the ranks, owner-computes "
+                    "scoring, chunk-pipelined RCCL all-reduce (queries) + reduce-scatter (scores)"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w, a.cpu_budget)
     if rank == 0:

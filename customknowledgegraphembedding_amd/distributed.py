@@ -16,6 +16,11 @@ Two layouts:
   Each (row, candidate) has exactly one owner, so the SUMs add exact zeros: the sharded scores
   equal the unsharded ones bitwise. Table rows never cross xGMI; per step a rank moves
   W*B*ent_dim*4 bytes of query rows and W*B*(N+1)*4 bytes of scores.
+  Pipelining: the global batch is cut into K chunks (each chunk = B/K rows of every home rank, so
+  the reduce-scatter of a chunk still lands on the home ranks). All chunks' query all-reduces are
+  issued up front; chunk k is scored as soon as its all-reduce completes while chunk k+1's
+  all-reduce and chunk k-1's reduce-scatter run on RCCL's stream, so the collectives hide behind
+  the scoring kernels.
 
 The GPU kernels are reached through a small backend object (`HipShardKernels`); tests on CPU swap
 in an oracle-backed backend to check the orchestration with gloo (tests/test_distributed_cpu.py).
@@ -82,6 +87,17 @@ def _reduce_scatter_rows(full, world, rank, group):
     return full[rank * B:(rank + 1) * B].contiguous()
 
 
+def _reduce_scatter_rows_into(out, full, world, rank, group):
+    """Async SUM reduce-scatter of `full` [W*b, C] into this rank's `out` [b, C] (a contiguous row
+    block). Returns the work handle (None when it completed synchronously: gloo fallback)."""
+    b = full.shape[0] // world
+    if full.is_cuda:
+        return dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=group, async_op=True)
+    dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
+    out.copy_(full[rank * b:(rank + 1) * b])
+    return None
+
+
 class ShardedKGE:
     """Row-sharded owner-computes forward of supervisor.py:17-18 (both model calls).
 
@@ -117,34 +133,66 @@ class ShardedKGE:
         self.relation_embedding = rel.contiguous().to(dev)  # replicated (R rows)
         self.device = torch.device(dev)
 
-    def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True):
+    def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None):
         """pos_g [W*B, 3], neg_g [W*B, N] (the global batch, identical on every rank) ->
         (out_neg [B], out_pos [B], scores [B, N]) for this rank's home rows [rank*B, (rank+1)*B)."""
         mode = ops.mode_id(mode)
         if mode not in (HEAD_BATCH, TAIL_BATCH):
             raise ValueError("step_forward needs a negative mode (0 or 1)")
         WB, N = neg_g.shape
-        if WB % self.world:
+        W = self.world
+        if WB % W:
             raise ValueError("global batch must split evenly over ranks")
+        B = WB // W
+        K = max(1, min(int(chunks if chunks is not None else (4 if W > 1 else 1)), B))
+        while B % K:
+            K -= 1
+        Bk = B // K
         k = self.kernels
         dev = self.device
-        # 1. query-entity rows (t for head-batch, h otherwise) and, in head-batch mode, the
-        #    positives' h rows, assembled by a SUM all-reduce of owner-gathered rows
         qcols = [2, 0] if mode == HEAD_BATCH else [0]
-        rows = torch.empty((len(qcols), WB, self.entity_dim), dtype=torch.float32, device=dev)
-        for i, c in enumerate(qcols):
-            k.gather_rows(self.shard, self.lo, pos_g[:, c:], 3, WB, rows[i])
-        if self.world > 1:
-            dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=self.group)
-        qe, ph = rows[0], rows[-1]
-        # 2. owner-computes scores: negatives in `mode`, positives in single mode -> column N
-        part = torch.empty((WB, N + 1), dtype=torch.float32, device=dev)
-        k.score_sharded(self.fn, mode, qe, self.relation_embedding, self.rel_off, self.shard, self.lo, pos_g,
-                        neg_g, self.D, self.gamma, self.emb_range, self.modulus, part)
-        k.score_sharded(self.fn, SINGLE, ph, self.relation_embedding, self.rel_off, self.shard, self.lo, pos_g,
-                        None, self.D, self.gamma, self.emb_range, self.modulus, part[:, N:])
-        # 3. SUM reduce-scatter -> home rows
-        home = _reduce_scatter_rows(part, self.world, self.rank, self.group) if self.world > 1 else part
+        dist_on = W > 1
+
+        # chunk k = rows h*B + k*Bk + [0, Bk) of every home rank h, in h-major order
+        def chunk_rows(kk):
+            if K == 1:
+                return pos_g, neg_g
+            base = torch.arange(W, device=pos_g.device, dtype=torch.int64) * B + kk * Bk
+            idx = (base[:, None] + torch.arange(Bk, device=pos_g.device, dtype=torch.int64)[None, :]).reshape(-1)
+            return pos_g.index_select(0, idx), neg_g.index_select(0, idx)
+
+        # 1. query-entity rows (t for head-batch, h otherwise; plus the positives' h rows in head-batch):
+        #    owner-gathered, SUM all-reduce; every chunk's all-reduce is in flight before any scoring
+        batches, rows_k, ar = [], [], []
+        for kk in range(K):
+            pk, nk = chunk_rows(kk)
+            rows = torch.empty((len(qcols), W * Bk, self.entity_dim), dtype=torch.float32, device=dev)
+            for i, c in enumerate(qcols):
+                k.gather_rows(self.shard, self.lo, pk[:, c:], 3, W * Bk, rows[i])
+            ar.append(dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                      if dist_on else None)
+            batches.append((pk, nk))
+            rows_k.append(rows)
+        # 2. owner-computes scores per chunk, 3. SUM reduce-scatter of the chunk to the home ranks
+        home = torch.empty((B, N + 1), dtype=torch.float32, device=dev)
+        pending = []
+        for kk in range(K):
+            if ar[kk] is not None:
+                ar[kk].wait()
+            pk, nk = batches[kk]
+            rows = rows_k[kk]
+            qe, ph = rows[0], rows[-1]
+            part = home if not dist_on else torch.empty((W * Bk, N + 1), dtype=torch.float32, device=dev)
+            k.score_sharded(self.fn, mode, qe, self.relation_embedding, self.rel_off, self.shard, self.lo, pk, nk,
+                            self.D, self.gamma, self.emb_range, self.modulus, part)
+            k.score_sharded(self.fn, SINGLE, ph, self.relation_embedding, self.rel_off, self.shard, self.lo, pk,
+                            None, self.D, self.gamma, self.emb_range, self.modulus, part[:, N:])
+            if dist_on:
+                pending.append((_reduce_scatter_rows_into(home[kk * Bk:(kk + 1) * Bk], part, W, self.rank,
+                                                          self.group), part))
+        for h, _ in pending:
+            if h is not None:
+                h.wait()
         scores = home[:, :N].contiguous()
         # 4. per-row reductions on the home rank
         out_neg = k.neg_reduce(scores, temperature, adversarial)

@@ -21,7 +21,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, name, results):
+def _worker(rank, world, port, name, results, chunks=None, B=3):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -29,7 +29,7 @@ def _worker(rank, world, port, name, results):
         from tests.shard_oracle_backend import OracleShardKernels
         from oracle import kge_oracle as O
 
-        E, R, d, B, N, gamma = 37, 5, 6, 3, 7, 9.0
+        E, R, d, N, gamma = 37, 5, 6, 7, 9.0
         de = name in ("ComplEx", "RotatE", "InterHT")
         sk = ShardedKGE(name, E, R, d, gamma, double_entity_embedding=de,
                         double_relation_embedding=(name == "ComplEx"), triple_relation_embedding=(name == "InterHT"),
@@ -44,7 +44,7 @@ def _worker(rank, world, port, name, results):
         home = slice(rank * B, (rank + 1) * B)
         errs = []
         for mode in (0, 1):
-            out_neg, out_pos, scores = sk.step_forward(pos, neg, mode)
+            out_neg, out_pos, scores = sk.step_forward(pos, neg, mode, chunks=chunks)
             want_s = O.score(name, ent, rel, pos[home], neg[home], mode, gamma, ref._range_f, sk.modulus)
             want_neg = O.tf_call(name, ent, rel, pos[home], neg[home], mode, gamma, ref._range_f, sk.modulus)
             want_pos = O.tf_call(name, ent, rel, pos[home], neg[home], 3, gamma, ref._range_f, sk.modulus)
@@ -63,6 +63,18 @@ def test_sharded_owner_computes_world2_gloo(name):
     results = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), name, results), nprocs=world, join=True)
     assert len(results) == world
+    for r in range(world):
+        assert results[r] < 1e-5, (r, results[r])
+
+
+@pytest.mark.parametrize("chunks,B", [(1, 4), (2, 4), (3, 4), (4, 5)])
+def test_sharded_pipelined_chunks_world2_gloo(chunks, B):
+    """Chunked pipeline (async all-reduce per chunk, per-chunk reduce-scatter into the home block):
+    any chunk count, including one that does not divide B (falls back to a divisor)."""
+    world = 2
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), "DistMult", results, chunks, B), nprocs=world, join=True)
     for r in range(world):
         assert results[r] < 1e-5, (r, results[r])
 

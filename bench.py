@@ -64,6 +64,10 @@ WORKLOADS = {
     "c4s": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512/rank, row-sharded owner-computes",
                 fn="DistMult", nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False,
                 dr=False, B=512, N=1024, sharded=True),
+    # the same, with the all-to-all row-fetch scheme (both schemes, measured side by side)
+    "c4g": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512/rank, row-sharded all-to-all row fetch",
+                fn="DistMult", nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False,
+                dr=False, B=512, N=1024, sharded=True, scheme="gather"),
 }
 
 
@@ -152,8 +156,9 @@ def sharded_bench(w, a, world, rank, device, dist_on):
         pos = np.stack([g.randint(E, size=WB), g.randint(R, size=WB), g.randint(E, size=WB)], 1)
         neg = np.random.RandomState(200 + i).randint(E, size=(WB, N))
         batches.append((torch.from_numpy(pos).to(device), torch.from_numpy(neg).to(device)))
+    step = sk.step_forward_gather if w.get("scheme") == "gather" else sk.step_forward
     for i in range(a.warmup):
-        sk.step_forward(*batches[i % 4], i % 2)
+        step(*batches[i % 4], i % 2)
     torch.cuda.synchronize()
     if dist_on:
         import torch.distributed as tdist
@@ -161,7 +166,7 @@ def sharded_bench(w, a, world, rank, device, dist_on):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        sk.step_forward(*batches[i % 4], i % 2)
+        step(*batches[i % 4], i % 2)
     torch.cuda.synchronize()
     if dist_on:
         tdist.barrier()
@@ -436,7 +441,7 @@ def main():
                 "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "f32", "data": "synthetic global batch replicated by seed",
                 "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N,
-                           "parallelism": f"rowshard{world}"},
+                           "parallelism": f"rowshard{world}", "scheme": w.get("scheme", "owner-computes")},
                 "roofline": {"bound": "hbm", "achieved": owned_bytes / (elapsed / a.steps) / 1e9,
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": owned_bytes / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, "traffic": None,
@@ -518,7 +523,7 @@ def main():
         # bz=512 per rank), measured beside the headline replica metric
         ws = WORKLOADS["c4s"]
         sa = argparse.Namespace(**{**vars(a), "steps": a.sharded_steps, "warmup": 3})
-        el = sharded_bench(ws, sa, world, rank, device, dist)
+        el = sharded_bench(ws, sa, world, rank, device, dist)  # symmetric on every rank
         if dist:
             t = torch.tensor([el], device=device, dtype=torch.float64)
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX)

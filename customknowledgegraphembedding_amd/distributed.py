@@ -14,13 +14,22 @@ Two layouts:
     3. SUM reduce-scatter of the [W*B, N+1] partial scores -> each rank's home rows  RCCL
     4. home rank: self-adversarial reduction + logsigmoid of its B rows               kge_neg_reduce/...
   Each (row, candidate) has exactly one owner, so the SUMs add exact zeros: the sharded scores
-  equal the unsharded ones bitwise. Table rows never cross xGMI; per step a rank moves
+  equal the unsharded ones bitwise. (An out-of-range candidate id has no owner and scores 0 here;
+  the unsharded kernels and the gather scheme score it against a zero row, as TF-GPU gather does.) Table rows never cross xGMI; per step a rank moves
   W*B*ent_dim*4 bytes of query rows and W*B*(N+1)*4 bytes of scores.
   Pipelining: the global batch is cut into K chunks (each chunk = B/K rows of every home rank, so
   the reduce-scatter of a chunk still lands on the home ranks). All chunks' query all-reduces are
   issued up front; chunk k is scored as soon as its all-reduce completes while chunk k+1's
   all-reduce and chunk k-1's reduce-scatter run on RCCL's stream, so the collectives hide behind
   the scoring kernels.
+
+* Row-sharded gather (`ShardedKGE.step_forward_gather`, the north star's literal scheme, kept beside
+  owner-computes as SURVEY §8e asks so the two can be measured against each other): every rank
+  fetches the rows its own B home rows need. Per step a rank dedups its ids (sorted unique), sends
+  each owner the ids in that owner's range (all-to-all), receives the rows (all-to-all), and scores
+  locally on the fetched cache with the unsharded kernels (kge_step_forward). Moves ~|unique rows| x
+  ent_dim x 4 bytes per rank (C4 at 8 ranks: ~45k rows, ~89 MB) instead of owner-computes' queries
+  + scores, which is why owner-computes is the default.
 
 The GPU kernels are reached through a small backend object (`HipShardKernels`); tests on CPU swap
 in an oracle-backed backend to check the orchestration with gloo (tests/test_distributed_cpu.py).
@@ -69,6 +78,12 @@ class HipShardKernels:
     @staticmethod
     def neg_reduce(scores, temperature, adversarial):
         return ops.neg_reduce_raw(scores, temperature, adversarial)
+
+    @staticmethod
+    def step_forward(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus, temperature, adversarial):
+        out_neg, out_pos, ns, _ = ops.step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range,
+                                                       modulus, temperature, adversarial)
+        return out_neg, out_pos, ns
 
     @staticmethod
     def log_sigmoid(x):
@@ -197,4 +212,59 @@ class ShardedKGE:
         # 4. per-row reductions on the home rank
         out_neg = k.neg_reduce(scores, temperature, adversarial)
         out_pos = k.log_sigmoid(home[:, N].contiguous())
+        return out_neg, out_pos, scores
+
+    def step_forward_gather(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True):
+        """Same contract and results as step_forward (bitwise: the same rows reach the same kernel
+        arithmetic), by fetching the home rows' entity rows from their owners (all-to-all)."""
+        mode = ops.mode_id(mode)
+        if mode not in (HEAD_BATCH, TAIL_BATCH):
+            raise ValueError("step_forward_gather needs a negative mode (0 or 1)")
+        WB, N = neg_g.shape
+        W, r = self.world, self.rank
+        if WB % W:
+            raise ValueError("global batch must split evenly over ranks")
+        B = WB // W
+        dev = self.device
+        pos_h = pos_g[r * B:(r + 1) * B].contiguous()
+        neg_h = neg_g[r * B:(r + 1) * B].contiguous()
+        ids = torch.cat([neg_h.reshape(-1), pos_h[:, 0], pos_h[:, 2]])
+        inr = (ids >= 0) & (ids < self.nentity)
+        U = torch.unique(ids[inr])  # sorted ascending
+        bounds = torch.tensor([shard_bounds(self.nentity, W, o)[0] for o in range(W)] + [self.nentity],
+                              dtype=torch.int64, device=U.device)
+        edges = torch.searchsorted(U, bounds)
+        need = (edges[1:] - edges[:-1]).to(torch.int64)  # rows this rank needs from each owner
+        if W > 1:
+            allneed = [torch.empty_like(need) for _ in range(W)]
+            dist.all_gather(allneed, need, group=self.group)
+            C = torch.stack(allneed).cpu()  # C[q, o]: rows requester q needs from owner o
+        else:
+            C = need.cpu().view(1, 1)
+        send_ids = C[r].tolist()                   # my requests, grouped by owner (U is owner-ordered)
+        recv_ids = C[:, r].tolist()                # requests addressed to me, per requester
+        if W > 1:
+            req = torch.empty(sum(recv_ids), dtype=torch.int64, device=U.device)
+            dist.all_to_all_single(req, U, recv_ids, send_ids, group=self.group)
+        else:
+            req = U
+        rows_out = torch.empty((req.numel(), self.entity_dim), dtype=torch.float32, device=dev)
+        if req.numel():
+            self.kernels.gather_rows(self.shard, self.lo, req.to(dev), 1, req.numel(), rows_out)
+        cache = torch.zeros((U.numel() + 1, self.entity_dim), dtype=torch.float32, device=dev)  # + zero row
+        if W > 1:
+            dist.all_to_all_single(cache[:U.numel()], rows_out, [c * 1 for c in send_ids], recv_ids,
+                                   group=self.group)
+        else:
+            cache[:U.numel()] = rows_out
+        # home ids -> cache rows (out-of-range ids -> the zero row, TF-GPU gather semantics)
+        loc = torch.searchsorted(U, ids.clamp(0, max(self.nentity - 1, 0)))
+        loc = torch.where(inr, loc, torch.full_like(loc, U.numel()))
+        neg_l = loc[:B * N].view(B, N).contiguous()
+        pos_l = pos_h.clone()
+        pos_l[:, 0] = loc[B * N:B * N + B]
+        pos_l[:, 2] = loc[B * N + B:]
+        out_neg, out_pos, scores = self.kernels.step_forward(
+            self.fn, mode, cache, self.relation_embedding, self.rel_off, pos_l.to(dev), neg_l.to(dev), self.D,
+            self.gamma, self.emb_range, self.modulus, temperature, adversarial)
         return out_neg, out_pos, scores

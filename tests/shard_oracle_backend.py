@@ -44,3 +44,12 @@ class OracleShardKernels:
     @staticmethod
     def log_sigmoid(x):
         return F.logsigmoid(x.double())
+
+    @staticmethod
+    def step_forward(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus, temperature, adversarial):
+        name = NAMES[fn]
+        e, rr = ent.double(), rel.double()
+        s = O.score(name, e, rr, pos, neg, mode, gamma, emb_range, modulus)
+        red = O.adv_reduce(s, temperature) if adversarial else O.mean_reduce(s)
+        ps = O.score(name, e, rr, pos, neg, 3, gamma, emb_range, modulus)
+        return red[:, 0], F.logsigmoid(ps)[:, 0], s

@@ -21,7 +21,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, name, results, chunks=None, B=3):
+def _worker(rank, world, port, name, results, chunks=None, B=3, scheme="owner"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -44,7 +44,10 @@ def _worker(rank, world, port, name, results, chunks=None, B=3):
         home = slice(rank * B, (rank + 1) * B)
         errs = []
         for mode in (0, 1):
-            out_neg, out_pos, scores = sk.step_forward(pos, neg, mode, chunks=chunks)
+            if scheme == "gather":
+                out_neg, out_pos, scores = sk.step_forward_gather(pos, neg, mode)
+            else:
+                out_neg, out_pos, scores = sk.step_forward(pos, neg, mode, chunks=chunks)
             want_s = O.score(name, ent, rel, pos[home], neg[home], mode, gamma, ref._range_f, sk.modulus)
             want_neg = O.tf_call(name, ent, rel, pos[home], neg[home], mode, gamma, ref._range_f, sk.modulus)
             want_pos = O.tf_call(name, ent, rel, pos[home], neg[home], 3, gamma, ref._range_f, sk.modulus)
@@ -75,6 +78,17 @@ def test_sharded_pipelined_chunks_world2_gloo(chunks, B):
     mgr = mp.Manager()
     results = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), "DistMult", results, chunks, B), nprocs=world, join=True)
+    for r in range(world):
+        assert results[r] < 1e-5, (r, results[r])
+
+
+@pytest.mark.parametrize("name", ["TransE", "InterHT"])
+def test_sharded_gather_scheme_world2_gloo(name):
+    """The all-to-all row-fetch scheme gives the unsharded results on every home row."""
+    world = 2
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), name, results, None, 3, "gather"), nprocs=world, join=True)
     for r in range(world):
         assert results[r] < 1e-5, (r, results[r])
 

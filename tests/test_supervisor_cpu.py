@@ -40,3 +40,14 @@ def test_lr_schedule_matches_reference_formula():
     s = LRSchedule(steps_per_epoch=100)
     assert resolve_lr(s, 0) == lrfn(0) and resolve_lr(s, 250) == lrfn(2)
     assert resolve_lr(lambda: 0.5, 7) == 0.5 and resolve_lr(0.25, 3) == 0.25
+
+
+def test_run_args_parser_matches_reference_flags():
+    """tensorflow_codes/run.py:20-37 flags (short and long forms)."""
+    from customknowledgegraphembedding_amd.run import args_parser
+
+    a = args_parser(["-ip", "x.tfrec", "-bz", "512", "-sf", "InterHT", "--nentity", "40943", "--nrelation", "11",
+                     "--hidden_dim", "1000", "--gamma", "24", "-de", "-tr"])
+    assert (a.input_path, a.batch_size, a.score_function) == (["x.tfrec"], 512, "InterHT")
+    assert a.double_entity_embedding and a.triple_relation_embedding and not a.double_relation_embedding
+    assert (a.epochs, a.steps_per_epoch, a.steps_per_tpu_call) == (1, 1000, 99)

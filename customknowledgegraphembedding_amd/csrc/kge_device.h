@@ -958,6 +958,22 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
     const int n = hi - lo;
     Cand<FN, V, G> c;
     if (n > 0 || p.adam.on) c.load(p.cent + e * p.c_ld, true, D, lane);
+    // fused optimizer: the row's Adam moments are requested now, so their latency overlaps the
+    // event walk instead of following it
+    constexpr int NH = is_split(FN) ? 2 : 1;
+    vecf<V> mm[NH][G], vv[NH][G];
+    if (p.adam.on) {
+        const rsrc_t sm = make_rsrc(p.adam.m + e * p.c_ld, (uint32_t)p.ent_w * 4u);
+        const rsrc_t sv = make_rsrc(p.adam.v + e * p.c_ld, (uint32_t)p.ent_w * 4u);
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                const uint32_t off = (uint32_t)(h * D * 4) + goff<V>(lane, k);
+                mm[h][k] = bload<V>(sm, off);
+                vv[h][k] = bload<V>(sv, off);
+            }
+    }
     if (n > 0) {
         if (n <= kWave) {
             int code = lane < n ? p.ev_code[lo + lane] : INT32_MAX;
@@ -984,25 +1000,22 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
         float* prow = const_cast<float*>(p.cent) + e * p.c_ld;
         float* mrow = p.adam.m + e * p.c_ld;
         float* vrow = p.adam.v + e * p.c_ld;
-        const rsrc_t sm = make_rsrc(mrow, (uint32_t)p.ent_w * 4u), sv = make_rsrc(vrow, (uint32_t)p.ent_w * 4u);
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             const int gi = lane + k * kWave;
             const bool in = gi < DV;
 #pragma unroll
-            for (int h = 0; h < (is_split(FN) ? 2 : 1); ++h) {
-                const uint32_t off = (uint32_t)(h * D * 4) + goff<V>(lane, k);
-                vecf<V> mm = bload<V>(sm, off), vv = bload<V>(sv, off);
+            for (int h = 0; h < NH; ++h) {
                 vecf<V> pp = h ? c.cb[k] : c.ca[k];
                 const vecf<V>& gg = h ? acc_b[k] : acc_a[k];
 #pragma unroll
                 for (int i = 0; i < V; ++i)
-                    adam_update(pp.a[i], gg.a[i], mm.a[i], vv.a[i], p.adam.b1, p.adam.b2, p.adam.eps, p.adam.alpha,
-                                p.adam.step_size, p.adam.bc2_sqrt, p.adam.keras);
+                    adam_update(pp.a[i], gg.a[i], mm[h][k].a[i], vv[h][k].a[i], p.adam.b1, p.adam.b2, p.adam.eps,
+                                p.adam.alpha, p.adam.step_size, p.adam.bc2_sqrt, p.adam.keras);
                 const int64_t col = (int64_t)h * D + gi * V;
                 vstore<V>(prow + col, pp, in);
-                vstore<V>(mrow + col, mm, in);
-                vstore<V>(vrow + col, vv, in);
+                vstore<V>(mrow + col, mm[h][k], in);
+                vstore<V>(vrow + col, vv[h][k], in);
             }
         }
         return;

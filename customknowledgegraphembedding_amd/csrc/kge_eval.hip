@@ -10,6 +10,8 @@
 //     run on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: exact f32, k-ordered fma chain).
 //   * Every score function: S via the VALU scorer with the candidate row stride 0 (kge_abi.hip).
 //   * kge_rank_filtered: exact integer ranks from S, the true entity and a CSR filter list.
+#include <stdlib.h>
+
 #include <string>
 
 #include "kge_device.h"
@@ -46,60 +48,71 @@ __global__ __launch_bounds__(kBlock) void eval_query_kernel(ScoreParams p, float
 
 // ---------------------------------------------------------------------------------------------
 // S[M, N] = A[M, K] . B[N, K]^T, fp32 in / fp32 out, on v_mfma_f32_32x32x2_f32.
-// Block 256 threads = 2 x 2 waves, block tile 128 x 128, wave tile 64 x 64 (2 x 2 MFMA tiles, four
-// independent accumulators -> back-to-back issue), K staged through LDS in chunks of 16, double
-// buffered (next chunk's global loads in registers while the current chunk is multiplied).
+// Block 256 threads = 2 x 2 waves, block tile 128 x BN (BN = 128 or 64), wave tile 64 x BN/2 (2 x JN
+// MFMA tiles, independent accumulators -> back-to-back issue), K staged through LDS in chunks of 16,
+// double buffered (next chunk's global loads in registers while the current chunk is multiplied).
 // LDS images are k-major ([k][m]) so a wave's fragment read (lanes 0-31 one k, 32-63 the next)
 // is 32 consecutive dwords per half-wave: conflict-free ds_read_b32.
+// BN = 64 halves the tile for grids too small to give every one of the 256 CUs a 128 x 128 tile.
 // ---------------------------------------------------------------------------------------------
-constexpr int GBM = 128, GBN = 128, GBK = 16;  // BK = 32 measured 92 vs 96 TFLOP/s at C5
-constexpr int GNU = GBK / 8;      // float4 per thread per operand and K chunk
-constexpr int GTPR = GBK / 4;     // threads per staged row
+constexpr int GBM = 128, GBK = 16;  // BK = 32 measured 92 vs 96 TFLOP/s at C5
+constexpr int GTPR = GBK / 4;       // threads per staged row
 constexpr int GRPP = kBlock / GTPR;  // rows staged per unit
-constexpr int GLD = GBM + 4;  // padded LDS row (floats)
+constexpr int GLD = GBM + 4;         // padded LDS row (floats)
 
+template <int BN>
 __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
                                                              float* __restrict__ C, int M, int N, int K, int64_t lda,
                                                              int64_t ldb, int64_t ldc) {
+    constexpr int JN = BN / 64;               // 32-wide MFMA tiles per wave in N
+    constexpr int AU = GBM * GBK / 4 / kBlock;  // float4 per thread for A
+    constexpr int BU = BN * GBK / 4 / kBlock;   // float4 per thread for B
+    constexpr int BLD = BN + 4;
     __shared__ __attribute__((aligned(16))) float As[2][GBK][GLD];
-    __shared__ __attribute__((aligned(16))) float Bs[2][GBK][GLD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][GBK][BLD];
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wave = t >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     // XCD-aware: blocks b and b+8 share an XCD (round-robin placement); give each XCD a contiguous
     // run of N-tiles (entity rows) so its L2 keeps reusing the same B rows across query tiles.
-    const int ntn = (N + GBN - 1) / GBN, ntm = (M + GBM - 1) / GBM;
+    const int ntn = (N + BN - 1) / BN, ntm = (M + GBM - 1) / GBM;
     const int nblk = ntn * ntm;
     int bid = blockIdx.x;
     if (nblk % 8 == 0) bid = (bid % 8) * (nblk / 8) + bid / 8;
     const int tn = bid / ntm, tm = bid % ntm;
-    const int m0 = tm * GBM, n0 = tn * GBN;
+    const int m0 = tm * GBM, n0 = tn * BN;
 
-    // global -> register staging: 128 rows x GBK floats per operand = GNU float4 per thread
-    // (thread t, unit u: row t / GTPR + GRPP u, k offset (t % GTPR) * 4)
-    float4 ra[GNU], rb[GNU];
+    // global -> register staging (thread t, unit u: row t / GTPR + GRPP u, k offset (t % GTPR) * 4)
+    float4 ra[AU], rb[BU];
     const int kq = (t % GTPR) * 4;
     auto gload = [&](int k0) {
         const int ka = k0 + kq;
 #pragma unroll
-        for (int u = 0; u < GNU; ++u) {
-            const int r = t / GTPR + GRPP * u;
-            const int gm = m0 + r, gn = n0 + r;
+        for (int u = 0; u < AU; ++u) {
+            const int gm = m0 + t / GTPR + GRPP * u;
             ra[u] = (gm < M && ka < K) ? *reinterpret_cast<const float4*>(A + (int64_t)gm * lda + ka)
                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < BU; ++u) {
+            const int gn = n0 + t / GTPR + GRPP * u;
             rb[u] = (gn < N && ka < K) ? *reinterpret_cast<const float4*>(Bm + (int64_t)gn * ldb + ka)
                                        : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto sstore = [&](int buf) {
 #pragma unroll
-        for (int u = 0; u < GNU; ++u) {
+        for (int u = 0; u < AU; ++u) {
             const int r = t / GTPR + GRPP * u;
             As[buf][kq + 0][r] = ra[u].x;
             As[buf][kq + 1][r] = ra[u].y;
             As[buf][kq + 2][r] = ra[u].z;
             As[buf][kq + 3][r] = ra[u].w;
+        }
+#pragma unroll
+        for (int u = 0; u < BU; ++u) {
+            const int r = t / GTPR + GRPP * u;
             Bs[buf][kq + 0][r] = rb[u].x;
             Bs[buf][kq + 1][r] = rb[u].y;
             Bs[buf][kq + 2][r] = rb[u].z;
@@ -107,11 +120,11 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __rest
         }
     };
 
-    f32x16 acc[2][2];
+    f32x16 acc[2][JN];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < JN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -126,15 +139,15 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __rest
 #pragma unroll
         for (int s = 0; s < GBK / 2; ++s) {
             const int kk = 2 * s + half;
-            float a[2], b[2];
+            float a[2], b[JN];
 #pragma unroll
             for (int i = 0; i < 2; ++i) a[i] = As[buf][kk][wm * 64 + i * 32 + col];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kk][wn * 64 + j * 32 + col];
+            for (int j = 0; j < JN; ++j) b[j] = Bs[buf][kk][wn * (BN / 2) + j * 32 + col];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
         if (kc + 1 < nk) {
             sstore(buf ^ 1);
@@ -145,8 +158,8 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int gn = n0 + wn * 64 + j * 32 + col;
+        for (int j = 0; j < JN; ++j) {
+            const int gn = n0 + wn * (BN / 2) + j * 32 + col;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -219,8 +232,18 @@ int launch_eval_query_any(int fn, bool ch, const ScoreParams& p, hipStream_t st,
 
 int launch_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
                    int64_t ldc, hipStream_t st) {
-    const int blocks = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
-    hipLaunchKernelGGL(gemm_nt_f32_kernel, dim3(blocks), dim3(kBlock), 0, st, A, B, C, M, N, K, lda, ldb, ldc);
+    // tile width: 128 x 128 unless that grid leaves CUs idle (fewer tiles than the 256 CUs); at C5
+    // (936 tiles) 128 wide measured 102 TFLOP/s against 92 for 64 wide
+    const int64_t tm = (M + GBM - 1) / GBM;
+    const int64_t t128 = tm * ((N + 127) / 128), t64 = tm * ((N + 63) / 64);
+    int bn = t128 < 256 ? 64 : 128;
+    if (const char* env = getenv("KGE_GEMM_BN")) bn = atoi(env) == 64 ? 64 : 128;  // tuning override
+    if (bn == 64)
+        hipLaunchKernelGGL(gemm_nt_f32_kernel<64>, dim3((unsigned)t64), dim3(kBlock), 0, st, A, B, C, M, N, K, lda,
+                           ldb, ldc);
+    else
+        hipLaunchKernelGGL(gemm_nt_f32_kernel<128>, dim3((unsigned)t128), dim3(kBlock), 0, st, A, B, C, M, N, K, lda,
+                           ldb, ldc);
     return 0;
 }
 

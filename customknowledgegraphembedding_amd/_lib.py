@@ -43,7 +43,7 @@ SIGNATURES = {
     "kge_step_forward": (
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
-         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p],
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p],
     ),
     "kge_step_finish": (
         _c_i,
@@ -83,14 +83,14 @@ SIGNATURES = {
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p,
-         _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p],
+         _c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p],
     ),
     "kge_step_backward_adam_workspace_size": (_c_i64, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
     "kge_step_backward_adam": (
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_p, _c_f, _c_f, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p,
-         _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_i64, _c_p],
+         _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_p, _c_i64, _c_p],
     ),
     "kge_sampler_create": (_c_p, [_c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i]),
     "kge_sampler_seed": (_c_i, [_c_p, ctypes.c_uint32]),

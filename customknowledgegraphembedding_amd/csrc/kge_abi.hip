@@ -335,8 +335,10 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         p.cpw = 1;
         p.wpr = 1;
         waves = p.B;
-    } else if (kind == KIND_BWD_ROWS) {
+    } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM) {
         waves = p.B * kWavesPerBlock;  // one block per slot
+    } else if (kind == KIND_BWD_CHAIN) {
+        waves = p.B;  // one wave per slot
     } else if (kind == KIND_BWD_ENT) {
         waves = p.c_rows;  // one wave per entity row
     } else {
@@ -347,7 +349,10 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > INT32_MAX) return fail(KGE_EINVAL, "problem too large for one launch");
     const bool ch = (kind != KIND_FINISH) && mode == KGE_HEAD_BATCH;
-    if ((kind == KIND_BWD_ROWS || kind == KIND_BWD_ENT) && G > kMaxG) return fail(KGE_ENOTSUP, "dimension too large");
+    if ((kind == KIND_BWD_ROWS || kind == KIND_BWD_ENT || kind == KIND_BWD_STREAM || kind == KIND_BWD_CHAIN) &&
+        G > kMaxG)
+        return fail(KGE_ENOTSUP, "dimension too large");
+    if (kind == KIND_BWD_STREAM && G % kWavesPerBlock) return fail(KGE_ENOTSUP, "streaming phase 1 needs G % 4 == 0");
     rc = dispatch(fn, p, kind, (hipStream_t)stream, (int)blocks, ch, V, G);
     if (rc) return fail(rc, "no kernel for this (function, width) combination");
     return check_launch(kind == KIND_BWD ? "kge score backward launch"
@@ -491,15 +496,20 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
                      int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
                      int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
                      float temperature, int adversarial, float* neg_scores, int64_t ns_ld, float* out_neg,
-                     float* pos_scores, float* out_pos, void* stream) {
+                     float* pos_scores, float* out_pos, float* cand_stats, void* stream) {
     int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
     if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_forward needs a negative mode (0 or 1)");
     if (B < 0 || N <= 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
     if (B == 0) return ok();
     if (!pos || !neg || !neg_scores || !out_neg || !out_pos) return fail(KGE_EINVAL, "null pointer");
-    rc = kge_score_indexed(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D,
-                           gamma, emb_range, modulus, neg_scores, ns_ld, stream);
+    ScoreParams p;
+    fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D, gamma,
+                 emb_range, modulus);
+    p.out = neg_scores;
+    p.out_ld = ns_ld;
+    p.cand_stats = reinterpret_cast<float2*>(cand_stats);
+    rc = run_score(fn, mode, p, (cand_stats && fn == KGE_INTERHT) ? KIND_FWD_STATS : KIND_FWD, stream);
     if (rc) return rc;
     return kge_step_finish(fn, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, B, D, gamma, emb_range,
                            modulus, neg_scores, N, ns_ld, temperature, adversarial, out_neg, pos_scores, out_pos,
@@ -701,7 +711,7 @@ int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq
 // Deterministic backward of the fused train step
 // ---------------------------------------------------------------------------------------------
 struct StepWs {
-    float *d_ns, *d_ps, *qbuf, *qg_ent, *qg_rel, *dmod;
+    float *d_ns, *d_ps, *qbuf, *qg_ent, *qg_rel, *dmod, *dqbuf;
     int *count, *off, *cursor, *code, *tiles;
     int64_t bytes;
 };
@@ -722,6 +732,7 @@ static StepWs step_ws_layout(char* base, int64_t E, int64_t B, int64_t N, int64_
     w.qg_ent = (float*)take(2 * B * ent_w * 4);
     w.qg_rel = (float*)take(2 * B * rel_w * 4);
     w.dmod = (float*)take(2 * B * 4);
+    w.dqbuf = (float*)take(B * 3 * D * 4);
     w.count = (int*)take(E * 4);
     w.off = (int*)take((E + 1) * 4);
     w.cursor = (int*)take(E * 4);
@@ -778,9 +789,9 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
                               const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma,
                               float emb_range, float modulus, float temperature, int adversarial, int detach,
                               const float* neg_scores, int64_t ns_ld, const float* pos_scores, const float* d_out_neg,
-                              const float* d_out_pos, float* d_ent, float* d_rel, float* d_modulus, void* workspace,
-                              int64_t workspace_bytes, void* stream, const AdamArgs* adam, float* m_ent,
-                              float* v_ent) {
+                              const float* d_out_pos, float* d_ent, float* d_rel, float* d_modulus,
+                              const float* cand_stats, void* workspace, int64_t workspace_bytes, void* stream,
+                              const AdamArgs* adam, float* m_ent, float* v_ent) {
     int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
     if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_backward needs a negative mode (0 or 1)");
@@ -820,7 +831,20 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
     p.ent_w = ent_w;
     p.rel_w = rel_w;
     p.slot0 = 0;
-    rc = run_score(fn, mode, p, KIND_BWD_ROWS, stream);
+    // streaming form when every wave of the block owns whole column groups (G a multiple of 4) and
+    // InterHT's candidate norms are available from the forward; the register-resident form otherwise
+    int V1 = 1, G1 = 1;
+    rc = pick_vg(p, V1, G1);
+    if (rc) return rc;
+    if (G1 >= kWavesPerBlock && G1 % kWavesPerBlock == 0 && G1 <= kMaxG && (fn != KGE_INTERHT || cand_stats)) {
+        p.cand_stats = reinterpret_cast<float2*>(const_cast<float*>(cand_stats));
+        p.dqbuf = w.dqbuf;
+        rc = run_score(fn, mode, p, KIND_BWD_STREAM, stream);
+        if (rc) return rc;
+        rc = run_score(fn, mode, p, KIND_BWD_CHAIN, stream);
+    } else {
+        rc = run_score(fn, mode, p, KIND_BWD_ROWS, stream);
+    }
     if (rc) return rc;
     ScoreParams pp;
     fill_indexed(pp, fn, KGE_SINGLE, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, nullptr, 0, B, 1, D,
@@ -898,11 +922,12 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
                       int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
                       float temperature, int adversarial, int detach, const float* neg_scores, int64_t ns_ld,
                       const float* pos_scores, const float* d_out_neg, const float* d_out_pos, float* d_ent,
-                      float* d_rel, float* d_modulus, void* workspace, int64_t workspace_bytes, void* stream) {
+                      float* d_rel, float* d_modulus, const float* cand_stats, void* workspace,
+                      int64_t workspace_bytes, void* stream) {
     return step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
                               D, gamma, emb_range, modulus, temperature, adversarial, detach, neg_scores, ns_ld,
-                              pos_scores, d_out_neg, d_out_pos, d_ent, d_rel, d_modulus, workspace, workspace_bytes,
-                              stream, nullptr, nullptr, nullptr);
+                              pos_scores, d_out_neg, d_out_pos, d_ent, d_rel, d_modulus, cand_stats, workspace,
+                              workspace_bytes, stream, nullptr, nullptr, nullptr);
 }
 
 int64_t kge_step_backward_adam_workspace_size(int fn, int64_t nentity, int64_t nrelation, int64_t rel_ld, int64_t B,
@@ -919,7 +944,8 @@ int kge_step_backward_adam(int fn, int mode, float* ent, int64_t nentity, int64_
                            const float* neg_scores, int64_t ns_ld, const float* pos_scores, const float* d_out_neg,
                            const float* d_out_pos, float* m_ent, float* v_ent, float* m_rel, float* v_rel,
                            float* m_mod, float* v_mod, float lr, float beta1, float beta2, float eps, int64_t step,
-                           int keras, void* workspace, int64_t workspace_bytes, void* stream) {
+                           int keras, const float* cand_stats, void* workspace, int64_t workspace_bytes,
+                           void* stream) {
     if (step < 1) return fail(KGE_EINVAL, "step is 1-based");
     if (!m_rel || !v_rel || (modulus_param && (!m_mod || !v_mod))) return fail(KGE_EINVAL, "null optimizer state");
     const int64_t base = kge_step_backward_workspace_size(fn, nentity, B, N, D);
@@ -942,7 +968,7 @@ int kge_step_backward_adam(int fn, int mode, float* ent, int64_t nentity, int64_
     int rc = step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B,
                                 N, D, gamma, emb_range, modulus, temperature, adversarial, detach, neg_scores, ns_ld,
                                 pos_scores, d_out_neg, d_out_pos, nullptr, d_rel, modulus_param ? d_mod : nullptr,
-                                workspace, base, stream, &a, m_ent, v_ent);
+                                cand_stats, workspace, base, stream, &a, m_ent, v_ent);
     if (rc) return rc;
     // the relation table (and the pRotatE modulus) are small: their gradients go through the dense
     // optimizer kernel, with the same adam_update as the fused entity rows

@@ -273,7 +273,7 @@ struct Cand {
 // Forward score of one candidate held in registers (every lane returns the full score).
 template <int FN, bool CH, int V, int G>
 __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Query<FN, CH, V, G>& q,
-                                            const ScoreParams& p) {
+                                            const ScoreParams& p, float2* stats = nullptr) {
     float acc = 0.f;
     if constexpr (FN == KGE_INTERHT) {
         float sa = 0.f, sb = 0.f;
@@ -285,6 +285,7 @@ __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Query
                 sb += c.cb[k].a[i] * c.cb[k].a[i];
             }
         const float ia = rsqrt_f(wave_sum(sa)), ib = rsqrt_f(wave_sum(sb));
+        if (stats) *stats = make_float2(ia, ib);  // kept for the streaming phase-1 backward
 #pragma unroll
         for (int k = 0; k < G; ++k)
 #pragma unroll
@@ -359,7 +360,7 @@ __device__ __forceinline__ const float* cand_row(const ScoreParams& p, int64_t i
     return p.cent + (ok ? id : 0) * p.c_ld;
 }
 
-template <int FN, bool CH, int V, int G>
+template <int FN, bool CH, int V, int G, bool ST = false>
 __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
     WaveTask t;
     if (!wave_task(p, t)) return;
@@ -374,34 +375,46 @@ __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
 
     // software pipeline: row j+1 is in flight while row j is reduced. A foreign candidate of a
     // row-sharded table (skip_foreign) loads nothing (0-byte descriptor) and scores 0.
+    // InterHT with cand_stats: the candidate's inverse half-norms are kept (lane j) for the backward.
     float my_score = 0.f;
+    float2 my_st = make_float2(0.f, 0.f), st;
+    float2* stp = ST ? &st : nullptr;
     Cand<FN, V, G> x0, x1;
     bool ok0, ok1;
     const float* row = cand_row(p, readlane64(my_id, 0), ok0);
     x0.load(row, ok0, p.D, lane);
     int j = 0;
+    auto keep = [&](int jj, float sc) {
+        if (lane == jj) {
+            my_score = sc;
+            if constexpr (ST) my_st = st;
+        }
+    };
     for (; j + 2 < t.nc; j += 2) {
         row = cand_row(p, readlane64(my_id, j + 1), ok1);
         x1.load(row, ok1, p.D, lane);
-        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p);
-        if (lane == j) my_score = s0;
+        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
+        keep(j, s0);
         row = cand_row(p, readlane64(my_id, j + 2), ok0);
         x0.load(row, ok0, p.D, lane);
-        const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p);
-        if (lane == j + 1) my_score = s1;
+        const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p, stp);
+        keep(j + 1, s1);
     }
     if (j + 1 < t.nc) {
         row = cand_row(p, readlane64(my_id, j + 1), ok1);
         x1.load(row, ok1, p.D, lane);
-        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p);
-        if (lane == j) my_score = s0;
-        const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p);
-        if (lane == j + 1) my_score = s1;
+        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
+        keep(j, s0);
+        const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p, stp);
+        keep(j + 1, s1);
     } else {
-        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p);
-        if (lane == j) my_score = s0;
+        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
+        keep(j, s0);
     }
     if (lane < t.nc) p.out[t.b * p.out_ld + t.n0 + lane] = my_score;
+    if constexpr (ST) {
+        if (lane < t.nc) p.cand_stats[t.b * p.N + t.n0 + lane] = my_st;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -777,6 +790,37 @@ __device__ __forceinline__ void vstore(float* dst, const vecf<V>& v, bool ok) {
     if (ok) *reinterpret_cast<vecf<V>*>(dst) = v;
 }
 
+// Phase-1 epilogue of one slot: the query chain (gradients of the raw query-entity and relation rows)
+// and the rows phase 2 reads (prebuilt query, query-entity gradient), relation gradient rows.
+template <int FN, bool CH, int V, int G>
+__device__ __forceinline__ void rows_finalize(const ScoreParams& p, int64_t b, const Query<FN, CH, V, G>& q,
+                                              vecf<V> (&dq0)[G], vecf<V> (&dq1)[G], vecf<V> (&dq2)[G], int64_t qi,
+                                              int64_t ri, bool qok, bool rok, int lane) {
+    const int D = p.D, DV = D / V;
+    const float* qrow = p.qent + (qok ? qi : 0) * p.q_ld;
+    const float* rrow = p.rel + (rok ? ri : 0) * p.r_ld + p.r_off;
+    vecf<V> gea[G], geb[G], gra[G], grb[G];
+    query_chain<FN, CH, V, G>(q, dq0, dq1, dq2, qrow, qok, rrow, rok, lane, D, p, gea, geb, gra, grb);
+    const int64_t slot = p.slot0 + b;
+    float* qb = p.qbuf + slot * 3 * D;
+    float* ge = p.qg_ent + slot * p.ent_w;
+    float* gr = p.qg_rel + slot * p.rel_w;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const int gi = lane + k * kWave;
+        const bool in = gi < DV;
+        const int e = gi * V;
+        vstore<V>(qb + e, q.q0[k], in);
+        vstore<V>(qb + D + e, q.q1[k], in);
+        vstore<V>(qb + 2 * D + e, q.q2[k], in);
+        // a query row that is out of range (TF zero-fill) receives no gradient
+        vstore<V>(ge + e, qok ? gea[k] : vzero<V>(), in);
+        if constexpr (is_split(FN)) vstore<V>(ge + D + e, qok ? geb[k] : vzero<V>(), in);
+        vstore<V>(gr + e, rok ? gra[k] : vzero<V>(), in);
+        if constexpr (rel_split(FN)) vstore<V>(gr + D + e, rok ? grb[k] : vzero<V>(), in);
+    }
+}
+
 template <int FN, bool CH, int V, int G>
 __global__ __launch_bounds__(kBlock) void bwd_rows_kernel(ScoreParams p) {
     constexpr int W = G * V * kWave;  // floats per operand per wave image
@@ -851,32 +895,11 @@ __global__ __launch_bounds__(kBlock) void bwd_rows_kernel(ScoreParams p) {
             dq1[k].a[i] = s1;
             dq2[k].a[i] = s2;
         }
-    const float* qrow = p.qent + (qok ? qi : 0) * p.q_ld;
-    const float* rrow = p.rel + (rok ? ri : 0) * p.r_ld + p.r_off;
-    vecf<V> gea[G], geb[G], gra[G], grb[G];
-    query_chain<FN, CH, V, G>(q, dq0, dq1, dq2, qrow, qok, rrow, rok, lane, D, p, gea, geb, gra, grb);
-    const int64_t slot = p.slot0 + b;
-    float* qb = p.qbuf + slot * 3 * D;
-    float* ge = p.qg_ent + slot * p.ent_w;
-    float* gr = p.qg_rel + slot * p.rel_w;
-#pragma unroll
-    for (int k = 0; k < G; ++k) {
-        const int gi = lane + k * kWave;
-        const bool in = gi < DV;
-        const int e = gi * V;
-        vstore<V>(qb + e, q.q0[k], in);
-        vstore<V>(qb + D + e, q.q1[k], in);
-        vstore<V>(qb + 2 * D + e, q.q2[k], in);
-        // a query row that is out of range (TF zero-fill) receives no gradient
-        vstore<V>(ge + e, qok ? gea[k] : vzero<V>(), in);
-        if constexpr (is_split(FN)) vstore<V>(ge + D + e, qok ? geb[k] : vzero<V>(), in);
-        vstore<V>(gr + e, rok ? gra[k] : vzero<V>(), in);
-        if constexpr (rel_split(FN)) vstore<V>(gr + D + e, rok ? grb[k] : vzero<V>(), in);
-    }
+    rows_finalize<FN, CH, V, G>(p, b, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
     if (lane == 0 && p.dmod_part) {
         float m = red_mod[0];
         for (int ww = 1; ww < kWavesPerBlock; ++ww) m += red_mod[ww];
-        p.dmod_part[slot] = m;
+        p.dmod_part[p.slot0 + b] = m;
     }
 }
 
@@ -1031,6 +1054,193 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Phase 1, streaming form (KIND_BWD_STREAM + KIND_BWD_CHAIN; used when each lane holds >= 4 column
+// groups). The query-side gradient of a slot is a sum over its N candidates of elementwise terms; the
+// only full-row quantities, InterHT's candidate half-norms, come from the forward (cand_stats). So the
+// block's four waves split the COLUMNS (wave w owns groups k = w, w + 4, ...) and each streams all N
+// candidates through its own columns: a wave holds only its query and accumulator groups (no full
+// candidate row), which keeps the kernel at high occupancy with 8 candidates' loads in flight.
+// The chain (normalisation backward of the query, full-row dots) runs afterwards, one wave per slot.
+// ---------------------------------------------------------------------------------------------
+template <int FN, bool CH, int V>
+__device__ __forceinline__ void group_grad(const vecf<V>& ca, const vecf<V>& cb, const vecf<V>& q0, const vecf<V>& q1,
+                                           const vecf<V>& q2, bool in, float g, float ia, float ib,
+                                           const ScoreParams& p, vecf<V>& dq0, vecf<V>& dq1, vecf<V>& dq2,
+                                           float& dmod) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const float x = ca.a[i];
+        if constexpr (FN == KGE_INTERHT) {
+            const float ah = x * ia;
+            const float bh = cb.a[i] * ib + 1.f;
+            if (CH) {
+                const float xx = ah * q1.a[i] - q0.a[i] * bh + q2.a[i];
+                const float Gx = in ? -g * sgnf(xx) : 0.f;
+                dq1.a[i] += Gx * ah;
+                dq0.a[i] += -Gx * bh;
+                dq2.a[i] += Gx;
+            } else {
+                const float xx = q0.a[i] * bh - ah * q1.a[i] + q2.a[i];
+                const float Gx = in ? -g * sgnf(xx) : 0.f;
+                dq0.a[i] += Gx * bh;
+                dq1.a[i] += -Gx * ah;
+                dq2.a[i] += Gx;
+            }
+        } else if constexpr (FN == KGE_TRANSE) {
+            const float r = CH ? (x + q0.a[i]) : (q0.a[i] - x);
+            dq0.a[i] += -g * sgnf(r);
+        } else if constexpr (FN == KGE_DISTMULT) {
+            dq0.a[i] += g * x;
+        } else if constexpr (FN == KGE_COMPLEX) {
+            dq0.a[i] += g * x;
+            dq1.a[i] += g * cb.a[i];
+        } else if constexpr (FN == KGE_ROTATE) {
+            const float xr = q0.a[i] - x, xi = q1.a[i] - cb.a[i];
+            const float m = sqrtf(xr * xr + xi * xi);
+            dq0.a[i] += -g * ((m > 0.f) ? xr / m : 0.f);
+            dq1.a[i] += -g * ((m > 0.f) ? xi / m : 0.f);
+        } else if constexpr (FN == KGE_PROTATE) {
+            const float pc = x / p.phase_div;
+            const float z = CH ? (pc + q0.a[i]) : (q0.a[i] - pc);
+            const float sz = sinf(z);
+            dq0.a[i] += in ? -g * p.modulus * sgnf(sz) * cosf(z) : 0.f;
+            dmod += in ? -g * fabsf(sz) : 0.f;
+        }
+    }
+}
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void bwd_stream_kernel(ScoreParams p) {
+    static_assert(G % kWavesPerBlock == 0, "the streaming phase 1 needs a multiple of 4 groups per lane");
+    constexpr int GW = G / kWavesPerBlock;  // column groups per wave
+    constexpr int U = 8;                     // candidates in flight per wave
+    constexpr bool SPLIT = is_split(FN);
+    __shared__ float red_mod[kWavesPerBlock];
+    const int64_t b = blockIdx.x;
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int D = p.D, DV = D / V;
+    vecf<V> q0w[GW], q1w[GW], q2w[GW], d0[GW], d1[GW], d2[GW];
+    {
+        Query<FN, CH, V, G> q;
+        int64_t qi, ri;
+        bool qok, rok;
+        build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+#pragma unroll
+        for (int gg = 0; gg < GW; ++gg) {
+#pragma unroll
+            for (int kk = 0; kk < G; ++kk)
+                if (kk == w + kWavesPerBlock * gg) {
+                    q0w[gg] = q.q0[kk];
+                    q1w[gg] = q.q1[kk];
+                    q2w[gg] = q.q2[kk];
+                }
+            d0[gg] = d1[gg] = d2[gg] = vzero<V>();
+        }
+    }
+    uint32_t goffs[GW];
+    bool gin[GW];
+#pragma unroll
+    for (int gg = 0; gg < GW; ++gg) {
+        const int k = w + kWavesPerBlock * gg;
+        goffs[gg] = goff<V>(lane, k);
+        gin[gg] = (lane + k * kWave) < DV;
+    }
+    float dmod = 0.f;
+    for (int64_t c0 = 0; c0 < p.N; c0 += kWave) {
+        const int nc = (int)min((int64_t)kWave, p.N - c0);
+        int64_t my_id = 0;
+        float my_g = 0.f;
+        float2 my_st = make_float2(0.f, 0.f);
+        if (lane < nc) {
+            my_id = p.c_idx ? p.c_idx[b * p.c_stride + c0 + lane] : b * p.c_dense + c0 + lane;
+            my_g = p.d_scores[b * p.d_ld + c0 + lane];
+            if constexpr (FN == KGE_INTERHT) my_st = p.cand_stats[b * p.N + c0 + lane];
+        }
+        for (int j = 0; j < nc; j += U) {
+            vecf<V> xa[U][GW], xb[U][GW];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                bool ok = false;
+                const float* row = cand_row(p, readlane64(my_id, min(j + u, nc - 1)), ok);
+                ok = ok && (j + u < nc);
+                const uint32_t nb = ok ? (uint32_t)D * 4u : 0u;
+                const rsrc_t sa = make_rsrc(row, nb);
+#pragma unroll
+                for (int gg = 0; gg < GW; ++gg) xa[u][gg] = bload<V>(sa, goffs[gg]);
+                if constexpr (SPLIT) {
+                    const rsrc_t sb = make_rsrc(row + D, nb);
+#pragma unroll
+                    for (int gg = 0; gg < GW; ++gg) xb[u][gg] = bload<V>(sb, goffs[gg]);
+                } else {
+#pragma unroll
+                    for (int gg = 0; gg < GW; ++gg) xb[u][gg] = vzero<V>();
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (j + u < nc) {  // wave-uniform
+                    const float g = readlanef(my_g, j + u);
+                    float ia = 0.f, ib = 0.f;
+                    if constexpr (FN == KGE_INTERHT) {
+                        ia = readlanef(my_st.x, j + u);
+                        ib = readlanef(my_st.y, j + u);
+                    }
+#pragma unroll
+                    for (int gg = 0; gg < GW; ++gg)
+                        group_grad<FN, CH, V>(xa[u][gg], xb[u][gg], q0w[gg], q1w[gg], q2w[gg], gin[gg], g, ia, ib, p,
+                                              d0[gg], d1[gg], d2[gg], dmod);
+                }
+            }
+        }
+    }
+    // the slot's query-part gradients, in the row layout the chain kernel reads
+    float* dq = p.dqbuf + b * 3 * D;
+#pragma unroll
+    for (int gg = 0; gg < GW; ++gg) {
+        const int e = (lane + (w + kWavesPerBlock * gg) * kWave) * V;
+        vstore<V>(dq + e, d0[gg], gin[gg]);
+        vstore<V>(dq + D + e, d1[gg], gin[gg]);
+        vstore<V>(dq + 2 * D + e, d2[gg], gin[gg]);
+    }
+    if constexpr (FN == KGE_PROTATE) {
+        dmod = wave_sum(dmod);
+        if (lane == 0) red_mod[w] = dmod;
+        __syncthreads();
+        if (threadIdx.x == 0 && p.dmod_part) {
+            float m = red_mod[0];
+            for (int ww = 1; ww < kWavesPerBlock; ++ww) m += red_mod[ww];
+            p.dmod_part[p.slot0 + b] = m;
+        }
+    } else if (threadIdx.x == 0 && p.dmod_part) {
+        p.dmod_part[p.slot0 + b] = 0.f;
+    }
+}
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void bwd_chain_kernel(ScoreParams p) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    const int D = p.D;
+    Query<FN, CH, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+    const float* dq = p.dqbuf + b * 3 * D;
+    const uint32_t nb = (uint32_t)D * 4u;
+    const rsrc_t s0 = make_rsrc(dq, nb), s1 = make_rsrc(dq + D, nb), s2 = make_rsrc(dq + 2 * D, nb);
+    vecf<V> dq0[G], dq1[G], dq2[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        dq0[k] = bload<V>(s0, goff<V>(lane, k));
+        dq1[k] = bload<V>(s1, goff<V>(lane, k));
+        dq2[k] = bload<V>(s2, goff<V>(lane, k));
+    }
+    rows_finalize<FN, CH, V, G>(p, b, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
+}
+
+// ---------------------------------------------------------------------------------------------
 // dispatch over (kind, candidate side, vector width, groups per lane) for one score function
 // ---------------------------------------------------------------------------------------------
 template <int FN, bool CH, int V, int G>
@@ -1041,6 +1251,15 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         hipLaunchKernelGGL((bwd_rows_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_BWD_ENT)
         hipLaunchKernelGGL((bwd_ent_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_BWD_STREAM) {
+        if constexpr (G % kWavesPerBlock == 0)
+            hipLaunchKernelGGL((bwd_stream_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    } else if (kind == KIND_BWD_CHAIN)
+        hipLaunchKernelGGL((bwd_chain_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_FWD_STATS) {
+        if constexpr (FN == KGE_INTERHT)
+            hipLaunchKernelGGL((score_fwd_kernel<FN, CH, V, G, true>), dim3(blocks), dim3(kBlock), 0, st, p);
+    }
     else if (kind == KIND_FINISH) {
         if constexpr (!CH) hipLaunchKernelGGL((finish_kernel<FN, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     } else

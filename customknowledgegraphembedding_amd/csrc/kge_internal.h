@@ -14,7 +14,16 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kMaxG = 8;  // float4 groups per lane per half-row kept in VGPRs (D <= 2048)
 constexpr int kBwdMaxG = 16;  // dword groups per lane of the backward's atomic-friendly layout (D <= 1024)
 
-enum Kind { KIND_FWD = 0, KIND_BWD = 1, KIND_FINISH = 2, KIND_BWD_ROWS = 3, KIND_BWD_ENT = 4 };
+enum Kind {
+    KIND_FWD = 0,
+    KIND_BWD = 1,
+    KIND_FINISH = 2,
+    KIND_BWD_ROWS = 3,
+    KIND_BWD_ENT = 4,
+    KIND_BWD_STREAM = 5,  // phase 1, column-group streaming (one wave per column group, dq -> dqbuf)
+    KIND_BWD_CHAIN = 6,   // phase 1 epilogue of the streaming form (one wave per slot)
+    KIND_FWD_STATS = 7    // forward that also keeps InterHT's candidate norms (train step)
+};
 
 // Parameters of one scoring launch. Rows are addressed as base + row * ld (floats).
 //   query entity row of batch row b:  q_idx ? q_idx[b * q_stride] : b
@@ -63,6 +72,8 @@ struct ScoreParams {
     float* qg_rel;        // [slots, rel_w] gradient of each slot's used relation part
     float* dmod_part;     // [slots] pRotatE modulus gradient partials
     int64_t slot0;        // first slot of a phase-1 launch
+    float2* cand_stats;   // [B * N] per-candidate (1/||a||, 1/||b||) of InterHT, written by the forward
+    float* dqbuf;         // [B, 3 * D] phase-1 query-part gradients (streaming form)
     int64_t ent_w, rel_w; // floats per entity row / per used relation part
     const int* ev_off;    // [E + 1] bucket offsets of the per-entity gradient events (phase 2)
     const int* ev_code;   // event codes, grouped by entity (order inside a bucket: arbitrary)

@@ -216,9 +216,11 @@ class TFKGEModel(_KGEBase):
         ent, rel = self.entity_embedding, self.relation_embedding
         is_p = self.model_name == "pRotatE"
         modulus = float(self.modulus.reshape(-1)[0]) if is_p else 0.0
+        stats = (torch.empty((negative_sample.shape[0] * negative_sample.shape[1], 2), dtype=torch.float32,
+                             device=ent.device) if self.model_name == "InterHT" else None)
         out_neg, out_pos, ns, ps = ops.step_forward_raw(fn, m, ent.detach(), rel.detach(), self._rel_off,
                                                         positive_sample, negative_sample, self._D, self._gamma_f,
-                                                        self._range_f, modulus)
+                                                        self._range_f, modulus, cand_stats=stats)
         w = subsampling_weight.reshape(-1).to(out_neg.dtype)
         sw = torch.sum(w)
         loss = (-torch.sum(w * out_pos) / sw - torch.sum(w * out_neg) / sw) / 2
@@ -253,7 +255,8 @@ class TFKGEModel(_KGEBase):
             optimizer.state[rel]["exp_avg"].data_ptr(), optimizer.state[rel]["exp_avg_sq"].data_ptr(),
             sm["exp_avg"].data_ptr() if is_p else None, sm["exp_avg_sq"].data_ptr() if is_p else None,
             float(lr), float(b1), float(b2), float(group["eps"]), int(step), int(group["semantics"] == "keras"),
-            ws.data_ptr(), ws.numel(), torch.cuda.current_stream(ent.device).cuda_stream)
+            None if stats is None else stats.data_ptr(), ws.data_ptr(), ws.numel(),
+            torch.cuda.current_stream(ent.device).cuda_stream)
         _lib.check(rc, "kge_step_backward_adam")
         return loss.detach()
 

@@ -118,9 +118,10 @@ def score_indexed_bwd_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_r
 
 
 def step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus=0.0,
-                     temperature=1.0, adversarial=True, neg_scores=None):
+                     temperature=1.0, adversarial=True, neg_scores=None, cand_stats=None):
     """Both model calls of supervisor.py:17-18 in two launches -> (out_neg [B], out_pos [B],
-    neg_scores [B, N], pos_scores [B])."""
+    neg_scores [B, N], pos_scores [B]). `cand_stats` ([B*N, 2] fp32, optional) receives InterHT's
+    per-candidate inverse half-norms for the streaming backward."""
     _need_gpu(ent, rel, pos, neg)
     _fp32(ent, "entity_embedding")
     _fp32(rel, "relation_embedding")
@@ -144,7 +145,7 @@ def step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range,
         rel.stride(0), rel_off, pos.data_ptr(), neg.data_ptr(), neg.stride(0), B, N, D,
         float(gamma), float(emb_range), float(modulus), float(temperature), int(bool(adversarial)),
         neg_scores.data_ptr(), neg_scores.stride(0), out_neg.data_ptr(), pos_scores.data_ptr(),
-        out_pos.data_ptr(), _stream(dev))
+        out_pos.data_ptr(), None if cand_stats is None else cand_stats.data_ptr(), _stream(dev))
     check(rc, "kge_step_forward")
     return out_neg, out_pos, neg_scores, pos_scores
 
@@ -398,9 +399,12 @@ class _StepForward(torch.autograd.Function):
     def forward(ctx, ent, rel, modulus_t, pos, neg, fn, mode, rel_off, D, gamma, emb_range,
                 temperature, adversarial, detach):
         modulus = float(modulus_t.item()) if (fn == FN_IDS["pRotatE"]) else 0.0
+        stats = (torch.empty((neg.shape[0] * neg.shape[1], 2), dtype=torch.float32, device=ent.device)
+                 if fn == FN_IDS["InterHT"] else None)
         out_neg, out_pos, ns, ps = step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma,
-                                                    emb_range, modulus, temperature, adversarial)
-        ctx.save_for_backward(ent, rel, pos, neg, ns, ps)
+                                                    emb_range, modulus, temperature, adversarial, cand_stats=stats)
+        ctx.save_for_backward(ent, rel, pos, neg, ns, ps, stats if stats is not None else ps)
+        ctx.has_stats = stats is not None
         ctx.cfg = (fn, mode, rel_off, D, gamma, emb_range, modulus, temperature, adversarial, detach,
                    None if modulus_t is None else modulus_t.shape)
         return out_neg, out_pos
@@ -409,7 +413,8 @@ class _StepForward(torch.autograd.Function):
     def backward(ctx, d_neg, d_pos):
         """kge_step_backward: deterministic two-phase backward (no float atomics); it overwrites
         every row of the gradient tables, so they are allocated uninitialised."""
-        ent, rel, pos, neg, ns, ps = ctx.saved_tensors
+        ent, rel, pos, neg, ns, ps, stats = ctx.saved_tensors
+        stats = stats if ctx.has_stats else None
         (fn, mode, rel_off, D, gamma, emb_range, modulus, temperature, adversarial, detach,
          mod_shape) = ctx.cfg
         lib = _lib.load()
@@ -427,7 +432,7 @@ class _StepForward(torch.autograd.Function):
             rel_off, pos.data_ptr(), neg.data_ptr(), neg.stride(0), B, N, D, float(gamma), float(emb_range),
             float(modulus), float(temperature), int(bool(adversarial)), int(bool(detach)), ns.data_ptr(),
             ns.stride(0), ps.data_ptr(), d_neg.data_ptr(), d_pos.data_ptr(), d_ent.data_ptr(), d_rel.data_ptr(),
-            ctypes_ptr(d_mod), ws.data_ptr(), ws.numel(), _stream(dev))
+            ctypes_ptr(d_mod), ctypes_ptr(stats), ws.data_ptr(), ws.numel(), _stream(dev))
         check(rc, "kge_step_backward")
         if d_mod is not None:
             d_mod = d_mod.view(mod_shape)

@@ -91,6 +91,8 @@ int kge_score_indexed(int fn, int mode,
  *                    (model.py:168-171,195-198), else mean logsigmoid(-s)
  *   pos_scores [B]   raw positive scores, single-mode formula (out, may be NULL)
  *   out_pos    [B]   logsigmoid(positive score) (model.py:145)
+ *   cand_stats [B*N] float2 (may be NULL): InterHT keeps each candidate's inverse half-norms here for
+ *                    kge_step_backward(_adam), whose phase 1 then streams the candidates column-group-wise
  */
 int kge_step_forward(int fn, int mode,
                      const float* ent, int64_t nentity, int64_t ent_ld,
@@ -100,7 +102,7 @@ int kge_step_forward(int fn, int mode,
                      float gamma, float emb_range, float modulus,
                      float temperature, int adversarial,
                      float* neg_scores, int64_t ns_ld, float* out_neg,
-                     float* pos_scores, float* out_pos, void* stream);
+                     float* pos_scores, float* out_pos, float* cand_stats, void* stream);
 
 /*
  * Second half of kge_step_forward, on scores kge_score_indexed already wrote: one wave per batch
@@ -211,7 +213,8 @@ int kge_log_sigmoid_bwd(const float* x, const float* d_out, int64_t n, float* d_
  * atomics: phase 1 reduces each batch row's query-side gradient inside one block; phase 2 walks,
  * for every entity row, the gradient events bucketed to it (counting sort) in a fixed order, so
  * the result is bitwise reproducible. detach != 0: upstream's detached self-adversarial weights.
- * workspace: device scratch of kge_step_backward_workspace_size(fn, nentity, B, N, D) bytes.
+ * cand_stats: the buffer kge_step_forward filled (or NULL; InterHT then uses the register-resident
+ * phase 1). workspace: device scratch of kge_step_backward_workspace_size(fn, nentity, B, N, D) bytes.
  */
 int64_t kge_step_backward_workspace_size(int fn, int64_t nentity, int64_t B, int64_t N, int64_t D);
 int kge_step_backward(int fn, int mode,
@@ -223,7 +226,7 @@ int kge_step_backward(int fn, int mode,
                       float temperature, int adversarial, int detach,
                       const float* neg_scores, int64_t ns_ld, const float* pos_scores,
                       const float* d_out_neg, const float* d_out_pos,
-                      float* d_ent, float* d_rel, float* d_modulus,
+                      float* d_ent, float* d_rel, float* d_modulus, const float* cand_stats,
                       void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
@@ -248,7 +251,7 @@ int kge_step_backward_adam(int fn, int mode,
                            const float* d_out_neg, const float* d_out_pos,
                            float* m_ent, float* v_ent, float* m_rel, float* v_rel, float* m_mod, float* v_mod,
                            float lr, float beta1, float beta2, float eps, int64_t step, int keras,
-                           void* workspace, int64_t workspace_bytes, void* stream);
+                           const float* cand_stats, void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
  * TranSparse scores (tensorflow_codes/model.py:226-235, gathers at :139-142, :161-164, :187-190; tables

@@ -103,6 +103,7 @@ SIGNATURES = {
     "kge_transparse_score_bwd": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p,
                                         _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p,
                                         ctypes.c_size_t, _c_p]),
+    "kge_step_loss": (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p]),
     "kge_crc32c": (ctypes.c_uint32, [_c_p, _c_i64]),
     "kge_tfrecord_open": (_c_p, [_c_p, _c_i64, _c_i]),
     "kge_tfrecord_next": (_c_i, [_c_p, _c_p]),

@@ -70,6 +70,42 @@ __global__ __launch_bounds__(kBlock) void log_sigmoid_kernel(const float* __rest
     if (i < n) out[i] = log_sigmoid(x[i]);
 }
 
+// Weighted train-step loss of supervisor.py:19-23 and its gradient, one block, fixed reduction order:
+//   loss = (-sum(w * pos) / sum(w) - sum(w * neg) / sum(w)) / 2,   d_out[b] = (-0.5 / sum(w)) * w[b]
+constexpr int kLossBlock = 1024;
+__global__ __launch_bounds__(kLossBlock) void step_loss_kernel(const float* __restrict__ out_neg,
+                                                               const float* __restrict__ out_pos,
+                                                               const float* __restrict__ w, int64_t B,
+                                                               float* __restrict__ loss, float* __restrict__ d_out) {
+    __shared__ float red[3][kLossBlock];
+    const int t = threadIdx.x;
+    float sw = 0.f, sp = 0.f, sn = 0.f;
+    for (int64_t b = t; b < B; b += kLossBlock) {
+        const float wb = w[b];
+        sw += wb;
+        sp += wb * out_pos[b];
+        sn += wb * out_neg[b];
+    }
+    red[0][t] = sw;
+    red[1][t] = sp;
+    red[2][t] = sn;
+    __syncthreads();
+    for (int o = kLossBlock / 2; o > 0; o >>= 1) {
+        if (t < o) {
+            red[0][t] += red[0][t + o];
+            red[1][t] += red[1][t + o];
+            red[2][t] += red[2][t + o];
+        }
+        __syncthreads();
+    }
+    const float tw = red[0][0];
+    if (t == 0 && loss) *loss = (-red[1][0] / tw + -red[2][0] / tw) / 2.f;
+    if (d_out) {
+        const float c = -0.5f / tw;
+        for (int64_t b = t; b < B; b += kLossBlock) d_out[b] = c * w[b];
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void log_sigmoid_bwd_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ d_out, int64_t n,
                                                                  float* __restrict__ d_x) {
@@ -669,6 +705,15 @@ int kge_log_sigmoid(const float* x, int64_t n, float* out, void* stream) {
     hipLaunchKernelGGL(log_sigmoid_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        (hipStream_t)stream, x, n, out);
     return check_launch("kge_log_sigmoid");
+}
+
+int kge_step_loss(const float* out_neg, const float* out_pos, const float* weight, int64_t B, float* loss,
+                  float* d_out, void* stream) {
+    if (B <= 0) return fail(KGE_EINVAL, "kge_step_loss needs B > 0");
+    if (!out_neg || !out_pos || !weight || (!loss && !d_out)) return fail(KGE_EINVAL, "null pointer");
+    hipLaunchKernelGGL(step_loss_kernel, dim3(1), dim3(kLossBlock), 0, (hipStream_t)stream, out_neg, out_pos, weight, B,
+                       loss, d_out);
+    return check_launch("kge_step_loss");
 }
 
 int kge_log_sigmoid_bwd(const float* x, const float* d_out, int64_t n, float* d_x, void* stream) {

@@ -221,10 +221,8 @@ class TFKGEModel(_KGEBase):
         out_neg, out_pos, ns, ps = ops.step_forward_raw(fn, m, ent.detach(), rel.detach(), self._rel_off,
                                                         positive_sample, negative_sample, self._D, self._gamma_f,
                                                         self._range_f, modulus, cand_stats=stats)
-        w = subsampling_weight.reshape(-1).to(out_neg.dtype)
-        sw = torch.sum(w)
-        loss = (-torch.sum(w * out_pos) / sw - torch.sum(w * out_neg) / sw) / 2
-        d_out = ((-0.5 / sw) * w).contiguous()  # the op order autograd uses for this loss
+        # supervisor.py:19-23 and its gradient in one launch (the same kernel as the autograd path)
+        loss, d_out = ops.step_loss_raw(out_neg, out_pos, subsampling_weight)
         from .optim import resolve_lr
 
         group = optimizer.param_groups[0]

@@ -470,6 +470,38 @@ def transparse_score(mode, ent, rel, W, mask, pos, neg, gamma):
     return _TranSparse.apply(ent, rel, W, mask, pos, neg, mode, float(gamma))
 
 
+def step_loss_raw(out_neg, out_pos, weight, want_grad=True):
+    """supervisor.py:19-23 in one HIP launch -> (loss 0-dim, d_out [B] or None)."""
+    _need_gpu(out_neg, out_pos, weight)
+    B = out_neg.numel()
+    n, p_, w = (t.reshape(-1).contiguous().to(torch.float32) for t in (out_neg, out_pos, weight))
+    loss = torch.empty((), dtype=torch.float32, device=n.device)
+    d_out = torch.empty(B, dtype=torch.float32, device=n.device) if want_grad else None
+    check(_lib.load().kge_step_loss(n.data_ptr(), p_.data_ptr(), w.data_ptr(), B, loss.data_ptr(), ctypes_ptr(d_out),
+                                    _stream(n.device)), "kge_step_loss")
+    return loss, d_out
+
+
+class _StepLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out_neg, out_pos, weight):
+        loss, d_out = step_loss_raw(out_neg, out_pos, weight)
+        ctx.save_for_backward(d_out)
+        ctx.shapes = (out_neg.shape, out_pos.shape)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (d_out,) = ctx.saved_tensors
+        d = d_out * g
+        return d.view(ctx.shapes[0]), d.view(ctx.shapes[1]), None
+
+
+def step_loss(out_neg, out_pos, weight):
+    """The weighted loss of supervisor.py:19-23, differentiable w.r.t. both outputs."""
+    return _StepLoss.apply(out_neg, out_pos, weight)
+
+
 def step_forward(fn, mode, ent, rel, pos, neg, D, gamma, emb_range, rel_off=0, modulus=None,
                  temperature=1.0, adversarial=True, detach=False):
     """Fused, differentiable forward of both model calls of one train step -> (neg [B], pos [B])."""

@@ -90,6 +90,10 @@ class Trainer:
     def loss(self, positive_sample, negative_sample, subsampling_weight, mode):
         """supervisor.py:17-23 — both calls fused, then the weighted loss."""
         negative_score, positive_score = self.model.step_forward(positive_sample, negative_sample, mode[0])
+        if negative_score.is_cuda:
+            from . import ops
+
+            return ops.step_loss(negative_score, positive_score, subsampling_weight)
         w = subsampling_weight.reshape(-1, 1).to(negative_score.dtype)
         positive_sample_loss = -torch.sum(w * positive_score) / torch.sum(w)
         negative_sample_loss = -torch.sum(w * negative_score) / torch.sum(w)

@@ -204,6 +204,15 @@ int kge_neg_reduce_bwd(const float* scores, int64_t B, int64_t N, int64_t ld,
                        const float* d_out, float* d_scores, int64_t d_ld, void* stream);
 
 /* d_x[i] = d_out[i] * sigmoid(-x[i])  (backward of kge_log_sigmoid). */
+/*
+ * The weighted loss of the train step (supervisor.py:19-23) over the two [B] outputs of
+ * kge_step_forward, and its gradient: loss = (-sum(w*pos)/sum(w) - sum(w*neg)/sum(w)) / 2 (device
+ * scalar, may be NULL), d_out[b] = dloss/dout_neg[b] = dloss/dout_pos[b] = (-0.5/sum(w)) * w[b]
+ * (may be NULL). One block, fixed reduction order (deterministic).
+ */
+int kge_step_loss(const float* out_neg, const float* out_pos, const float* weight, int64_t B, float* loss,
+                  float* d_out, void* stream);
+
 int kge_log_sigmoid_bwd(const float* x, const float* d_out, int64_t n, float* d_x, void* stream);
 
 /*

@@ -13,7 +13,7 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
         k = row["Kernel_Name"]
-        k = k.split("(")[0].replace("void ", "").replace("kge_impl::", "")
+        k = k.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("kge_impl::", "")
         per = vals[k][row["Counter_Name"]]
         per.append(float(row["Counter_Value"]))
 out = []

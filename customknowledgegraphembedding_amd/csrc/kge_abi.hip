@@ -371,8 +371,9 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         p.cpw = 1;
         p.wpr = 1;
         waves = p.B;
-    } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM) {
-        waves = p.B * kWavesPerBlock;  // one block per slot
+    } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM || kind == KIND_STEP_FWD ||
+               kind == KIND_STEP_FWD_STATS) {
+        waves = p.B * kWavesPerBlock;  // one block per slot / batch row
     } else if (kind == KIND_BWD_CHAIN) {
         waves = p.B;  // one wave per slot
     } else if (kind == KIND_BWD_ENT) {
@@ -545,11 +546,14 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
     p.out = neg_scores;
     p.out_ld = ns_ld;
     p.cand_stats = reinterpret_cast<float2*>(cand_stats);
-    rc = run_score(fn, mode, p, (cand_stats && fn == KGE_INTERHT) ? KIND_FWD_STATS : KIND_FWD, stream);
-    if (rc) return rc;
-    return kge_step_finish(fn, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, B, D, gamma, emb_range,
-                           modulus, neg_scores, N, ns_ld, temperature, adversarial, out_neg, pos_scores, out_pos,
-                           stream);
+    p.pos_base = pos;
+    p.temperature = temperature;
+    p.adversarial = adversarial;
+    p.out_neg = out_neg;
+    p.out_pos_raw = pos_scores;
+    p.out_pos_ls = out_pos;
+    // one launch: negatives + the per-row finish (positive, reduction)
+    return run_score(fn, mode, p, (cand_stats && fn == KGE_INTERHT) ? KIND_STEP_FWD_STATS : KIND_STEP_FWD, stream);
 }
 
 int kge_score_sharded(int fn, int mode, const float* qent, int64_t q_ld, const float* rel, int64_t nrelation,

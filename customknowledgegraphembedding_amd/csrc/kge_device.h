@@ -360,22 +360,16 @@ __device__ __forceinline__ const float* cand_row(const ScoreParams& p, int64_t i
     return p.cent + (ok ? id : 0) * p.c_ld;
 }
 
-template <int FN, bool CH, int V, int G, bool ST = false>
-__global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
-    WaveTask t;
-    if (!wave_task(p, t)) return;
-    const int lane = threadIdx.x & 63;
-    Query<FN, CH, V, G> q;
-    int64_t qi, ri;
-    bool qok, rok;
-    build_query_for<FN, CH, V, G>(p, t.b, lane, q, qi, ri, qok, rok);
-
+// Scores candidates [n0, n0 + nc) (nc <= 64) of batch row b against the wave's query; score n0 + j
+// is produced in lane j and stored coalesced (and, with ST, InterHT's candidate inverse half-norms).
+template <int FN, bool CH, int V, int G, bool ST>
+__device__ __forceinline__ void score_run(const ScoreParams& p, const Query<FN, CH, V, G>& q, int64_t b, int64_t n0,
+                                          int nc, int lane) {
     int64_t my_id = 0;
-    if (lane < t.nc) my_id = p.c_idx ? p.c_idx[t.b * p.c_stride + t.n0 + lane] : t.b * p.c_dense + t.n0 + lane;
+    if (lane < nc) my_id = p.c_idx ? p.c_idx[b * p.c_stride + n0 + lane] : b * p.c_dense + n0 + lane;
 
     // software pipeline: row j+1 is in flight while row j is reduced. A foreign candidate of a
     // row-sharded table (skip_foreign) loads nothing (0-byte descriptor) and scores 0.
-    // InterHT with cand_stats: the candidate's inverse half-norms are kept (lane j) for the backward.
     float my_score = 0.f;
     float2 my_st = make_float2(0.f, 0.f), st;
     float2* stp = ST ? &st : nullptr;
@@ -390,7 +384,7 @@ __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
             if constexpr (ST) my_st = st;
         }
     };
-    for (; j + 2 < t.nc; j += 2) {
+    for (; j + 2 < nc; j += 2) {
         row = cand_row(p, readlane64(my_id, j + 1), ok1);
         x1.load(row, ok1, p.D, lane);
         const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
@@ -400,7 +394,7 @@ __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
         const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p, stp);
         keep(j + 1, s1);
     }
-    if (j + 1 < t.nc) {
+    if (j + 1 < nc) {
         row = cand_row(p, readlane64(my_id, j + 1), ok1);
         x1.load(row, ok1, p.D, lane);
         const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
@@ -411,10 +405,22 @@ __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
         const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
         keep(j, s0);
     }
-    if (lane < t.nc) p.out[t.b * p.out_ld + t.n0 + lane] = my_score;
+    if (lane < nc) p.out[b * p.out_ld + n0 + lane] = my_score;
     if constexpr (ST) {
-        if (lane < t.nc) p.cand_stats[t.b * p.N + t.n0 + lane] = my_st;
+        if (lane < nc) p.cand_stats[b * p.N + n0 + lane] = my_st;
     }
+}
+
+template <int FN, bool CH, int V, int G, bool ST = false>
+__global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
+    WaveTask t;
+    if (!wave_task(p, t)) return;
+    const int lane = threadIdx.x & 63;
+    Query<FN, CH, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, CH, V, G>(p, t.b, lane, q, qi, ri, qok, rok);
+    score_run<FN, CH, V, G, ST>(p, q, t.b, t.n0, t.nc, lane);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -441,28 +447,59 @@ __device__ __forceinline__ float row_reduce(const float* row, int64_t N, float T
     return wave_sum(w) / (float)N;
 }
 
+// One batch row's finish: the positive (h, r, t) scored with the single-mode (tail) formula, and the
+// reduction of the row's N negative scores. `pos` is the [B, 3] positive batch.
 template <int FN, int V, int G>
-__global__ __launch_bounds__(kBlock) void finish_kernel(ScoreParams p) {
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (b >= p.B) return;
-    const int lane = threadIdx.x & 63;
+__device__ __forceinline__ void finish_row(const ScoreParams& p, const int64_t* pos, int64_t b, int lane,
+                                           const float* scores, int64_t n_neg) {
     // issue every independent load before the first reduction: the positive tail row, then the
     // query rows (h, r), then the negative row's scores (latency-bound: one wave per batch row)
     bool ok;
-    const float* row = cand_row(p, p.c_idx ? p.c_idx[b * p.c_stride] : b, ok);
+    const float* row = cand_row(p, pos[b * 3 + 2], ok);
     Cand<FN, V, G> c;
     c.load(row, ok, p.D, lane);
     Query<FN, false, V, G> q;
-    int64_t qi, ri;
-    bool qok, rok;
-    build_query_for<FN, false, V, G>(p, b, lane, q, qi, ri, qok, rok);
-    const float red = row_reduce(p.neg_scores + b * p.ns_ld, p.n_neg, p.temperature, p.adversarial, lane);
+    const int64_t qi = pos[b * 3], ri = pos[b * 3 + 1];
+    const bool qok = qi >= 0 && qi < p.q_rows, rok = ri >= 0 && ri < p.r_rows;
+    q.build(p.qent + (qok ? qi : 0) * p.q_ld, qok, p.rel + (rok ? ri : 0) * p.r_ld + p.r_off, rok, p.D, lane, p);
+    const float red = row_reduce(scores, n_neg, p.temperature, p.adversarial, lane);
     const float s = cand_score<FN, false, V, G>(c, q, p);
     if (lane == 0) {
         if (p.out_pos_raw) p.out_pos_raw[b] = s;
         p.out_pos_ls[b] = log_sigmoid(s);
         p.out_neg[b] = red;
     }
+}
+
+template <int FN, int V, int G>
+__global__ __launch_bounds__(kBlock) void finish_kernel(ScoreParams p) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= p.B) return;
+    // single-mode parameters: q_idx = pos (h column), stride 3
+    finish_row<FN, V, G>(p, p.q_idx, b, threadIdx.x & 63, p.neg_scores + b * p.ns_ld, p.n_neg);
+}
+
+// Fused train-step forward (kge_step_forward): one block per batch row. The four waves score a
+// quarter of the row's negatives each (the scoring code above), then wave 0 runs the row's finish
+// (positive + reduction) once the block's scores are written: one launch instead of two, and the
+// finish's latency overlaps the other rows' gathers instead of following the whole negative pass.
+template <int FN, bool CH, int V, int G, bool ST>
+__global__ __launch_bounds__(kBlock) void step_fwd_kernel(ScoreParams p) {
+    const int64_t b = blockIdx.x;
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    {
+        Query<FN, CH, V, G> q;
+        int64_t qi, ri;
+        bool qok, rok;
+        build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+        const int64_t per = (p.N + kWavesPerBlock - 1) / kWavesPerBlock;
+        const int64_t lo = w * per, hi = min(p.N, lo + per);
+        for (int64_t c0 = lo; c0 < hi; c0 += kWave)
+            score_run<FN, CH, V, G, ST>(p, q, b, c0, (int)min((int64_t)kWave, hi - c0), lane);
+    }
+    __syncthreads();  // the row's scores are in memory, visible to the block
+    if (w == 0) finish_row<FN, V, G>(p, p.pos_base, b, lane, p.out + b * p.out_ld, p.N);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1259,6 +1296,12 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
     else if (kind == KIND_FWD_STATS) {
         if constexpr (FN == KGE_INTERHT)
             hipLaunchKernelGGL((score_fwd_kernel<FN, CH, V, G, true>), dim3(blocks), dim3(kBlock), 0, st, p);
+    }
+    else if (kind == KIND_STEP_FWD)
+        hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, false>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_STEP_FWD_STATS) {
+        if constexpr (FN == KGE_INTERHT)
+            hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, true>), dim3(blocks), dim3(kBlock), 0, st, p);
     }
     else if (kind == KIND_FINISH) {
         if constexpr (!CH) hipLaunchKernelGGL((finish_kernel<FN, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);

@@ -22,7 +22,9 @@ enum Kind {
     KIND_BWD_ENT = 4,
     KIND_BWD_STREAM = 5,  // phase 1, column-group streaming (one wave per column group, dq -> dqbuf)
     KIND_BWD_CHAIN = 6,   // phase 1 epilogue of the streaming form (one wave per slot)
-    KIND_FWD_STATS = 7    // forward that also keeps InterHT's candidate norms (train step)
+    KIND_FWD_STATS = 7,   // forward that also keeps InterHT's candidate norms (train step)
+    KIND_STEP_FWD = 8,    // fused train-step forward: block per batch row, negatives + finish in one launch
+    KIND_STEP_FWD_STATS = 9
 };
 
 // Parameters of one scoring launch. Rows are addressed as base + row * ld (floats).
@@ -73,6 +75,7 @@ struct ScoreParams {
     float* dmod_part;     // [slots] pRotatE modulus gradient partials
     int64_t slot0;        // first slot of a phase-1 launch
     float2* cand_stats;   // [B * N] per-candidate (1/||a||, 1/||b||) of InterHT, written by the forward
+    const int64_t* pos_base;  // [B, 3] positive triples (fused step forward)
     float* dqbuf;         // [B, 3 * D] phase-1 query-part gradients (streaming form)
     int64_t ent_w, rel_w; // floats per entity row / per used relation part
     const int* ev_off;    // [E + 1] bucket offsets of the per-entity gradient events (phase 2)

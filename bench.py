@@ -402,8 +402,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--train-steps", type=int, default=10, help="train-step side measurement (0 = skip)")
-    ap.add_argument("--event-every", type=int, default=5,
-                    help="bracket every k-th launch with timing events (odd k samples both modes)")
+    ap.add_argument("--event-group", type=int, default=5,
+                    help="timing events bracket groups of this many consecutive launches")
     ap.add_argument("--sharded-steps", type=int, default=20,
                     help="side measurement of the YAGO3-10 row-sharded step (c4s) at the same world size (0 = skip)")
     a = ap.parse_args()
@@ -463,23 +463,42 @@ def main():
         run_step(m, pos, neg, i % 2, fn)
     torch.cuda.synchronize()
 
-    # kernel timing: events bracket every `ev_every`-th launch (odd, so both modes are sampled); the
-    # event packets are kept off the other launches so the wall-clock step is not perturbed by them
-    ev_every = max(1, a.event_every)
-    evs = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for i in range(a.steps) if i % ev_every == 0}
+    # kernel timing: event pairs bracket groups of `ev_group` consecutive launches (every other
+    # group), so the event packets are amortised over several kernels and kept off most launches
+    # (a bracket around every single launch adds ~3 us to each step)
+    ev_group = max(1, a.event_group)
+    evs = {}
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
         pos, neg = batches[i % len(batches)]
-        run_step(m, pos, neg, i % 2, fn, evs.get(i))
+        g, r = divmod(i, ev_group)
+        if g % 2 == 0 and r == 0 and i + ev_group <= a.steps:
+            evs[g] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            evs[g][0].record()
+        run_step(m, pos, neg, i % 2, fn)
+        if g in evs and r == ev_group - 1:
+            evs[g][1].record()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in sorted(evs)]
-    head_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in sorted(evs) if i % 2 == 0]
-    tail_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in sorted(evs) if i % 2 == 1]
+    kern_ms = [evs[g][0].elapsed_time(evs[g][1]) / ev_group for g in sorted(evs)]
+    # SURVEY §8d per-mode kernel times, after the timed region: one event pair around ev_group
+    # consecutive launches of the same mode
+    per_mode = {}
+    for mode in (0, 1):
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        e[0].record()
+        for i in range(ev_group):
+            pos, neg = batches[i % len(batches)]
+            run_step(m, pos, neg, mode, fn)
+        e[1].record()
+        torch.cuda.synchronize()
+        per_mode[mode] = e[0].elapsed_time(e[1]) / ev_group
+    head_ms, tail_ms = [per_mode[0]], [per_mode[1]]
+    if not kern_ms:  # fewer steps than one event group
+        kern_ms = head_ms + tail_ms
     if dist:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -518,8 +537,8 @@ def main():
                      "traffic_source": traffic_src,
                      "kernel": "step_fwd_kernel (negatives + positives + row reductions, one launch)",
                      "kernel_avg_us": kern_avg_s * 1e6,
-                     "kernel_avg_us_head_batch": statistics.mean(head_ms) * 1e3 if head_ms else None,
-                     "kernel_avg_us_tail_batch": statistics.mean(tail_ms) * 1e3 if tail_ms else None,
+                     "kernel_avg_us_head_batch": head_ms[0] * 1e3,
+                     "kernel_avg_us_tail_batch": tail_ms[0] * 1e3,
                      "algorithmic_bytes_per_launch": step_bytes,
                      "unique_row_bytes_per_step": uniq * ent_dim_ * 4,
                      "row_reuse": (B * N + 2 * B) / max(1, uniq)},

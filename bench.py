@@ -172,9 +172,11 @@ def sharded_bench(w, a, world, rank, device, dist_on):
     return time.perf_counter() - t0
 
 
-def eval_bench(w, a, device):
+def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
     """c5: upstream test_step's scoring + filtered ranking for batches of queries: kge_eval_query +
-    kge_gemm_nt (fp32 MFMA, events around it) + kge_rank_filtered. Returns the JSON line."""
+    kge_gemm_nt (fp32 MFMA, events around it) + kge_rank_filtered. Multi-GPU = replicas: every rank
+    holds the (60 MB) table and ranks its own query batches (weak scaling, no collective in the
+    data path); value = all ranks' queries / max elapsed. Returns the JSON line."""
     from customknowledgegraphembedding_amd import evaluate
     from customknowledgegraphembedding_amd.model import KGEModel
     m = KGEModel(w["fn"], w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"], device=device, seed=0)
@@ -183,7 +185,7 @@ def eval_bench(w, a, device):
     true = np.stack([g.randint(E, size=200000), g.randint(R, size=200000), g.randint(E, size=200000)], 1)
     batches = []
     for i in range(4):
-        q = true[i * Bq:(i + 1) * Bq]
+        q = true[(rank * 4 + i) * Bq:(rank * 4 + i + 1) * Bq]
         mode = "head-batch" if i % 2 == 0 else "tail-batch"
         ptr, ids = evaluate.build_filter(q, mode, true)
         col = 0 if mode == "head-batch" else 2
@@ -213,21 +215,35 @@ def eval_bench(w, a, device):
         step(batches[i % 4])
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if dist_on:
+        import torch.distributed as tdist
+        tdist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     ranks = []
     for i in range(a.steps):
         ranks.append(step(batches[i % 4], evs[i]))
     torch.cuda.synchronize()
+    if dist_on:
+        tdist.barrier()
     dt = time.perf_counter() - t0
     gemm_s = statistics.mean(e0.elapsed_time(e1) for e0, e1 in evs) / 1e3
     flops = 2.0 * Bq * E * K
-    r = torch.cat(ranks).cpu().numpy()
-    met = evaluate.metrics_from_ranks(r)
-    return {"metric": f"ranked queries/sec, {w['name']}", "value": Bq * a.steps / dt, "unit": "queries/s",
-            "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+    r = torch.cat(ranks)
+    if dist_on:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+        allr = [torch.empty_like(r) for _ in range(world)]
+        tdist.all_gather(allr, r)
+        r = torch.cat(allr)
+    met = evaluate.metrics_from_ranks(r.cpu().numpy())
+    return {"metric": f"ranked queries/sec, {w['name']}", "value": Bq * a.steps * world / dt, "unit": "queries/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic triples (random init: MRR is not a quality number)",
-            "config": {"workload": w["name"], "queries_per_step": Bq, "entities": E, "K": K},
+            "config": {"workload": w["name"], "queries_per_step": Bq * world, "entities": E, "K": K,
+                       "parallelism": f"replicas{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": flops / gemm_s / 1e12, "peak": 157.3, "unit": "TFLOP/s",
                          "frac": flops / gemm_s / 1e12 / 157.3, "traffic": None,
                          "kernel": "gemm_nt_f32_kernel (v_mfma_f32_32x32x2_f32)", "kernel_avg_us": gemm_s * 1e6},
@@ -423,7 +439,8 @@ def main():
     fn = FN_IDS.get(w["fn"])
     B, N = w["B"], w["N"]
     if w.get("eval") or w.get("transparse"):
-        line = eval_bench(w, a, device) if w.get("eval") else transparse_bench(w, a, device)
+        line = (eval_bench(w, a, device, world, rank, dist) if w.get("eval")
+                else transparse_bench(w, a, device))
         if rank == 0:
             print(json.dumps(line), flush=True)
         if dist:

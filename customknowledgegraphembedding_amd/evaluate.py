@@ -106,6 +106,13 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
     bs = batch_size or int(getattr(args, "test_batch_size", 1024) or 1024)
     dev = model.entity_embedding.device
     triples = np.asarray(test_triples, dtype=np.int64).reshape(-1, 3)
+    # multi-GPU: replicas. Each rank ranks a strided share of the test triples against its own copy
+    # of the table; the integer ranks are all-gathered before the metrics (no collective while scoring)
+    import torch.distributed as dist
+
+    world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+    if world > 1:
+        triples = triples[dist.get_rank()::world]
     all_ranks = []
     with torch.no_grad():
         for mode in ("head-batch", "tail-batch"):
@@ -119,7 +126,12 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
                 fptr = torch.from_numpy(p - p[0]).to(dev)
                 fids = torch.from_numpy(ids[p[0]:p[-1]]).to(dev)
                 all_ranks.append(rank_filtered(S, pos[:, col].contiguous(), fptr, fids).cpu().numpy())
-    return metrics_from_ranks(np.concatenate(all_ranks))
+    ranks = np.concatenate(all_ranks) if all_ranks else np.zeros(0, dtype=np.int64)
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ranks)
+        ranks = np.concatenate(gathered)
+    return metrics_from_ranks(ranks)
 
 
 __all__ = ["build_filter", "score_all", "rank_filtered", "metrics_from_ranks", "test_step", "HEAD_BATCH",

@@ -237,8 +237,12 @@ int launch_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K
     const int64_t tm = (M + GBM - 1) / GBM;
     const int64_t t128 = tm * ((N + 127) / 128), t64 = tm * ((N + 63) / 64);
     int bn = t128 < 256 ? 64 : 128;
-    if (const char* env = getenv("KGE_GEMM_BN")) bn = atoi(env) == 64 ? 64 : 128;  // tuning override
-    if (bn == 64)
+    const int64_t t256 = tm * ((N + 255) / 256);
+    if (const char* env = getenv("KGE_GEMM_BN")) bn = atoi(env) == 64 ? 64 : (atoi(env) == 256 ? 256 : 128);
+    if (bn == 256)
+        hipLaunchKernelGGL(gemm_nt_f32_kernel<256>, dim3((unsigned)t256), dim3(kBlock), 0, st, A, B, C, M, N, K, lda,
+                           ldb, ldc);
+    else if (bn == 64)
         hipLaunchKernelGGL(gemm_nt_f32_kernel<64>, dim3((unsigned)t64), dim3(kBlock), 0, st, A, B, C, M, N, K, lda,
                            ldb, ldc);
     else

@@ -88,16 +88,11 @@ class Trainer:
         self.fused = bool(fused)
 
     def loss(self, positive_sample, negative_sample, subsampling_weight, mode):
-        """supervisor.py:17-23 — both calls fused, then the weighted loss."""
-        negative_score, positive_score = self.model.step_forward(positive_sample, negative_sample, mode[0])
-        if negative_score.is_cuda:
-            from . import ops
+        """supervisor.py:17-23 — both calls fused, then the weighted loss (one HIP launch each)."""
+        from . import ops
 
-            return ops.step_loss(negative_score, positive_score, subsampling_weight)
-        w = subsampling_weight.reshape(-1, 1).to(negative_score.dtype)
-        positive_sample_loss = -torch.sum(w * positive_score) / torch.sum(w)
-        negative_sample_loss = -torch.sum(w * negative_score) / torch.sum(w)
-        return (positive_sample_loss + negative_sample_loss) / 2
+        negative_score, positive_score = self.model.step_forward(positive_sample, negative_sample, mode[0])
+        return ops.step_loss(negative_score, positive_score, subsampling_weight)  # kge_step_loss
 
     def train_step(self, data_iter):
         """supervisor.py:13-30."""

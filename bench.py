@@ -52,10 +52,10 @@ WORKLOADS = {
     # configs[3] as the north star states it: entity table row-sharded over the ranks
     # (owner-computes, distributed.ShardedKGE; bz=512 per rank)
     # configs[4]: FB15k link-prediction eval, each query vs all 14 951 entities, filtered ranks
-    # (DistMult d=1000 assumed); a step = one batch of 1024 queries, one mode
-    "c5": dict(name="FB15k filtered eval DistMult d=1000, 1024 queries/step vs all 14951 entities",
+    # (DistMult d=1000 assumed); a step = one batch of 4096 queries, one mode
+    "c5": dict(name="FB15k filtered eval DistMult d=1000, 4096 queries/step vs all 14951 entities",
                fn="DistMult", nentity=14951, nrelation=1345, hidden_dim=1000, gamma=24.0, de=False, tr=False,
-               dr=False, B=1024, N=14951, eval=True),
+               dr=False, B=4096, N=14951, eval=True),
     # TranSparse (model.py:226-235; in the reference's model_func dict, not in a BASELINE config):
     # WN18RR-sized graph, d=500, head-batch (the only mode whose scores depend on the negatives, Q9)
     "c6": dict(name="WN18RR-sized TranSparse d=500 gamma=12 n_neg=256 bz=512 head-batch", fn="TranSparse",

@@ -334,3 +334,24 @@ def test_fused_step_train_grads(path):
         assert rel_close(loss.item(), z[f"loss_mode{mode}"]) <= TOL
         assert _grad_close(m.entity_embedding.grad.cpu(), z[f"d_ent_mode{mode}"]), name
         assert _grad_close(m.relation_embedding.grad.cpu(), z[f"d_rel_mode{mode}"]), name
+
+
+@pytest.mark.parametrize("name", FNS)
+@pytest.mark.parametrize("N", [1, 3, 67, 1030])
+def test_fused_step_kernel_any_n(name, N):
+    """The fused step kernel (block per batch row, four waves splitting the row's N negatives, wave 0
+    finishing the row) equals the separate scoring + reduction + positive calls bitwise for N that
+    do not split evenly over the waves, including N < 4 and more than 256 per wave."""
+    em, rm = MULT[name]
+    E, R, d, B = 300, 5, 24, 7
+    m = kge.TFKGEModel(name, E, R, d, 9.0, double_entity_embedding=(em == 2),
+                       double_relation_embedding=(name == "ComplEx"), triple_relation_embedding=(rm == 3),
+                       device=DEV, seed=3)
+    g = np.random.RandomState(N)
+    pos = torch.from_numpy(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1)).to(DEV)
+    neg = torch.from_numpy(g.randint(E, size=(B, N))).to(DEV)
+    with torch.no_grad():
+        for mode in (0, 1):
+            n, p = m.step_forward(pos, neg, mode)
+            assert torch.equal(n, m(((pos, neg), mode)))
+            assert torch.equal(p, m(((pos, neg), 3)))

@@ -100,9 +100,53 @@ def metrics_from_ranks(ranks: np.ndarray) -> dict:
             "HITS@3": float(np.mean(r <= 3.0)), "HITS@10": float(np.mean(r <= 10.0))}
 
 
+def average_precision(y_true, y_score) -> float:
+    """Average precision = area under the precision-recall curve, as sklearn's
+    average_precision_score (the metric upstream test_step reports as auc_pr for countries):
+    sum over distinct score thresholds (descending) of (R_n - R_{n-1}) * P_n."""
+    y_true = np.asarray(y_true, dtype=np.float64).reshape(-1)
+    y_score = np.asarray(y_score, dtype=np.float64).reshape(-1)
+    order = np.argsort(-y_score, kind="mergesort")
+    y_true, y_score = y_true[order], y_score[order]
+    last = np.r_[np.where(np.diff(y_score) != 0)[0], y_true.size - 1]  # last index of each tie group
+    tps = np.cumsum(y_true)[last]
+    fps = (last + 1) - tps
+    if tps[-1] == 0:
+        return 0.0
+    precision = tps / (tps + fps)
+    recall = tps / tps[-1]
+    return float(np.sum(np.diff(np.r_[0.0, recall]) * precision))
+
+
+def read_regions(data_path, entity2id):
+    """Upstream run.py: the countries datasets' candidate regions (data/countries_S*/regions.list)."""
+    import os
+
+    with open(os.path.join(data_path, "regions.list")) as fin:
+        return [entity2id[line.strip()] for line in fin if line.strip()]
+
+
+def countries_auc_pr(model, test_triples, regions):
+    """Upstream test_step for args.countries: every test (h, r, t) is scored against every candidate
+    region (single mode, on the GPU); y_true marks the true region; auc_pr = average precision."""
+    dev = model.entity_embedding.device
+    sample, y_true = [], []
+    for h, r, t in np.asarray(test_triples, dtype=np.int64).reshape(-1, 3).tolist():
+        for region in regions:
+            y_true.append(1 if region == t else 0)
+            sample.append((h, r, region))
+    pos = torch.tensor(sample, dtype=torch.int64, device=dev)
+    with torch.no_grad():
+        y_score = model.score(ops.SINGLE, pos).reshape(-1).cpu().numpy()
+    return {"auc_pr": average_precision(np.array(y_true), y_score)}
+
+
 def test_step(model, test_triples, all_true_triples, args=None, batch_size=None):
     """Upstream `KGEModel.test_step(model, test_triples, all_true_triples, args)`: filtered MRR,
-    MR and HITS@{1,3,10} over head-batch and tail-batch ranking of every test triple."""
+    MR and HITS@{1,3,10} over head-batch and tail-batch ranking of every test triple; with
+    args.countries, the AUC-PR over args.regions instead."""
+    if args is not None and getattr(args, "countries", False):
+        return countries_auc_pr(model, test_triples, args.regions)
     bs = batch_size or int(getattr(args, "test_batch_size", 1024) or 1024)
     dev = model.entity_embedding.device
     triples = np.asarray(test_triples, dtype=np.int64).reshape(-1, 3)

@@ -88,3 +88,24 @@ def test_test_step_replicas_world2_gloo():
     for r in range(2):
         for k, v in single.items():
             assert abs(results[r][k] - v) < 1e-12, (k, results[r][k], v)
+
+
+def test_average_precision_matches_sklearn():
+    """evaluate.average_precision == sklearn.metrics.average_precision_score (upstream's auc_pr),
+    including tied scores."""
+    from sklearn.metrics import average_precision_score
+
+    g = np.random.RandomState(0)
+    for n, ties in ((10, False), (200, False), (200, True), (5, True)):
+        y = g.randint(2, size=n)
+        y[0] = 1
+        s = g.rand(n)
+        if ties:
+            s = np.round(s * 4) / 4
+        assert abs(evaluate.average_precision(y, s) - average_precision_score(y, s)) < 1e-12
+
+
+def test_read_regions(tmp_path):
+    """Upstream run.py reads data/countries_S*/regions.list (one entity name per line) into ids."""
+    (tmp_path / "regions.list").write_text("oceania\nasia\neurope\n")
+    assert evaluate.read_regions(str(tmp_path), {"asia": 7, "europe": 3, "oceania": 9}) == [9, 7, 3]

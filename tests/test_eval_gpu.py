@@ -79,3 +79,30 @@ def test_test_step_metrics():
     want = evaluate.metrics_from_ranks(ranks)
     for k in want:
         assert met[k] == pytest.approx(want[k], rel=1e-12)
+
+
+def test_countries_auc_pr_matches_oracle():
+    """Upstream test_step with args.countries on the reference's countries_S1 test triples and regions:
+    single-mode scores on the GPU, auc_pr vs sklearn on the fp64 oracle's scores."""
+    import os
+    import types
+
+    from sklearn.metrics import average_precision_score
+
+    from oracle import kge_oracle as O
+
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    z = np.load(os.path.join(gold, "countries_S1_regions.npz"))
+    tr = np.load(os.path.join(gold, "countries_S1_train_ids.npz"))
+    E, R = int(tr["nentity"]), int(tr["nrelation"])
+    m = kge.KGEModel("TransE", E, R, 50, 1.0, device="cuda", seed=5)
+    args = types.SimpleNamespace(countries=True, regions=z["regions"].tolist())
+    got = evaluate.test_step(m, z["test"], tr["triples"], args)
+    sample, y = [], []
+    for h, r, t in z["test"].tolist():
+        for reg in args.regions:
+            sample.append((h, r, reg))
+            y.append(1 if reg == t else 0)
+    ent, rel = m.entity_embedding.detach().cpu().double(), m.relation_embedding.detach().cpu().double()
+    s = O.score("TransE", ent, rel, torch.tensor(sample), None, "single", 1.0)[:, 0].numpy()
+    assert abs(got["auc_pr"] - average_precision_score(np.array(y), s)) < 1e-9

@@ -61,14 +61,16 @@ struct MT19937 {
         key[623] = key[396] ^ (y >> 1) ^ (-(y & 1u) & 0x9908b0dfu);
         pos = 0;
     }
-    uint32_t next32() {
-        if (pos >= 624) gen();
-        uint32_t y = key[pos++];
+    static inline uint32_t temper(uint32_t y) {
         y ^= (y >> 11);
         y ^= (y << 7) & 0x9d2c5680u;
         y ^= (y << 15) & 0xefc60000u;
         y ^= (y >> 18);
         return y;
+    }
+    uint32_t next32() {
+        if (pos >= 624) gen();
+        return temper(key[pos++]);
     }
 };
 
@@ -91,18 +93,36 @@ void randint(MT19937& mt, int64_t high, int64_t n, std::vector<int64_t>& out) {
     mask |= mask >> 4;
     mask |= mask >> 8;
     mask |= mask >> 16;
-    for (int64_t i = 0; i < n; ++i) {
-        uint32_t v;
-        while ((v = (mt.next32() & mask)) > (uint32_t)rng) {
+    // branch-free rejection over whole MT blocks: every raw draw is consumed in order, an accepted one
+    // advances k (the same draws, in the same order, as numpy's loop)
+    const uint32_t lim = (uint32_t)rng;
+    int64_t k = 0;
+    while (k < n) {
+        if (mt.pos >= 624) mt.gen();
+        while (mt.pos < 624 && k < n) {
+            const uint32_t v = MT19937::temper(mt.key[mt.pos++]) & mask;
+            out[(size_t)k] = v;
+            k += (v <= lim) ? 1 : 0;
         }
-        out[(size_t)i] = v;
     }
 }
 
 struct TrueSet {
-    std::vector<int64_t> ids;            // distinct
-    std::unordered_set<int64_t> member;  // same ids
+    std::vector<int64_t> ids;     // distinct, in insertion order (build) then sorted (finalize)
     int64_t lo = 0, hi = 0;
+
+    // membership: most true sets hold a handful of ids, so a short linear scan beats hashing;
+    // larger sets binary-search the sorted ids
+    bool contains(int64_t v) const {
+        if (v < lo || v > hi) return false;
+        const size_t n = ids.size();
+        if (n <= 16) {
+            for (size_t i = 0; i < n; ++i)
+                if (ids[i] == v) return true;
+            return false;
+        }
+        return std::binary_search(ids.begin(), ids.end(), v);
+    }
 };
 
 inline uint64_t pair_key(int64_t a, int64_t b) { return ((uint64_t)(uint32_t)a << 32) | (uint32_t)(int32_t)b; }
@@ -122,23 +142,27 @@ struct kge_sampler {
 
 namespace {
 
-// mask of np.in1d(ar1, ts.ids, assume_unique=True, invert=True) as numpy 2.2.6 computes it
-void in1d_invert(const std::vector<int64_t>& ar1, const TrueSet& ts, std::vector<char>& keep,
+// appends ar1[np.in1d(ar1, ts.ids, assume_unique=True, invert=True)] to kept, as numpy 2.2.6 computes it
+void append_kept(const std::vector<int64_t>& ar1, const TrueSet& ts, std::vector<int64_t>& kept,
                  std::unordered_map<int64_t, int64_t>& last) {
     const size_t n1 = ar1.size(), n2 = ts.ids.size();
-    keep.assign(n1, 1);
-    if (n2 == 0) return;
+    if (n2 == 0) {
+        kept.insert(kept.end(), ar1.begin(), ar1.end());
+        return;
+    }
     const int64_t range = ts.hi - ts.lo;
     const bool table = range <= 6 * (int64_t)(n1 + n2);
     const bool loop = (double)n2 < 10.0 * pow((double)n1, 0.145);
     if (table || loop) {  // both are exact membership tests
-        for (size_t i = 0; i < n1; ++i) keep[i] = !ts.member.count(ar1[i]);
+        for (size_t i = 0; i < n1; ++i)
+            if (!ts.contains(ar1[i])) kept.push_back(ar1[i]);
         return;
     }
     // stable mergesort path, assume_unique=True: a value not in ar2 survives only at its last index
     last.clear();
     for (size_t i = 0; i < n1; ++i) last[ar1[i]] = (int64_t)i;
-    for (size_t i = 0; i < n1; ++i) keep[i] = !ts.member.count(ar1[i]) && last[ar1[i]] == (int64_t)i;
+    for (size_t i = 0; i < n1; ++i)
+        if (!ts.contains(ar1[i]) && last[ar1[i]] == (int64_t)i) kept.push_back(ar1[i]);
 }
 
 }  // namespace
@@ -172,12 +196,15 @@ kge_sampler* kge_sampler_create(const int64_t* triples, int64_t ntriples, int64_
         const uint64_t k = mode == KGE_HEAD_BATCH ? pair_key(r, t) : pair_key(h, r);
         const int64_t v = mode == KGE_HEAD_BATCH ? h : t;
         TrueSet& ts = s->truth[k];
-        if (ts.member.insert(v).second) {
-            if (ts.ids.empty()) ts.lo = ts.hi = v;
-            ts.ids.push_back(v);
-            ts.lo = std::min(ts.lo, v);
-            ts.hi = std::max(ts.hi, v);
-        }
+        if (ts.ids.empty()) ts.lo = ts.hi = v;
+        ts.ids.push_back(v);
+        ts.lo = std::min(ts.lo, v);
+        ts.hi = std::max(ts.hi, v);
+    }
+    for (auto& kv : s->truth) {  // distinct, sorted
+        auto& ids = kv.second.ids;
+        std::sort(ids.begin(), ids.end());
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
     }
     s->mt.seed(0);
     return s;
@@ -196,7 +223,6 @@ int kge_sampler_get(kge_sampler* s, const int64_t* idx, int64_t B, int64_t* pos_
     if (!s || (B > 0 && (!idx || !pos_out || !neg_out || !weight_out)) || B < 0)
         return kge_impl::set_error(KGE_EINVAL, "kge_sampler_get: bad arguments");
     const int64_t T = (int64_t)(s->triples.size() / 3), N = s->nneg;
-    std::vector<char> keep;
     static const TrueSet empty_set;
     for (int64_t b = 0; b < B; ++b) {
         const int64_t i = idx[b];
@@ -212,9 +238,7 @@ int kge_sampler_get(kge_sampler* s, const int64_t* idx, int64_t B, int64_t* pos_
         s->kept.clear();
         while ((int64_t)s->kept.size() < N) {
             randint(s->mt, s->nentity, 2 * N, s->draw);
-            in1d_invert(s->draw, ts, keep, s->last);
-            for (size_t j = 0; j < s->draw.size(); ++j)
-                if (keep[j]) s->kept.push_back(s->draw[j]);
+            append_kept(s->draw, ts, s->kept, s->last);
         }
         memcpy(neg_out + b * N, s->kept.data(), (size_t)N * sizeof(int64_t));
     }

@@ -67,15 +67,52 @@ class TrainDataset:
         mode = data[0][3]
         return positive_sample, negative_sample, subsample_weight, mode
 
-    def batches(self, batch_size, shuffle=True, rng=None, drop_last=True):
-        """Endless batches (pos, neg, weight, mode) like a DataLoader over this dataset."""
+    def batches(self, batch_size, shuffle=True, rng=None, drop_last=True, prefetch=0):
+        """Endless batches (pos, neg, weight, mode) like a DataLoader over this dataset. With
+        prefetch > 0 a host thread samples ahead (the C++ sampler releases the GIL), so sampling
+        overlaps the GPU step; the batches and their order are unchanged."""
         rng = rng or np.random.RandomState(0)
-        while True:
-            order = rng.permutation(self.len) if shuffle else np.arange(self.len)
-            stop = self.len - (self.len % batch_size if drop_last else 0)
-            for s in range(0, stop, batch_size):
-                pos, neg, w = self.sample(order[s:s + batch_size])
-                yield torch.from_numpy(pos), torch.from_numpy(neg), torch.from_numpy(w), self.mode
+
+        def produce():
+            while True:
+                order = rng.permutation(self.len) if shuffle else np.arange(self.len)
+                stop = self.len - (self.len % batch_size if drop_last else 0)
+                for s in range(0, stop, batch_size):
+                    pos, neg, w = self.sample(order[s:s + batch_size])
+                    yield torch.from_numpy(pos), torch.from_numpy(neg), torch.from_numpy(w), self.mode
+
+        if prefetch <= 0:
+            yield from produce()
+            return
+        import queue
+        import threading
+
+        q: queue.Queue = queue.Queue(maxsize=prefetch)
+        stop = threading.Event()
+
+        def worker():
+            try:
+                for item in produce():
+                    while not stop.is_set():
+                        try:
+                            q.put(item, timeout=0.1)
+                            break
+                        except queue.Full:
+                            continue
+                    if stop.is_set():
+                        return
+            except BaseException as e:  # noqa: BLE001 (re-raised in the consumer)
+                q.put(e)
+
+        threading.Thread(target=worker, daemon=True).start()
+        try:
+            while True:
+                item = q.get()
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+        finally:
+            stop.set()
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -71,3 +71,14 @@ def test_bad_index_raises():
     ds = TrainDataset(triples, E, R, 4, "tail-batch")
     with pytest.raises(Exception):
         ds.sample([len(triples)])
+
+
+def test_prefetching_batches_are_identical():
+    triples, E, R = _countries()
+    a = TrainDataset(triples, E, R, 8, "head-batch", seed=3).batches(16, rng=np.random.RandomState(1))
+    b = TrainDataset(triples, E, R, 8, "head-batch", seed=3).batches(16, rng=np.random.RandomState(1), prefetch=3)
+    for _ in range(5):
+        x, y = next(a), next(b)
+        for u, v in zip(x[:3], y[:3]):
+            assert np.array_equal(u.numpy(), v.numpy())
+    b.close()

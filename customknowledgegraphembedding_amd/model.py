@@ -183,7 +183,7 @@ class TFKGEModel(_KGEBase):
     call = forward
 
     def step_forward(self, positive_sample, negative_sample, mode):
-        """Both calls of supervisor.py:17-18 fused into two launches:
+        """Both calls of supervisor.py:17-18 fused into one launch (kge_step_forward):
         returns (self(((pos, neg), mode)), self(((pos, neg), 3))), each [B, 1], differentiable."""
         m = ops.mode_id(mode)
         if m == SINGLE:

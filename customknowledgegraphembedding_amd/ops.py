@@ -119,7 +119,7 @@ def score_indexed_bwd_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_r
 
 def step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus=0.0,
                      temperature=1.0, adversarial=True, neg_scores=None, cand_stats=None):
-    """Both model calls of supervisor.py:17-18 in two launches -> (out_neg [B], out_pos [B],
+    """Both model calls of supervisor.py:17-18 in one launch -> (out_neg [B], out_pos [B],
     neg_scores [B, N], pos_scores [B]). `cand_stats` ([B*N, 2] fp32, optional) receives InterHT's
     per-candidate inverse half-norms for the streaming backward."""
     _need_gpu(ent, rel, pos, neg)

@@ -84,7 +84,8 @@ int kge_score_indexed(int fn, int mode,
 
 /*
  * Fused forward of one TF train step (supervisor.py:17-18): the negative call
- * model(((pos, neg), mode)) and the positive call model(((pos, neg), 3)) in two launches.
+ * model(((pos, neg), mode)) and the positive call model(((pos, neg), 3)) in ONE launch: a block per batch
+ * row scores its negatives, then finishes the row (positive, reduction).
  *   mode       KGE_HEAD_BATCH or KGE_TAIL_BATCH (the batch's negative mode)
  *   neg_scores [B,N] raw negative scores (out, row stride ns_ld) — kept for the backward
  *   out_neg    [B]   reduced negative branch: adversarial != 0 -> sum softmax(T s) logsigmoid(-s)

@@ -315,14 +315,15 @@ class KGEModel(_KGEBase):
         negative_sample = negative_sample.to(dev, non_blocking=True)
         subsampling_weight = subsampling_weight.to(dev, non_blocking=True).reshape(-1)
 
-        negative_score = model((positive_sample, negative_sample), mode=mode)
-        if args.negative_adversarial_sampling:
-            # self-adversarial weights are detached upstream
-            negative_score = ops.neg_reduce(negative_score, args.adversarial_temperature,
-                                            adversarial=True, detach=True)
-        else:
-            negative_score = ops.neg_reduce(negative_score, 1.0, adversarial=False)
-        positive_score = ops.log_sigmoid(model(positive_sample)).squeeze(dim=1)
+        # both scoring calls and their reductions in one kge_step_forward launch; the backward is the
+        # deterministic two-phase pass (detach: upstream detaches the self-adversarial weights)
+        adv = bool(args.negative_adversarial_sampling)
+        temp = float(args.adversarial_temperature) if adv else 1.0
+        modulus = model.modulus if model.model_name == "pRotatE" else None
+        negative_score, positive_score = ops.step_forward(
+            FN_IDS[model.model_name], ops.mode_id(mode), model.entity_embedding, model.relation_embedding,
+            positive_sample, negative_sample, model._D, model._gamma_f, model._range_f, rel_off=model._rel_off,
+            modulus=modulus, temperature=temp, adversarial=adv, detach=True)
 
         if args.uni_weight:
             positive_sample_loss = -positive_score.mean()

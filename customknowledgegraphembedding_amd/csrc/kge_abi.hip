@@ -378,6 +378,8 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         waves = p.B;  // one wave per slot
     } else if (kind == KIND_BWD_ENT) {
         waves = p.c_rows;  // one wave per entity row
+    } else if (kind == KIND_BWD_ENT_STREAM) {
+        waves = p.c_rows * kWavesPerBlock;  // one block per entity row
     } else {
         p.cpw = pick_cpw(p.B, p.N);
         p.wpr = (int)((p.N + p.cpw - 1) / p.cpw);
@@ -386,10 +388,12 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > INT32_MAX) return fail(KGE_EINVAL, "problem too large for one launch");
     const bool ch = (kind != KIND_FINISH) && mode == KGE_HEAD_BATCH;
-    if ((kind == KIND_BWD_ROWS || kind == KIND_BWD_ENT || kind == KIND_BWD_STREAM || kind == KIND_BWD_CHAIN) &&
+    if ((kind == KIND_BWD_ROWS || kind == KIND_BWD_ENT || kind == KIND_BWD_STREAM || kind == KIND_BWD_CHAIN ||
+         kind == KIND_BWD_ENT_STREAM) &&
         G > kMaxG)
         return fail(KGE_ENOTSUP, "dimension too large");
-    if (kind == KIND_BWD_STREAM && G % kWavesPerBlock) return fail(KGE_ENOTSUP, "streaming phase 1 needs G % 4 == 0");
+    if ((kind == KIND_BWD_STREAM || kind == KIND_BWD_ENT_STREAM) && G % kWavesPerBlock)
+        return fail(KGE_ENOTSUP, "the streaming backward needs G % 4 == 0");
     rc = dispatch(fn, p, kind, (hipStream_t)stream, (int)blocks, ch, V, G);
     if (rc) return fail(rc, "no kernel for this (function, width) combination");
     return check_launch(kind == KIND_BWD ? "kge score backward launch"
@@ -953,7 +957,9 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
         q.adam.keras = adam->keras;
     }
     if (nentity > 0) {
-        rc = run_score(fn, mode, q, KIND_BWD_ENT, stream);
+        // streaming form (block per row, waves split the columns) under the same condition as phase 1
+        const bool ent_stream = G1 >= kWavesPerBlock && G1 % kWavesPerBlock == 0 && G1 <= kMaxG;
+        rc = run_score(fn, mode, q, ent_stream ? KIND_BWD_ENT_STREAM : KIND_BWD_ENT, stream);
         if (rc) return rc;
     }
     // 5. relation rows (slot order) and the pRotatE modulus

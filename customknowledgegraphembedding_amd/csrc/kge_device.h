@@ -54,23 +54,46 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
 }
 
-template <int V>
+// AUX: cache policy bits of the buffer instruction (gfx950: 2 = nt, 16 = sc1)
+constexpr int kAuxNT = 2, kAuxSC1 = 16;
+
+template <int V, int AUX = 0>
 __device__ __forceinline__ vecf<V> bload(rsrc_t r, uint32_t off) {
     vecf<V> o;
     if constexpr (V == 4) {
-        const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
         o.a[0] = __uint_as_float(u[0]);
         o.a[1] = __uint_as_float(u[1]);
         o.a[2] = __uint_as_float(u[2]);
         o.a[3] = __uint_as_float(u[3]);
     } else if constexpr (V == 2) {
-        const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX);
         o.a[0] = __uint_as_float(u[0]);
         o.a[1] = __uint_as_float(u[1]);
     } else {
-        o.a[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+        o.a[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX));
     }
     return o;
+}
+
+// buffer store (range-checked: bytes at or past the descriptor's size are dropped)
+template <int V, int AUX = 0>
+__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, const vecf<V>& v) {
+    if constexpr (V == 4) {
+        __attribute__((ext_vector_type(4))) unsigned u;
+        u[0] = __float_as_uint(v.a[0]);
+        u[1] = __float_as_uint(v.a[1]);
+        u[2] = __float_as_uint(v.a[2]);
+        u[3] = __float_as_uint(v.a[3]);
+        __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, AUX);
+    } else if constexpr (V == 2) {
+        __attribute__((ext_vector_type(2))) unsigned u;
+        u[0] = __float_as_uint(v.a[0]);
+        u[1] = __float_as_uint(v.a[1]);
+        __builtin_amdgcn_raw_buffer_store_b64(u, r, off, 0, AUX);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.a[0]), r, off, 0, AUX);
+    }
 }
 
 // byte offset of lane `lane`'s group k in a half-row
@@ -1278,6 +1301,298 @@ __global__ __launch_bounds__(kBlock) void bwd_chain_kernel(ScoreParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Phase 2, streaming form (KIND_BWD_ENT_STREAM; same condition as the streaming phase 1). One block
+// per entity row; wave w owns column groups w, w + 4, ... A candidate event's contribution is
+// elementwise against the slot's stored query once the row's InterHT half-norms are known, and the
+// normalisation backward d(x/n) = (dy - y<y,dy>)/n is linear in dy: so the block sums the
+// normalised-space terms of all candidate events (code order, per column), applies the chain once
+// with two block-wide dots, and adds the row events (query-entity gradients, code order). A wave
+// holds one row slice, its Adam moments and U events' query slices in flight (~100 VGPRs instead of
+// the register-resident form's 250), so the Adam stream over the table runs at high occupancy.
+// ---------------------------------------------------------------------------------------------
+template <int FN, bool CH, int V>
+__device__ __forceinline__ void ent_group_term(const vecf<V>& ca, const vecf<V>& cb, const vecf<V>& q0,
+                                               const vecf<V>& q1, const vecf<V>& q2, bool in, float g, float ia,
+                                               float ib, const ScoreParams& p, vecf<V>& sa, vecf<V>& sb) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const float x = ca.a[i];
+        float da = 0.f, db = 0.f;
+        if constexpr (FN == KGE_INTERHT) {  // normalised-space terms (dy of d(x/n))
+            const float ah = x * ia;
+            const float bh = cb.a[i] * ib + 1.f;
+            if (CH) {
+                const float xx = ah * q1.a[i] - q0.a[i] * bh + q2.a[i];
+                const float Gx = in ? -g * sgnf(xx) : 0.f;
+                da = Gx * q1.a[i];
+                db = -Gx * q0.a[i];
+            } else {
+                const float xx = q0.a[i] * bh - ah * q1.a[i] + q2.a[i];
+                const float Gx = in ? -g * sgnf(xx) : 0.f;
+                da = -Gx * q1.a[i];
+                db = Gx * q0.a[i];
+            }
+        } else if constexpr (FN == KGE_TRANSE) {
+            const float r = CH ? (x + q0.a[i]) : (q0.a[i] - x);
+            const float Gx = -g * sgnf(r);
+            da = CH ? Gx : -Gx;
+        } else if constexpr (FN == KGE_DISTMULT) {
+            da = g * q0.a[i];
+        } else if constexpr (FN == KGE_COMPLEX) {
+            da = g * q0.a[i];
+            db = g * q1.a[i];
+        } else if constexpr (FN == KGE_ROTATE) {
+            const float xr = q0.a[i] - x, xi = q1.a[i] - cb.a[i];
+            const float m = sqrtf(xr * xr + xi * xi);
+            da = g * ((m > 0.f) ? xr / m : 0.f);
+            db = g * ((m > 0.f) ? xi / m : 0.f);
+        } else if constexpr (FN == KGE_PROTATE) {
+            const float pc = x / p.phase_div;
+            const float z = CH ? (pc + q0.a[i]) : (q0.a[i] - pc);
+            const float Gx = in ? -g * p.modulus * sgnf(sinf(z)) * cosf(z) : 0.f;
+            da = (CH ? Gx : -Gx) / p.phase_div;
+        }
+        sa.a[i] += in ? da : 0.f;
+        sb.a[i] += in ? db : 0.f;
+    }
+}
+
+// block-wide sum of two per-lane partials, waves combined in wave order (deterministic)
+__device__ __forceinline__ float2 block_sum2(float a, float b, float (*red)[kWavesPerBlock], int lane, int w) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    __syncthreads();  // red may still be read from a previous call
+    if (lane == 0) {
+        red[0][w] = a;
+        red[1][w] = b;
+    }
+    __syncthreads();
+    float sa = red[0][0], sb = red[1][0];
+#pragma unroll
+    for (int ww = 1; ww < kWavesPerBlock; ++ww) {
+        sa += red[0][ww];
+        sb += red[1][ww];
+    }
+    return make_float2(sa, sb);
+}
+
+// query operands a candidate event of function FN reads from the slot's stored query (InterHT's third,
+// the relation row, is read from the relation table instead: it stays in L2)
+constexpr int ent_nq(int fn) { return (fn == KGE_COMPLEX || fn == KGE_ROTATE || fn == KGE_INTERHT) ? 2 : 1; }
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
+    static_assert(G % kWavesPerBlock == 0, "the streaming phase 2 needs a multiple of 4 groups per lane");
+    constexpr int GW = G / kWavesPerBlock;
+    constexpr int U = GW == 1 ? 4 : (GW == 2 ? 2 : 1);  // events whose query slices are in flight
+    constexpr bool SPLIT = is_split(FN);
+    constexpr int NH = SPLIT ? 2 : 1;
+    constexpr int NQ = ent_nq(FN);
+    __shared__ float red[2][kWavesPerBlock];
+    const int64_t e = blockIdx.x;
+    if (e >= p.c_rows) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int D = p.D, DV = D / V;
+    const int64_t BN = p.Bn * p.Nn;
+    const uint32_t nb = (uint32_t)D * 4u;
+    uint32_t goffs[GW];
+    bool gin[GW];
+#pragma unroll
+    for (int gg = 0; gg < GW; ++gg) {
+        const int k = w + kWavesPerBlock * gg;
+        goffs[gg] = goff<V>(lane, k);
+        gin[gg] = (lane + k * kWave) < DV;
+    }
+    // streamed (read-once) operands: the table row and its Adam moments. Default cache policy: nt
+    // loads / sc1 stores measured no faster here (the next step's forward re-reads the table)
+    auto sload = [&](rsrc_t r, uint32_t off) { return bload<V>(r, off); };
+    const int lo = p.ev_off[e], hi = p.ev_off[e + 1];
+    const int n = hi - lo;
+    // the row slice, and the Adam moments requested up front so their latency overlaps the walk
+    vecf<V> ca[GW], cb[GW], mm[NH][GW], vv[NH][GW];
+    {
+        const float* row = p.cent + e * p.c_ld;
+        const uint32_t rb = (n > 0 || p.adam.on) ? nb : 0u;
+        const rsrc_t sa = make_rsrc(row, rb), sb = make_rsrc(row + D, SPLIT ? rb : 0u);
+#pragma unroll
+        for (int gg = 0; gg < GW; ++gg) {
+            ca[gg] = sload(sa, goffs[gg]);
+            cb[gg] = SPLIT ? sload(sb, goffs[gg]) : vzero<V>();
+        }
+    }
+    if (p.adam.on) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const rsrc_t sm = make_rsrc(p.adam.m + e * p.c_ld + h * D, nb);
+            const rsrc_t sv = make_rsrc(p.adam.v + e * p.c_ld + h * D, nb);
+#pragma unroll
+            for (int gg = 0; gg < GW; ++gg) {
+                mm[h][gg] = sload(sm, goffs[gg]);
+                vv[h][gg] = sload(sv, goffs[gg]);
+            }
+        }
+    }
+    vecf<V> sa[GW], sb[GW], ra[GW], rb[GW];  // candidate terms (normalised space), row events
+#pragma unroll
+    for (int gg = 0; gg < GW; ++gg) sa[gg] = sb[gg] = ra[gg] = rb[gg] = vzero<V>();
+    float ia = 0.f, ib = 0.f;
+    bool any_cand = false;
+    if (n > 0) {
+        if constexpr (FN == KGE_INTERHT) {
+            float s2a = 0.f, s2b = 0.f;
+#pragma unroll
+            for (int gg = 0; gg < GW; ++gg)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    s2a += ca[gg].a[i] * ca[gg].a[i];
+                    s2b += cb[gg].a[i] * cb[gg].a[i];
+                }
+            const float2 s = block_sum2(s2a, s2b, red, lane, w);
+            ia = rsqrt_f(s.x);
+            ib = rsqrt_f(s.y);
+        }
+        // one event: its slice of the slot's stored query (candidate event) or of the slot's
+        // query-entity gradient (row event)
+        auto load_ev = [&](int code, vecf<V>(&x0)[GW], vecf<V>(&x1)[GW], vecf<V>(&x2)[GW]) {
+            const float *b0, *b1, *b2 = p.rel;
+            uint32_t n1, n2 = 0u;
+            if (code < BN + p.Bn) {
+                const int64_t slot = code < BN ? code / p.Nn : p.Bn + (code - BN);
+                b0 = p.qbuf + slot * 3 * D;
+                b1 = b0 + D;
+                n1 = NQ > 1 ? nb : 0u;
+                if constexpr (FN == KGE_INTERHT) {  // q2 = the slot's relation row (zero when out of range)
+                    const int64_t bb = slot < p.Bn ? slot : slot - p.Bn;
+                    const int64_t ri = p.r_idx ? p.r_idx[bb * p.r_stride] : bb;
+                    const bool rok = ri >= 0 && ri < p.r_rows;
+                    b2 = p.rel + (rok ? ri : 0) * p.r_ld + p.r_off;
+                    n2 = rok ? nb : 0u;
+                }
+            } else {
+                b0 = p.qg_ent + (code - BN - p.Bn) * p.ent_w;
+                b1 = b0 + D;
+                n1 = SPLIT ? nb : 0u;
+            }
+            const rsrc_t s0 = make_rsrc(b0, nb), s1 = make_rsrc(b1, n1), s2 = make_rsrc(b2, n2);
+#pragma unroll
+            for (int gg = 0; gg < GW; ++gg) {
+                x0[gg] = bload<V>(s0, goffs[gg]);
+                x1[gg] = (NQ > 1 || SPLIT) ? bload<V>(s1, goffs[gg]) : vzero<V>();
+                x2[gg] = FN == KGE_INTERHT ? bload<V>(s2, goffs[gg]) : vzero<V>();
+            }
+        };
+        auto apply_ev = [&](int code, const vecf<V>(&x0)[GW], const vecf<V>(&x1)[GW], const vecf<V>(&x2)[GW]) {
+            if (code < BN + p.Bn) {
+                const bool neg = code < BN;
+                const float g = neg ? p.d_ns[code] : p.d_ps[code - BN];
+                any_cand = true;
+#pragma unroll
+                for (int gg = 0; gg < GW; ++gg) {
+                    if (neg)
+                        ent_group_term<FN, CH, V>(ca[gg], cb[gg], x0[gg], x1[gg], x2[gg], gin[gg], g, ia, ib, p,
+                                                  sa[gg], sb[gg]);
+                    else  // the positive call scores the tail
+                        ent_group_term<FN, false, V>(ca[gg], cb[gg], x0[gg], x1[gg], x2[gg], gin[gg], g, ia, ib, p,
+                                                     sa[gg], sb[gg]);
+                }
+            } else {
+#pragma unroll
+                for (int gg = 0; gg < GW; ++gg)
+#pragma unroll
+                    for (int i = 0; i < V; ++i) {
+                        ra[gg].a[i] += x0[gg].a[i];
+                        if constexpr (SPLIT) rb[gg].a[i] += x1[gg].a[i];
+                    }
+            }
+        };
+        if (n <= kWave) {
+            int code = lane < n ? p.ev_code[lo + lane] : INT32_MAX;
+            code = wave_sort_asc(code, lane);
+            for (int j = 0; j < n; j += U) {
+                vecf<V> x0[U][GW], x1[U][GW], x2[U][GW];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (j + u < n) load_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (j + u < n) apply_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
+            }
+        } else {
+            // large bucket: extract codes in ascending order (O(n^2 / 64), rare for random ids)
+            int last = -1;
+            for (int it = 0; it < n; ++it) {
+                int m = INT32_MAX;
+                for (int i = lo + lane; i < hi; i += kWave) {
+                    const int v = p.ev_code[i];
+                    if (v > last && v < m) m = v;
+                }
+                m = wave_min_i(m);
+                vecf<V> x0[GW], x1[GW], x2[GW];
+                load_ev(m, x0, x1, x2);
+                apply_ev(m, x0, x1, x2);
+                last = m;
+            }
+        }
+        if constexpr (FN == KGE_INTERHT) {
+            // any_cand is block-uniform (every wave walks the same events)
+            if (any_cand) {
+                float da = 0.f, db = 0.f;
+#pragma unroll
+                for (int gg = 0; gg < GW; ++gg)
+#pragma unroll
+                    for (int i = 0; i < V; ++i) {
+                        da += (ca[gg].a[i] * ia) * sa[gg].a[i];
+                        db += (cb[gg].a[i] * ib) * sb[gg].a[i];
+                    }
+                const float2 dot = block_sum2(da, db, red, lane, w);
+#pragma unroll
+                for (int gg = 0; gg < GW; ++gg)
+#pragma unroll
+                    for (int i = 0; i < V; ++i) {
+                        sa[gg].a[i] = (sa[gg].a[i] - (ca[gg].a[i] * ia) * dot.x) * ia;
+                        sb[gg].a[i] = (sb[gg].a[i] - (cb[gg].a[i] * ib) * dot.y) * ib;
+                    }
+            }
+        }
+#pragma unroll
+        for (int gg = 0; gg < GW; ++gg)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                sa[gg].a[i] += ra[gg].a[i];
+                sb[gg].a[i] += rb[gg].a[i];
+            }
+    }
+    auto sstore = [&](rsrc_t r, uint32_t off, const vecf<V>& v) { bstore<V>(r, off, v); };
+    if (p.adam.on) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const rsrc_t sp = make_rsrc(p.cent + e * p.c_ld + h * D, nb);
+            const rsrc_t sm = make_rsrc(p.adam.m + e * p.c_ld + h * D, nb);
+            const rsrc_t sv = make_rsrc(p.adam.v + e * p.c_ld + h * D, nb);
+#pragma unroll
+            for (int gg = 0; gg < GW; ++gg) {
+                vecf<V> pp = h ? cb[gg] : ca[gg];
+                const vecf<V>& gr = h ? sb[gg] : sa[gg];
+#pragma unroll
+                for (int i = 0; i < V; ++i)
+                    adam_update(pp.a[i], gr.a[i], mm[h][gg].a[i], vv[h][gg].a[i], p.adam.b1, p.adam.b2, p.adam.eps,
+                                p.adam.alpha, p.adam.step_size, p.adam.bc2_sqrt, p.adam.keras);
+                sstore(sp, goffs[gg], pp);
+                sstore(sm, goffs[gg], mm[h][gg]);
+                sstore(sv, goffs[gg], vv[h][gg]);
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const rsrc_t so = make_rsrc(p.d_out_ent + e * p.c_ld + h * D, nb);
+#pragma unroll
+        for (int gg = 0; gg < GW; ++gg) sstore(so, goffs[gg], h ? sb[gg] : sa[gg]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // dispatch over (kind, candidate side, vector width, groups per lane) for one score function
 // ---------------------------------------------------------------------------------------------
 template <int FN, bool CH, int V, int G>
@@ -1291,6 +1606,9 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
     else if (kind == KIND_BWD_STREAM) {
         if constexpr (G % kWavesPerBlock == 0)
             hipLaunchKernelGGL((bwd_stream_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    } else if (kind == KIND_BWD_ENT_STREAM) {
+        if constexpr (G % kWavesPerBlock == 0)
+            hipLaunchKernelGGL((bwd_ent_stream_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     } else if (kind == KIND_BWD_CHAIN)
         hipLaunchKernelGGL((bwd_chain_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_FWD_STATS) {

@@ -24,7 +24,8 @@ enum Kind {
     KIND_BWD_CHAIN = 6,   // phase 1 epilogue of the streaming form (one wave per slot)
     KIND_FWD_STATS = 7,   // forward that also keeps InterHT's candidate norms (train step)
     KIND_STEP_FWD = 8,    // fused train-step forward: block per batch row, negatives + finish in one launch
-    KIND_STEP_FWD_STATS = 9
+    KIND_STEP_FWD_STATS = 9,
+    KIND_BWD_ENT_STREAM = 10,  // phase 2, column-group streaming (one block per entity row)
 };
 
 // Parameters of one scoring launch. Rows are addressed as base + row * ld (floats).

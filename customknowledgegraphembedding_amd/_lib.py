@@ -92,6 +92,13 @@ SIGNATURES = {
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_p, _c_f, _c_f, _c_i, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p,
          _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_p, _c_i64, _c_p],
     ),
+    "kge_train_step_workspace_size": (_c_i64, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
+    "kge_train_step": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p,
+         _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p],
+    ),
     "kge_sampler_create": (_c_p, [_c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i]),
     "kge_sampler_seed": (_c_i, [_c_p, ctypes.c_uint32]),
     "kge_sampler_get": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p, _c_p]),

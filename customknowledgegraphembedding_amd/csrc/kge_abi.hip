@@ -26,13 +26,19 @@ __global__ __launch_bounds__(kBlock) void neg_reduce_kernel(const float* __restr
     if (lane == 0) out[b] = res;
 }
 
+// With `ps` set it also writes the positive branch's d_ps[b] = d_out_pos[b] * sigmoid(-ps[b])
+// (logsigmoid backward, model.py:145), saving the separate launch in the train step.
 __global__ __launch_bounds__(kBlock) void neg_reduce_bwd_kernel(const float* __restrict__ s, int64_t B, int64_t N,
                                                                 int64_t ld, float T, int adversarial, int detach,
                                                                 const float* __restrict__ d_out,
-                                                                float* __restrict__ d_s, int64_t d_ld) {
+                                                                float* __restrict__ d_s, int64_t d_ld,
+                                                                const float* __restrict__ ps,
+                                                                const float* __restrict__ d_out_pos,
+                                                                float* __restrict__ d_ps) {
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (b >= B) return;
     const int lane = threadIdx.x & 63;
+    if (ps && lane == 0) d_ps[b] = d_out_pos[b] * sigmoidf(-ps[b]);
     const float* row = s + b * ld;
     float* drow = d_s + b * d_ld;
     const float go = d_out[b];
@@ -372,7 +378,7 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         p.wpr = 1;
         waves = p.B;
     } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM || kind == KIND_STEP_FWD ||
-               kind == KIND_STEP_FWD_STATS) {
+               kind == KIND_STEP_FWD_STATS || kind == KIND_STEP_FWD_GRAD) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
     } else if (kind == KIND_BWD_CHAIN) {
         waves = p.B;  // one wave per slot
@@ -392,6 +398,8 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
          kind == KIND_BWD_ENT_STREAM) &&
         G > kMaxG)
         return fail(KGE_ENOTSUP, "dimension too large");
+    if (kind == KIND_STEP_FWD_GRAD && (G > kFwdGradMaxG || fn == KGE_PROTATE))
+        return fail(KGE_ENOTSUP, "the fused forward + query gradient needs D <= 1024 and no pRotatE");
     if ((kind == KIND_BWD_STREAM || kind == KIND_BWD_ENT_STREAM) && G % kWavesPerBlock)
         return fail(KGE_ENOTSUP, "the streaming backward needs G % 4 == 0");
     rc = dispatch(fn, p, kind, (hipStream_t)stream, (int)blocks, ch, V, G);
@@ -702,7 +710,7 @@ int kge_neg_reduce_bwd(const float* scores, int64_t B, int64_t N, int64_t ld, fl
     if (!scores || !d_out || !d_scores) return fail(KGE_EINVAL, "null pointer");
     const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
     hipLaunchKernelGGL(neg_reduce_bwd_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, scores,
-                       B, N, ld, temperature, adversarial, detach, d_out, d_scores, d_ld);
+                       B, N, ld, temperature, adversarial, detach, d_out, d_scores, d_ld, nullptr, nullptr, nullptr);
     return check_launch("kge_neg_reduce_bwd");
 }
 
@@ -837,6 +845,37 @@ int64_t kge_step_backward_workspace_size(int fn, int64_t nentity, int64_t B, int
     return step_ws_layout(nullptr, nentity, B, N, D, ent_width(fn, D), rel_width(fn, D)).bytes;
 }
 
+// Options of the shared backward body. The defaults are kge_step_backward's behaviour.
+struct StepOpts {
+    bool dq_ready = false;      // phase 1 done by the fused forward: dqbuf holds unscaled query gradients
+    bool events_ready = false;  // the entity buckets were built by the caller (e.g. on a side stream)
+    bool fused_dscores = false; // the positive score gradient comes out of the neg_reduce_bwd launch
+};
+
+static EvArgs ev_args(const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t E,
+                      int mode) {
+    EvArgs a;
+    a.pos = pos;
+    a.neg = neg;
+    a.neg_ld = neg_ld;
+    a.B = B;
+    a.N = N;
+    a.E = E;
+    a.qcol = mode == KGE_HEAD_BATCH ? 2 : 0;
+    a.total = (int)(B * N + 3 * B);
+    return a;
+}
+
+// bucket the gradient events by entity: count, exclusive scan, scatter (counting sort)
+static int launch_events(const EvArgs& a, const StepWs& w, hipStream_t st) {
+    if (hipMemsetAsync(w.count, 0, (size_t)(a.E * 4), st) != hipSuccess) return check_launch("memset");
+    const unsigned eb = (unsigned)((a.total + kBlock - 1) / kBlock);
+    if (a.total > 0) hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
+    launch_exclusive_scan(w.count, a.E, w.off, w.cursor, w.tiles, st);
+    if (a.total > 0) hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
+    return check_launch("kge_step_backward events");
+}
+
 static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
                               int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos,
                               const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma,
@@ -844,7 +883,7 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
                               const float* neg_scores, int64_t ns_ld, const float* pos_scores, const float* d_out_neg,
                               const float* d_out_pos, float* d_ent, float* d_rel, float* d_modulus,
                               const float* cand_stats, void* workspace, int64_t workspace_bytes, void* stream,
-                              const AdamArgs* adam, float* m_ent, float* v_ent) {
+                              const AdamArgs* adam, float* m_ent, float* v_ent, const StepOpts& o = StepOpts()) {
     int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
     if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_backward needs a negative mode (0 or 1)");
@@ -867,9 +906,17 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
         return ok();
     }
     // 1. loss -> score gradients
-    rc = kge_neg_reduce_bwd(neg_scores, B, N, ns_ld, temperature, adversarial, detach, d_out_neg, w.d_ns, N, stream);
-    if (rc) return rc;
-    rc = kge_log_sigmoid_bwd(pos_scores, d_out_pos, B, w.d_ps, stream);
+    if (o.fused_dscores) {
+        const unsigned nb = (unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock);
+        hipLaunchKernelGGL(neg_reduce_bwd_kernel, dim3(nb), dim3(kBlock), 0, st, neg_scores, B, N, ns_ld,
+                           temperature, adversarial, detach, d_out_neg, w.d_ns, N, pos_scores, d_out_pos, w.d_ps);
+        rc = check_launch("kge_step_backward score gradients");
+    } else {
+        rc = kge_neg_reduce_bwd(neg_scores, B, N, ns_ld, temperature, adversarial, detach, d_out_neg, w.d_ns, N,
+                                stream);
+        if (rc) return rc;
+        rc = kge_log_sigmoid_bwd(pos_scores, d_out_pos, B, w.d_ps, stream);
+    }
     if (rc) return rc;
     // 2. phase 1: per-slot query gradients (negative call, then positive call)
     ScoreParams p;
@@ -889,7 +936,12 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
     int V1 = 1, G1 = 1;
     rc = pick_vg(p, V1, G1);
     if (rc) return rc;
-    if (G1 >= kWavesPerBlock && G1 % kWavesPerBlock == 0 && G1 <= kMaxG && (fn != KGE_INTERHT || cand_stats)) {
+    if (o.dq_ready) {
+        // the fused forward (KIND_STEP_FWD_GRAD) left each row's query gradient, unscaled, in dqbuf
+        p.dqbuf = w.dqbuf;
+        p.dq_scale = d_out_neg;
+        rc = run_score(fn, mode, p, KIND_BWD_CHAIN, stream);
+    } else if (G1 >= kWavesPerBlock && G1 % kWavesPerBlock == 0 && G1 <= kMaxG && (fn != KGE_INTERHT || cand_stats)) {
         p.cand_stats = reinterpret_cast<float2*>(const_cast<float*>(cand_stats));
         p.dqbuf = w.dqbuf;
         rc = run_score(fn, mode, p, KIND_BWD_STREAM, stream);
@@ -914,22 +966,10 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
     rc = run_score(fn, KGE_SINGLE, pp, KIND_BWD_ROWS, stream);
     if (rc) return rc;
     // 3. bucket the gradient events by entity
-    EvArgs a;
-    a.pos = pos;
-    a.neg = neg;
-    a.neg_ld = neg_ld;
-    a.B = B;
-    a.N = N;
-    a.E = nentity;
-    a.qcol = mode == KGE_HEAD_BATCH ? 2 : 0;
-    a.total = (int)(B * N + 3 * B);
-    if (hipMemsetAsync(w.count, 0, (size_t)(nentity * 4), st) != hipSuccess) return check_launch("memset");
-    const unsigned eb = (unsigned)((a.total + kBlock - 1) / kBlock);
-    if (a.total > 0) hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
-    launch_exclusive_scan(w.count, nentity, w.off, w.cursor, w.tiles, st);
-    if (a.total > 0) hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
-    rc = check_launch("kge_step_backward events");
-    if (rc) return rc;
+    if (!o.events_ready) {
+        rc = launch_events(ev_args(pos, neg, neg_ld, B, N, nentity, mode), w, st);
+        if (rc) return rc;
+    }
     // 4. phase 2: one wave per entity row, events in code order -> every row of d_ent written
     ScoreParams q;
     fill_indexed(q, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D, gamma,
@@ -985,6 +1025,22 @@ int kge_step_backward(int fn, int mode, const float* ent, int64_t nentity, int64
                               workspace_bytes, stream, nullptr, nullptr, nullptr);
 }
 
+// Adam coefficients of step t (1-based), in double on the host
+static AdamArgs adam_args(float lr, float beta1, float beta2, float eps, int64_t step, int keras) {
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    AdamArgs a;
+    a.b1 = beta1;
+    a.b2 = beta2;
+    a.eps = eps;
+    a.alpha = (float)((double)lr * std::sqrt(bc2) / bc1);
+    a.step_size = (float)((double)lr / bc1);
+    a.bc2_sqrt = (float)std::sqrt(bc2);
+    a.keras = keras;
+    a.zero_grad = 0;
+    return a;
+}
+
 int64_t kge_step_backward_adam_workspace_size(int fn, int64_t nentity, int64_t nrelation, int64_t rel_ld, int64_t B,
                                               int64_t N, int64_t D) {
     const int64_t base = kge_step_backward_workspace_size(fn, nentity, B, N, D);
@@ -1009,17 +1065,7 @@ int kge_step_backward_adam(int fn, int mode, float* ent, int64_t nentity, int64_
         return fail(KGE_EINVAL, "workspace too small");
     float* d_rel = (float*)((char*)workspace + base);
     float* d_mod = (float*)((char*)workspace + base + align256(nrelation * rel_ld * 4));
-    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
-    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
-    AdamArgs a;
-    a.b1 = beta1;
-    a.b2 = beta2;
-    a.eps = eps;
-    a.alpha = (float)((double)lr * std::sqrt(bc2) / bc1);
-    a.step_size = (float)((double)lr / bc1);
-    a.bc2_sqrt = (float)std::sqrt(bc2);
-    a.keras = keras;
-    a.zero_grad = 0;
+    const AdamArgs a = adam_args(lr, beta1, beta2, eps, step, keras);
     int rc = step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B,
                                 N, D, gamma, emb_range, modulus, temperature, adversarial, detach, neg_scores, ns_ld,
                                 pos_scores, d_out_neg, d_out_pos, nullptr, d_rel, modulus_param ? d_mod : nullptr,
@@ -1034,6 +1080,124 @@ int kge_step_backward_adam(int fn, int mode, float* ent, int64_t nentity, int64_
         if (rc) return rc;
     }
     return ok();
+}
+
+// ---------------------------------------------------------------------------------------------
+// One whole train step (supervisor.py:15-26 train_step_fn): both model calls with phase 1 of the
+// backward fused into the forward, the weighted loss and its gradient, the deterministic backward
+// with Adam fused into the entity pass, and Adam on the relation table.
+// ---------------------------------------------------------------------------------------------
+struct TrainWs {
+    float *ns, *ps, *d_out, *stats;
+    int64_t bwd_bytes, bytes;
+};
+
+static TrainWs train_ws_layout(char* base, int fn, int64_t E, int64_t R, int64_t rel_ld, int64_t B, int64_t N,
+                               int64_t D) {
+    TrainWs t;
+    t.bwd_bytes = kge_step_backward_adam_workspace_size(fn, E, R, rel_ld, B, N, D);
+    int64_t o = t.bwd_bytes;
+    auto take = [&](int64_t bytes) {
+        char* p = base ? base + o : nullptr;
+        o += align256(bytes);
+        return (float*)p;
+    };
+    t.ns = take(B * N * 4);
+    t.ps = take(B * 4);
+    t.d_out = take(B * 4);
+    t.stats = take(B * N * 8);
+    t.bytes = o;
+    return t;
+}
+
+int64_t kge_train_step_workspace_size(int fn, int64_t nentity, int64_t nrelation, int64_t rel_ld, int64_t B, int64_t N,
+                                      int64_t D) {
+    if (kge_step_backward_adam_workspace_size(fn, nentity, nrelation, rel_ld, B, N, D) < 0) return -1;
+    return train_ws_layout(nullptr, fn, nentity, nrelation, rel_ld, B, N, D).bytes;
+}
+
+int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld, float* rel, int64_t nrelation,
+                   int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t B,
+                   int64_t N, int64_t D, float gamma, float emb_range, float temperature, int adversarial, int detach,
+                   const float* weight, float* loss, float* out_neg, float* out_pos, float* m_ent, float* v_ent,
+                   float* m_rel, float* v_rel, float lr, float beta1, float beta2, float eps, int64_t step, int keras,
+                   void* workspace, int64_t workspace_bytes, void* stream, void* aux_stream, void* fork_event,
+                   void* join_event) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (fn == KGE_PROTATE) return fail(KGE_ENOTSUP, "kge_train_step: pRotatE uses kge_step_backward_adam");
+    if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_train_step needs a negative mode (0 or 1)");
+    if (B <= 0 || N <= 0 || D <= 0 || nentity < 0 || nrelation < 0) return fail(KGE_EINVAL, "bad shape");
+    if (step < 1) return fail(KGE_EINVAL, "step is 1-based");
+    if (!ent || !rel || !pos || !neg || !weight || !loss || !out_neg || !out_pos || !m_ent || !v_ent || !m_rel ||
+        !v_rel)
+        return fail(KGE_EINVAL, "null pointer");
+    const bool side = aux_stream && fork_event && join_event;
+    if (!side && (aux_stream || fork_event || join_event))
+        return fail(KGE_EINVAL, "aux_stream, fork_event and join_event go together");
+    if (B * N + 3 * B >= (int64_t)INT32_MAX || nentity >= (int64_t)INT32_MAX)
+        return fail(KGE_EINVAL, "too many gradient events for 32-bit codes");
+    const TrainWs t = train_ws_layout((char*)workspace, fn, nentity, nrelation, rel_ld, B, N, D);
+    if (!workspace || workspace_bytes < t.bytes) return fail(KGE_EINVAL, "workspace too small");
+    const int64_t base = kge_step_backward_workspace_size(fn, nentity, B, N, D);
+    const StepWs w = step_ws_layout((char*)workspace, nentity, B, N, D, ent_width(fn, D), rel_width(fn, D));
+    float* d_rel = (float*)((char*)workspace + base);
+    hipStream_t st = (hipStream_t)stream;
+
+    // 0. entity buckets of the gradient events: they depend only on the ids, so with a side stream
+    //    they are built while the forward runs
+    StepOpts o;
+    o.fused_dscores = true;
+    if (side) {
+        hipStream_t aux = (hipStream_t)aux_stream;
+        if (hipEventRecord((hipEvent_t)fork_event, st) != hipSuccess ||
+            hipStreamWaitEvent(aux, (hipEvent_t)fork_event, 0) != hipSuccess)
+            return check_launch("kge_train_step fork");
+        rc = launch_events(ev_args(pos, neg, neg_ld, B, N, nentity, mode), w, aux);
+        if (rc) return rc;
+        if (hipEventRecord((hipEvent_t)join_event, aux) != hipSuccess) return check_launch("kge_train_step join");
+        o.events_ready = true;
+    }
+    // 1. forward of both model calls (supervisor.py:17-18); phase 1 fused in where the accumulators fit
+    ScoreParams p;
+    fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D, gamma,
+                 emb_range, 0.f);
+    p.out = t.ns;
+    p.out_ld = N;
+    p.pos_base = pos;
+    p.temperature = temperature;
+    p.adversarial = adversarial;
+    p.detach = detach;
+    p.out_neg = out_neg;
+    p.out_pos_raw = t.ps;
+    p.out_pos_ls = out_pos;
+    p.dqbuf = w.dqbuf;
+    int V = 1, G = 1;
+    rc = pick_vg(p, V, G);
+    if (rc) return rc;
+    o.dq_ready = G <= kFwdGradMaxG;
+    const float* stats = nullptr;
+    if (o.dq_ready) {
+        rc = run_score(fn, mode, p, KIND_STEP_FWD_GRAD, stream);
+    } else {
+        p.cand_stats = reinterpret_cast<float2*>(t.stats);
+        stats = t.stats;
+        rc = run_score(fn, mode, p, fn == KGE_INTERHT ? KIND_STEP_FWD_STATS : KIND_STEP_FWD, stream);
+    }
+    if (rc) return rc;
+    // 2. supervisor.py:19-23: loss and dL/d(out_neg) = dL/d(out_pos) in one launch
+    hipLaunchKernelGGL(step_loss_kernel, dim3(1), dim3(kLossBlock), 0, st, out_neg, out_pos, weight, B, loss, t.d_out);
+    rc = check_launch("kge_train_step loss");
+    if (rc) return rc;
+    if (side && hipStreamWaitEvent(st, (hipEvent_t)join_event, 0) != hipSuccess)
+        return check_launch("kge_train_step join wait");
+    // 3. backward with Adam fused into the entity pass (supervisor.py:25-26), then the relation table
+    const AdamArgs a = adam_args(lr, beta1, beta2, eps, step, keras);
+    rc = step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D,
+                            gamma, emb_range, 0.f, temperature, adversarial, detach, t.ns, N, t.ps, t.d_out, t.d_out,
+                            nullptr, d_rel, nullptr, stats, workspace, base, stream, &a, m_ent, v_ent, o);
+    if (rc) return rc;
+    return kge_adam_update(rel, d_rel, m_rel, v_rel, nrelation * rel_ld, lr, beta1, beta2, eps, step, keras, 0, stream);
 }
 
 }  // extern "C"

@@ -41,6 +41,11 @@ __device__ __forceinline__ vecf<V> vload(const float* p, bool ok) {
     return vzero<V>();
 }
 
+template <int V>
+__device__ __forceinline__ void vstore(float* dst, const vecf<V>& v, bool ok) {
+    if (ok) *reinterpret_cast<vecf<V>*>(dst) = v;
+}
+
 // Raw buffer descriptor over `bytes` bytes at `base`, built from wave-uniform values only (the
 // readfirstlanes make that provable to the compiler, so no waterfall loop is emitted). Loads at or
 // past `bytes` return 0 (hardware range check): rows past D, or a whole invalid row (bytes = 0),
@@ -294,9 +299,21 @@ struct Cand {
 };
 
 // Forward score of one candidate held in registers (every lane returns the full score).
-template <int FN, bool CH, int V, int G>
-__device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Query<FN, CH, V, G>& q,
-                                            const ScoreParams& p, float2* stats = nullptr) {
+// Query operands held in LDS (one copy per block, shared by its waves): q.q0[k] reads lane's group k.
+template <int V>
+struct LdsOperand {
+    const vecf<V>* base;  // the operand image
+    int idx;              // lane
+    __device__ __forceinline__ vecf<V> operator[](int k) const { return base[idx + k * kWave]; }
+};
+template <int V>
+struct LdsQuery {
+    LdsOperand<V> q0, q1, q2;
+};
+
+template <int FN, bool CH, int V, int G, class Q>
+__device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Q& q, const ScoreParams& p,
+                                            float2* stats = nullptr) {
     float acc = 0.f;
     if constexpr (FN == KGE_INTERHT) {
         float sa = 0.f, sb = 0.f;
@@ -523,6 +540,259 @@ __global__ __launch_bounds__(kBlock) void step_fwd_kernel(ScoreParams p) {
     }
     __syncthreads();  // the row's scores are in memory, visible to the block
     if (w == 0) finish_row<FN, V, G>(p, p.pos_base, b, lane, p.out + b * p.out_ld, p.N);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Train-step forward with the query side of the backward fused in (kge_train_step; KIND_STEP_FWD_GRAD).
+//
+// The negative branch's loss term of row b is R_b = sum_n p_n f_n (p = softmax(T s), f = logsigmoid(-s),
+// model.py:168-171) or mean_n f_n, so dR_b/ds_n = p_n (-sigmoid(s_n) + T (f_n - R_b)) (TF: softmax not
+// detached, Q3), p_n (-sigmoid(s_n)) (detached) or -sigmoid(s_n)/N (mean). The query-side gradient
+// sum_n dR_b/ds_n J_n (J_n = ds_n/dq, elementwise in the candidate row) therefore needs only two running
+// sums while the row is still in registers: A = sum e_n (-sigmoid(s_n) + T f_n) J_n and B = sum e_n J_n
+// with e_n = exp(T s_n - m) under a running max m (rescaled when m grows, as an online softmax does),
+// and the row's gradient is (A - T R_b B) / Z. This removes phase 1's second gather of every candidate
+// row (1.05 GB at C2). The result is written unscaled: the loss weight dL/dR_b = -w_b / (2 sum w) is a
+// whole-batch quantity, applied by the chain kernel (dq_scale).
+//   RED: 0 mean, 1 self-adversarial with the softmax detached, 2 self-adversarial (TF semantics).
+// Scores, the row finish and the per-candidate code are the step forward's (bitwise the same scores).
+// ---------------------------------------------------------------------------------------------
+template <int FN, bool CH, int V, bool TWO>
+__device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, const vecf<V>& q0, const vecf<V>& q1,
+                                          const vecf<V>& q2, bool in, float ia, float ib, const ScoreParams& p,
+                                          float wa, float wb, vecf<V>& a0, vecf<V>& a1, vecf<V>& a2, vecf<V>& b0,
+                                          vecf<V>& b1, vecf<V>& b2) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const float x = ca.a[i];
+        float j0 = 0.f, j1 = 0.f, j2 = 0.f;  // d score / d (q0, q1, q2) of this element
+        if constexpr (FN == KGE_INTERHT) {
+            const float ah = x * ia;
+            const float bh = cb.a[i] * ib + 1.f;
+            if (CH) {
+                const float xx = ah * q1.a[i] - q0.a[i] * bh + q2.a[i];
+                const float Gx = in ? -sgnf(xx) : 0.f;
+                j1 = Gx * ah;
+                j0 = -Gx * bh;
+                j2 = Gx;
+            } else {
+                const float xx = q0.a[i] * bh - ah * q1.a[i] + q2.a[i];
+                const float Gx = in ? -sgnf(xx) : 0.f;
+                j0 = Gx * bh;
+                j1 = -Gx * ah;
+                j2 = Gx;
+            }
+        } else if constexpr (FN == KGE_TRANSE) {
+            const float r = CH ? (x + q0.a[i]) : (q0.a[i] - x);
+            j0 = -sgnf(r);
+        } else if constexpr (FN == KGE_DISTMULT) {
+            j0 = x;
+        } else if constexpr (FN == KGE_COMPLEX) {
+            j0 = x;
+            j1 = cb.a[i];
+        } else if constexpr (FN == KGE_ROTATE) {
+            const float xr = q0.a[i] - x, xi = q1.a[i] - cb.a[i];
+            const float m = sqrtf(xr * xr + xi * xi);
+            j0 = -((m > 0.f) ? xr / m : 0.f);
+            j1 = -((m > 0.f) ? xi / m : 0.f);
+        }
+        a0.a[i] += wa * j0;
+        a1.a[i] += wa * j1;
+        a2.a[i] += wa * j2;
+        if constexpr (TWO) {
+            b0.a[i] += wb * j0;
+            b1.a[i] += wb * j1;
+            b2.a[i] += wb * j2;
+        }
+    }
+}
+
+template <int FN, bool CH, int V, int G, int RED>
+__global__ __launch_bounds__(kBlock) void step_fwd_grad_kernel(ScoreParams p) {
+    static_assert(FN != KGE_PROTATE, "pRotatE's modulus gradient is not part of the fused query pass");
+    constexpr bool TWO = RED == 2;
+    constexpr int W = G * kWave;  // vecf<V> per operand per wave image
+    __shared__ vecf<V> part[kWavesPerBlock - 1][3][W];
+    __shared__ vecf<V> qimg[3][W];  // the row's query operands, shared by the four waves
+    __shared__ float st[kWavesPerBlock][3];
+    const int64_t b = blockIdx.x;
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int DV = p.D / V;
+    const float T = p.temperature;
+    if (w == 0) {
+        Query<FN, CH, V, G> qr;
+        int64_t qi, ri;
+        bool qok, rok;
+        build_query_for<FN, CH, V, G>(p, b, lane, qr, qi, ri, qok, rok);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            qimg[0][lane + k * kWave] = qr.q0[k];
+            qimg[1][lane + k * kWave] = qr.q1[k];
+            qimg[2][lane + k * kWave] = qr.q2[k];
+        }
+    }
+    __syncthreads();
+    vecf<V> a0[G], a1[G], a2[G], b0[G], b1[G], b2[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) a0[k] = a1[k] = a2[k] = b0[k] = b1[k] = b2[k] = vzero<V>();
+    float mrun = -INFINITY, Z = 0.f, Ln = 0.f;
+    {
+
+        // one candidate's contribution (s is wave-uniform)
+        auto accumulate = [&](const Cand<FN, V, G>& c, const LdsQuery<V>& q, float s, float2 nst) {
+            float wa, wb = 0.f;
+            if constexpr (RED == 0) {
+                wa = -sigmoidf(s);
+            } else {
+                const float t = T * s;
+                if (t > mrun) {  // online softmax: rescale the running sums to the new maximum
+                    const float sc = expf(mrun - t);
+                    Z *= sc;
+                    Ln *= sc;
+#pragma unroll
+                    for (int k = 0; k < G; ++k)
+#pragma unroll
+                        for (int i = 0; i < V; ++i) {
+                            a0[k].a[i] *= sc;
+                            a1[k].a[i] *= sc;
+                            a2[k].a[i] *= sc;
+                            if constexpr (TWO) {
+                                b0[k].a[i] *= sc;
+                                b1[k].a[i] *= sc;
+                                b2[k].a[i] *= sc;
+                            }
+                        }
+                    mrun = t;
+                }
+                const float e = expf(t - mrun);
+                const float f = log_sigmoid(-s);
+                Z += e;
+                Ln += e * f;
+                wa = e * -sigmoidf(s);
+                if constexpr (TWO) {
+                    wa += e * (T * f);
+                    wb = e;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+                group_jac<FN, CH, V, TWO>(c.ca[k], c.cb[k], q.q0[k], q.q1[k], q.q2[k], (lane + k * kWave) < DV, nst.x,
+                                          nst.y, p, wa, wb, a0[k], a1[k], a2[k], b0[k], b1[k], b2[k]);
+        };
+        const int64_t per = (p.N + kWavesPerBlock - 1) / kWavesPerBlock;
+        const int64_t lo = w * per, hi = min(p.N, lo + per);
+        for (int64_t c0 = lo; c0 < hi; c0 += kWave) {
+            const int nc = (int)min((int64_t)kWave, hi - c0);
+            int64_t my_id = 0;
+            if (lane < nc) my_id = p.c_idx[b * p.c_stride + c0 + lane];
+            float my_score = 0.f;
+            Cand<FN, V, G> x0, x1;
+            bool ok0, ok1;
+            auto one = [&](const Cand<FN, V, G>& c, int jj) {
+                // the query is re-read from LDS for every candidate: an opaque lane index keeps the
+                // compiler from hoisting the reads into 48 loop-invariant VGPRs
+                int li = lane;
+                asm volatile("" : "+v"(li));
+                const LdsQuery<V> q{{qimg[0], li}, {qimg[1], li}, {qimg[2], li}};
+                float2 nst = make_float2(0.f, 0.f);
+                const float s = cand_score<FN, CH, V, G>(c, q, p, &nst);
+                if (lane == jj) my_score = s;
+                // opaque copies of the half-norms: the gradient recomputes the candidate's terms
+                // instead of keeping the score's per-element values alive across the reductions
+                asm volatile("" : "+v"(nst.x), "+v"(nst.y));
+                accumulate(c, q, s, nst);
+            };
+            // software pipeline (as score_run): row j + 1 is in flight while row j is reduced
+            x0.load(cand_row(p, readlane64(my_id, 0), ok0), ok0, p.D, lane);
+            int j = 0;
+            for (; j + 2 < nc; j += 2) {
+                x1.load(cand_row(p, readlane64(my_id, j + 1), ok1), ok1, p.D, lane);
+                one(x0, j);
+                x0.load(cand_row(p, readlane64(my_id, j + 2), ok0), ok0, p.D, lane);
+                one(x1, j + 1);
+            }
+            if (j + 1 < nc) {
+                x1.load(cand_row(p, readlane64(my_id, j + 1), ok1), ok1, p.D, lane);
+                one(x0, j);
+                one(x1, j + 1);
+            } else {
+                one(x0, j);
+            }
+            if (lane < nc) p.out[b * p.out_ld + c0 + lane] = my_score;
+        }
+    }
+    // combine the four waves' partial sums in wave order
+    if (lane == 0) {
+        st[w][0] = mrun;
+        st[w][1] = Z;
+        st[w][2] = Ln;
+    }
+    __syncthreads();  // also: the row's scores are in memory, visible to the block
+    float scale, TR = 0.f;
+    if constexpr (RED == 0) {
+        scale = 1.f / (float)p.N;
+    } else {
+        float M = st[0][0];
+#pragma unroll
+        for (int ww = 1; ww < kWavesPerBlock; ++ww) M = fmaxf(M, st[ww][0]);
+        float Zt = 0.f, Lt = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kWavesPerBlock; ++ww) {
+            const float f = expf(st[ww][0] - M);  // 0 for a wave without candidates (m = -inf)
+            Zt += st[ww][1] * f;
+            Lt += st[ww][2] * f;
+        }
+        scale = expf(mrun - M) / Zt;
+        if constexpr (TWO) TR = T * (Lt / Zt);
+    }
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            if constexpr (TWO) {
+                a0[k].a[i] = scale * (a0[k].a[i] - TR * b0[k].a[i]);
+                a1[k].a[i] = scale * (a1[k].a[i] - TR * b1[k].a[i]);
+                a2[k].a[i] = scale * (a2[k].a[i] - TR * b2[k].a[i]);
+            } else {
+                a0[k].a[i] *= scale;
+                a1[k].a[i] *= scale;
+                a2[k].a[i] *= scale;
+            }
+        }
+    if (w > 0) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            part[w - 1][0][lane + k * kWave] = a0[k];
+            part[w - 1][1][lane + k * kWave] = a1[k];
+            part[w - 1][2][lane + k * kWave] = a2[k];
+        }
+    }
+    __syncthreads();
+    if (w == 0) {
+        float* dq = p.dqbuf + b * 3 * p.D;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+#pragma unroll
+            for (int ww = 0; ww < kWavesPerBlock - 1; ++ww) {
+                const vecf<V> u0 = part[ww][0][lane + k * kWave], u1 = part[ww][1][lane + k * kWave],
+                              u2 = part[ww][2][lane + k * kWave];
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    a0[k].a[i] += u0.a[i];
+                    a1[k].a[i] += u1.a[i];
+                    a2[k].a[i] += u2.a[i];
+                }
+            }
+            const int gi = lane + k * kWave;
+            const bool in = gi < DV;
+            vstore<V>(dq + gi * V, a0[k], in);
+            vstore<V>(dq + p.D + gi * V, a1[k], in);
+            vstore<V>(dq + 2 * p.D + gi * V, a2[k], in);
+        }
+    } else if (w == 1) {
+        finish_row<FN, V, G>(p, p.pos_base, b, lane, p.out + b * p.out_ld, p.N);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -843,11 +1113,6 @@ __device__ __forceinline__ void load_prebuilt_query(Query<FN, CH, V, G>& q, cons
         q.q2[k] = bload<V>(s2, goff<V>(lane, k));
     }
     q.na_inv = q.nb_inv = 0.f;
-}
-
-template <int V>
-__device__ __forceinline__ void vstore(float* dst, const vecf<V>& v, bool ok) {
-    if (ok) *reinterpret_cast<vecf<V>*>(dst) = v;
 }
 
 // Phase-1 epilogue of one slot: the query chain (gradients of the raw query-entity and relation rows)
@@ -1297,6 +1562,17 @@ __global__ __launch_bounds__(kBlock) void bwd_chain_kernel(ScoreParams p) {
         dq1[k] = bload<V>(s1, goff<V>(lane, k));
         dq2[k] = bload<V>(s2, goff<V>(lane, k));
     }
+    if (p.dq_scale) {  // the fused forward's unscaled query gradient: times dL/d(reduced row b)
+        const float sc = p.dq_scale[b];
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                dq0[k].a[i] *= sc;
+                dq1[k].a[i] *= sc;
+                dq2[k].a[i] *= sc;
+            }
+    }
     rows_finalize<FN, CH, V, G>(p, b, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
 }
 
@@ -1617,6 +1893,16 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
     }
     else if (kind == KIND_STEP_FWD)
         hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, false>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_STEP_FWD_GRAD) {
+        if constexpr (FN != KGE_PROTATE && G <= kFwdGradMaxG) {
+            if (!p.adversarial)
+                hipLaunchKernelGGL((step_fwd_grad_kernel<FN, CH, V, G, 0>), dim3(blocks), dim3(kBlock), 0, st, p);
+            else if (p.detach)
+                hipLaunchKernelGGL((step_fwd_grad_kernel<FN, CH, V, G, 1>), dim3(blocks), dim3(kBlock), 0, st, p);
+            else
+                hipLaunchKernelGGL((step_fwd_grad_kernel<FN, CH, V, G, 2>), dim3(blocks), dim3(kBlock), 0, st, p);
+        }
+    }
     else if (kind == KIND_STEP_FWD_STATS) {
         if constexpr (FN == KGE_INTERHT)
             hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, true>), dim3(blocks), dim3(kBlock), 0, st, p);

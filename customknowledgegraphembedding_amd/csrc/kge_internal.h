@@ -26,7 +26,9 @@ enum Kind {
     KIND_STEP_FWD = 8,    // fused train-step forward: block per batch row, negatives + finish in one launch
     KIND_STEP_FWD_STATS = 9,
     KIND_BWD_ENT_STREAM = 10,  // phase 2, column-group streaming (one block per entity row)
+    KIND_STEP_FWD_GRAD = 11,   // train-step forward with phase 1 fused (kge_train_step)
 };
+constexpr int kFwdGradMaxG = 4;  // the fused forward + query gradient keeps 6 accumulators per element
 
 // Parameters of one scoring launch. Rows are addressed as base + row * ld (floats).
 //   query entity row of batch row b:  q_idx ? q_idx[b * q_stride] : b
@@ -65,6 +67,8 @@ struct ScoreParams {
     int64_t ns_ld, n_neg;
     float temperature;
     int adversarial;
+    int detach;                // self-adversarial weights detached (upstream) or not (TF, Q3)
+    const float* dq_scale;     // [B] chain kernel: scale of the fused forward's query gradient
     float* out_neg;      // [B] reduced negative branch
     float* out_pos_raw;  // [B] raw positive score (may be null)
     float* out_pos_ls;   // [B] logsigmoid(positive score)

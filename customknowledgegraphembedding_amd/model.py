@@ -198,12 +198,24 @@ class TFKGEModel(_KGEBase):
         return neg.unsqueeze(1), pos.unsqueeze(1)
 
 
-    def train_step_fused(self, positive_sample, negative_sample, subsampling_weight, mode, optimizer):
-        """supervisor.py:15-26 entirely in HIP: fused forward (kge_step_forward), the loss of
-        supervisor.py:19-23, and kge_step_backward_adam — the deterministic backward with the
-        optimizer applied to each entity row inside the entity-major pass (no dense gradient is
-        materialised). Needs `optimizer` = customknowledgegraphembedding_amd.optim.Adam over this
-        model's parameters. Returns the loss (0-dim tensor)."""
+    def _side_stream(self, device):
+        """A side stream and two events (fork/join) for kge_train_step's event bucketing."""
+        side = getattr(self, "_side", None)
+        if side is None or side[0] != device:
+            side = (device, torch.cuda.Stream(device), _hip_event(), _hip_event())
+            self._side = side
+        return side[1:]
+
+    def train_step_fused(self, positive_sample, negative_sample, subsampling_weight, mode, optimizer,
+                         one_call=True):
+        """supervisor.py:15-26 entirely in HIP. Needs `optimizer` =
+        customknowledgegraphembedding_amd.optim.Adam over this model's parameters; returns the loss
+        (0-dim tensor).
+          one_call (default): kge_train_step — forward with phase 1 of the backward fused in (each
+            candidate row gathered once per step), loss, deterministic backward with Adam fused into
+            the entity pass; the entity bucketing runs on a side stream beside the forward.
+          one_call=False (and pRotatE): kge_step_forward, kge_step_loss, kge_step_backward_adam —
+            bitwise equal to the autograd path (kge_step_backward + kge_adam_update)."""
         from .optim import Adam
         from . import _lib
 
@@ -215,6 +227,8 @@ class TFKGEModel(_KGEBase):
         fn = FN_IDS[self.model_name]
         ent, rel = self.entity_embedding, self.relation_embedding
         is_p = self.model_name == "pRotatE"
+        if one_call and not is_p:
+            return self._train_step_one_call(fn, m, positive_sample, negative_sample, subsampling_weight, optimizer)
         modulus = float(self.modulus.reshape(-1)[0]) if is_p else 0.0
         stats = (torch.empty((negative_sample.shape[0] * negative_sample.shape[1], 2), dtype=torch.float32,
                              device=ent.device) if self.model_name == "InterHT" else None)
@@ -223,21 +237,8 @@ class TFKGEModel(_KGEBase):
                                                         self._range_f, modulus, cand_stats=stats)
         # supervisor.py:19-23 and its gradient in one launch (the same kernel as the autograd path)
         loss, d_out = ops.step_loss_raw(out_neg, out_pos, subsampling_weight)
-        from .optim import resolve_lr
-
-        group = optimizer.param_groups[0]
-        st0 = optimizer.state[self.entity_embedding]
-        lr = resolve_lr(group["lr"], st0["step"] if st0 else 0)
+        group, lr, step = self._adam_state(optimizer, [ent, rel] + ([self.modulus] if is_p else []))
         b1, b2 = group["betas"]
-        params = [ent, rel] + ([self.modulus] if is_p else [])
-        for prm in params:
-            st = optimizer.state[prm]
-            if not st:
-                st["step"] = 0
-                st["exp_avg"] = torch.zeros_like(prm)
-                st["exp_avg_sq"] = torch.zeros_like(prm)
-            st["step"] += 1
-        step = optimizer.state[ent]["step"]
         B, N = ns.shape
         lib = _lib.load()
         nbytes = lib.kge_step_backward_adam_workspace_size(fn, ent.shape[0], rel.shape[0], rel.stride(0), B, N,
@@ -257,6 +258,52 @@ class TFKGEModel(_KGEBase):
             torch.cuda.current_stream(ent.device).cuda_stream)
         _lib.check(rc, "kge_step_backward_adam")
         return loss.detach()
+
+    def _adam_state(self, optimizer, params):
+        from .optim import resolve_lr
+
+        group = optimizer.param_groups[0]
+        st0 = optimizer.state[self.entity_embedding]
+        lr = resolve_lr(group["lr"], st0["step"] if st0 else 0)
+        for prm in params:
+            st = optimizer.state[prm]
+            if not st:
+                st["step"] = 0
+                st["exp_avg"] = torch.zeros_like(prm)
+                st["exp_avg_sq"] = torch.zeros_like(prm)
+            st["step"] += 1
+        return group, lr, optimizer.state[self.entity_embedding]["step"]
+
+    def _train_step_one_call(self, fn, m, positive_sample, negative_sample, subsampling_weight, optimizer):
+        """kge_train_step: supervisor.py:15-26 in one C-ABI call."""
+        from . import _lib
+
+        ent, rel = self.entity_embedding, self.relation_embedding
+        ops._need_gpu(ent, positive_sample, negative_sample, subsampling_weight)
+        dev = ent.device
+        pos = positive_sample.contiguous()
+        neg = negative_sample
+        if neg.stride(1) != 1:
+            neg = neg.contiguous()
+        w = subsampling_weight.reshape(-1).to(torch.float32).contiguous()
+        B, N = neg.shape
+        group, lr, step = self._adam_state(optimizer, [ent, rel])
+        b1, b2 = group["betas"]
+        lib = _lib.load()
+        nbytes = lib.kge_train_step_workspace_size(fn, ent.shape[0], rel.shape[0], rel.stride(0), B, N, self._D)
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        out = torch.empty(2 * B + 1, dtype=torch.float32, device=dev)  # loss | out_neg | out_pos
+        aux, fork, join = self._side_stream(dev)
+        rc = lib.kge_train_step(
+            fn, m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0),
+            self._rel_off, pos.data_ptr(), neg.data_ptr(), neg.stride(0), B, N, self._D, self._gamma_f,
+            self._range_f, 1.0, 1, 0, w.data_ptr(), out.data_ptr(), out[1:].data_ptr(), out[1 + B:].data_ptr(),
+            optimizer.state[ent]["exp_avg"].data_ptr(), optimizer.state[ent]["exp_avg_sq"].data_ptr(),
+            optimizer.state[rel]["exp_avg"].data_ptr(), optimizer.state[rel]["exp_avg_sq"].data_ptr(),
+            float(lr), float(b1), float(b2), float(group["eps"]), int(step), int(group["semantics"] == "keras"),
+            ws.data_ptr(), ws.numel(), torch.cuda.current_stream(dev).cuda_stream, aux.cuda_stream, fork, join)
+        _lib.check(rc, "kge_train_step")
+        return out[0]
 
 
 class KGEModel(_KGEBase):
@@ -348,6 +395,18 @@ class KGEModel(_KGEBase):
             "loss": loss.item(),
         }
         return log
+
+
+def _hip_event():
+    """A timing-free hipEvent_t (caller-owned handle for kge_train_step's fork/join)."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    ev = ctypes.c_void_p()
+    rc = hip.hipEventCreateWithFlags(ctypes.byref(ev), ctypes.c_uint(0x2))  # hipEventDisableTiming
+    if rc != 0:
+        raise RuntimeError(f"hipEventCreateWithFlags failed ({rc})")
+    return ev.value
 
 
 def default_hidden_range(gamma, hidden_dim, epsilon=2.0):

@@ -85,6 +85,9 @@ class Trainer:
                      and len(optimizer.param_groups) == 1
                      and {id(p) for p in optimizer.param_groups[0]["params"] if p.requires_grad}
                      == {id(p) for p in model.parameters() if p.requires_grad})
+        # fused="split": the three-call form (kge_step_forward, kge_step_loss, kge_step_backward_adam),
+        # bitwise equal to the autograd path; otherwise the single kge_train_step call
+        self.one_call = fused != "split"
         self.fused = bool(fused)
 
     def loss(self, positive_sample, negative_sample, subsampling_weight, mode):
@@ -106,7 +109,7 @@ class Trainer:
             if self.fused:
                 # forward + loss + deterministic backward with Adam fused into the entity pass
                 loss = self.model.train_step_fused(positive_sample, negative_sample, subsampling_weight, mode[0],
-                                                   self.optimizer)
+                                                   self.optimizer, one_call=self.one_call)
                 self.metrics.update_state(loss * self.strategy.num_replicas_in_sync)
                 return loss
             self.optimizer.zero_grad(set_to_none=True)

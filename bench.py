@@ -349,7 +349,7 @@ def train_step_bench(m, batches, steps, warmup):
     return {"ms_per_step": dt * 1e3, "triples_per_s": (B * N + B) / dt, "steps": steps, "fused": tr.fused,
             "what": "supervisor.py:13-30 in one C-ABI call (kge_train_step): forward with the backward's query "
                     "pass fused in (one gather of every candidate row), loss, deterministic entity-major backward "
-                    "with Keras Adam fused in; event bucketing on a side stream" if tr.fused else
+                    "with Keras Adam fused in (4 launches per step)" if tr.fused else
                     "fwd + loss + deterministic bwd (kge_step_backward) + Keras Adam (kge_adam_update)"}
 
 

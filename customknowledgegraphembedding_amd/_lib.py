@@ -96,8 +96,8 @@ SIGNATURES = {
     "kge_train_step": (
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
-         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p,
-         _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p],
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_i64, _c_p],
     ),
     "kge_sampler_create": (_c_p, [_c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i]),
     "kge_sampler_seed": (_c_i, [_c_p, ctypes.c_uint32]),

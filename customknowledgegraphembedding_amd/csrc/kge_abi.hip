@@ -39,35 +39,7 @@ __global__ __launch_bounds__(kBlock) void neg_reduce_bwd_kernel(const float* __r
     if (b >= B) return;
     const int lane = threadIdx.x & 63;
     if (ps && lane == 0) d_ps[b] = d_out_pos[b] * sigmoidf(-ps[b]);
-    const float* row = s + b * ld;
-    float* drow = d_s + b * d_ld;
-    const float go = d_out[b];
-    if (adversarial) {
-        float m = -INFINITY;
-        for (int64_t n = lane; n < N; n += kWave) m = fmaxf(m, T * row[n]);
-        m = wave_max(m);
-        float z = 0.f, w = 0.f;
-        for (int64_t n = lane; n < N; n += kWave) {
-            const float x = row[n];
-            const float e = expf(T * x - m);
-            z += e;
-            w += e * log_sigmoid(-x);
-        }
-        z = wave_sum(z);
-        w = wave_sum(w);
-        const float outv = w / z;
-        // d/ds_n [sum_m p_m L_m] = p_n * dL_n/ds_n + T p_n (L_n - out)   (second term: no detach)
-        for (int64_t n = lane; n < N; n += kWave) {
-            const float x = row[n];
-            const float pn = expf(T * x - m) / z;
-            float gsn = pn * (-sigmoidf(x));
-            if (!detach) gsn += T * pn * (log_sigmoid(-x) - outv);
-            drow[n] = go * gsn;
-        }
-    } else {
-        const float inv = 1.f / (float)N;
-        for (int64_t n = lane; n < N; n += kWave) drow[n] = go * (-sigmoidf(row[n])) * inv;
-    }
+    neg_row_bwd(s + b * ld, N, T, adversarial, detach, d_out[b], d_s + b * d_ld, lane);
 }
 
 __global__ __launch_bounds__(kBlock) void log_sigmoid_kernel(const float* __restrict__ x, int64_t n,
@@ -111,6 +83,8 @@ __global__ __launch_bounds__(kLossBlock) void step_loss_kernel(const float* __re
         for (int64_t b = t; b < B; b += kLossBlock) d_out[b] = c * w[b];
     }
 }
+
+__global__ void add_scalar_kernel(const float* __restrict__ x, float* __restrict__ acc) { *acc += *x; }
 
 __global__ __launch_bounds__(kBlock) void log_sigmoid_bwd_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ d_out, int64_t n,
@@ -235,32 +209,42 @@ __global__ __launch_bounds__(kBlock) void ev_scatter_kernel(EvArgs a, int* __res
     if (k >= 0 && k < a.E) code[atomicAdd(&cursor[k], 1)] = i;
 }
 
-// Relation gradient: one wave per (relation, 64-column chunk). The wave finds the slots that use
-// the relation 64 at a time (ballot) and adds their rows in slot order, 8 rows' loads in flight.
+// Relation gradient: one block per (relation, 64-column chunk). Its four waves split the slots (a
+// quarter each), find the slots that use the relation 64 at a time (ballot) and add their rows in
+// slot order with 8 rows' loads in flight; the partials are combined in wave order (deterministic).
+// With `ra.on` the block then applies Adam to its 64 columns of the relation table in place (the
+// dense optimizer of supervisor.py:26: columns no score function reads get a zero gradient).
+struct RelAdam {
+    float *p, *m, *v;
+    AdamArgs a;
+    int on;
+};
+
 __global__ __launch_bounds__(kBlock) void bwd_rel_kernel(const int64_t* __restrict__ pos, int64_t B, int64_t R,
                                                          const float* __restrict__ qg_rel, int64_t rel_w,
                                                          int64_t rel_off, float* __restrict__ d_rel, int64_t rel_ld,
                                                          int64_t rel_dim, const float* __restrict__ dmod_part,
-                                                         float* __restrict__ d_mod) {
-    const int64_t wid = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+                                                         float* __restrict__ d_mod, RelAdam ra) {
+    __shared__ float red[kWavesPerBlock][kWave];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (blockIdx.x == 0 && threadIdx.x == 0 && d_mod && dmod_part) {
         float m = 0.f;
         for (int64_t s = 0; s < 2 * B; ++s) m += dmod_part[s];
         *d_mod = m;
     }
     const int64_t chunks = (rel_dim + kWave - 1) / kWave;
-    const int64_t rho = wid / chunks;
+    const int64_t rho = blockIdx.x / chunks;
     if (rho >= R) return;
-    const int64_t c = (wid - rho * chunks) * kWave + lane;  // column of the full relation row
-    float* out = d_rel + rho * rel_ld;
+    const int64_t c = (blockIdx.x - rho * chunks) * kWave + lane;  // column of the full relation row
     const bool used = c >= rel_off && c < rel_off + rel_w;
     const int64_t cu = c - rel_off;
+    const int64_t S = 2 * B, per = (S + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t s_lo = w * per, s_hi = min(S, s_lo + per);
     float acc = 0.f;
     if (__ballot(used)) {
-        for (int64_t s0 = 0; s0 < 2 * B; s0 += kWave) {
+        for (int64_t s0 = s_lo; s0 < s_hi; s0 += kWave) {
             const int64_t s = s0 + lane;
-            unsigned long long m = __ballot(s < 2 * B && pos[(s % B) * 3 + 1] == rho);  // slot s: row s % B
+            unsigned long long m = __ballot(s < s_hi && pos[(s % B) * 3 + 1] == rho);  // slot s: row s % B
             while (m) {
                 float v[8];
                 int nv = 0;
@@ -280,7 +264,21 @@ __global__ __launch_bounds__(kBlock) void bwd_rel_kernel(const int64_t* __restri
             }
         }
     }
-    if (c < rel_dim) out[c] = used ? acc : 0.f;  // parts no score function reads get 0
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w != 0 || c >= rel_dim) return;
+    float g = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    g = used ? g : 0.f;  // parts no score function reads get 0
+    if (ra.on) {
+        const int64_t e = rho * rel_ld + c;
+        float p = ra.p[e], m = ra.m[e], v = ra.v[e];
+        adam_update(p, g, m, v, ra.a.b1, ra.a.b2, ra.a.eps, ra.a.alpha, ra.a.step_size, ra.a.bc2_sqrt, ra.a.keras);
+        ra.p[e] = p;
+        ra.m[e] = m;
+        ra.v[e] = v;
+    } else {
+        d_rel[rho * rel_ld + c] = g;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -382,6 +380,9 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
     } else if (kind == KIND_BWD_CHAIN) {
         waves = p.B;  // one wave per slot
+    } else if (kind == KIND_STEP_EPILOGUE) {
+        // one wave per slot (negative rows, then positives), then one block for the loss
+        waves = (2 * p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock + kWavesPerBlock;
     } else if (kind == KIND_BWD_ENT) {
         waves = p.c_rows;  // one wave per entity row
     } else if (kind == KIND_BWD_ENT_STREAM) {
@@ -398,7 +399,7 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
          kind == KIND_BWD_ENT_STREAM) &&
         G > kMaxG)
         return fail(KGE_ENOTSUP, "dimension too large");
-    if (kind == KIND_STEP_FWD_GRAD && (G > kFwdGradMaxG || fn == KGE_PROTATE))
+    if ((kind == KIND_STEP_FWD_GRAD || kind == KIND_STEP_EPILOGUE) && (G > kFwdGradMaxG || fn == KGE_PROTATE))
         return fail(KGE_ENOTSUP, "the fused forward + query gradient needs D <= 1024 and no pRotatE");
     if ((kind == KIND_BWD_STREAM || kind == KIND_BWD_ENT_STREAM) && G % kWavesPerBlock)
         return fail(KGE_ENOTSUP, "the streaming backward needs G % 4 == 0");
@@ -850,6 +851,8 @@ struct StepOpts {
     bool dq_ready = false;      // phase 1 done by the fused forward: dqbuf holds unscaled query gradients
     bool events_ready = false;  // the entity buckets were built by the caller (e.g. on a side stream)
     bool fused_dscores = false; // the positive score gradient comes out of the neg_reduce_bwd launch
+    bool epilogue_done = false; // score gradients and both slots' chains done (KIND_STEP_EPILOGUE)
+    float *rel_p = nullptr, *rel_m = nullptr, *rel_v = nullptr;  // Adam on the relation table, fused
 };
 
 static EvArgs ev_args(const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t E,
@@ -871,7 +874,7 @@ static int launch_events(const EvArgs& a, const StepWs& w, hipStream_t st) {
     if (hipMemsetAsync(w.count, 0, (size_t)(a.E * 4), st) != hipSuccess) return check_launch("memset");
     const unsigned eb = (unsigned)((a.total + kBlock - 1) / kBlock);
     if (a.total > 0) hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
-    launch_exclusive_scan(w.count, a.E, w.off, w.cursor, w.tiles, st);
+    if (a.E > 0) hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, a.E, w.off, w.cursor, 1);
     if (a.total > 0) hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
     return check_launch("kge_step_backward events");
 }
@@ -906,7 +909,9 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
         return ok();
     }
     // 1. loss -> score gradients
-    if (o.fused_dscores) {
+    if (o.epilogue_done) {
+        rc = 0;
+    } else if (o.fused_dscores) {
         const unsigned nb = (unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock);
         hipLaunchKernelGGL(neg_reduce_bwd_kernel, dim3(nb), dim3(kBlock), 0, st, neg_scores, B, N, ns_ld,
                            temperature, adversarial, detach, d_out_neg, w.d_ns, N, pos_scores, d_out_pos, w.d_ps);
@@ -936,7 +941,9 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
     int V1 = 1, G1 = 1;
     rc = pick_vg(p, V1, G1);
     if (rc) return rc;
-    if (o.dq_ready) {
+    if (o.epilogue_done) {
+        rc = 0;
+    } else if (o.dq_ready) {
         // the fused forward (KIND_STEP_FWD_GRAD) left each row's query gradient, unscaled, in dqbuf
         p.dqbuf = w.dqbuf;
         p.dq_scale = d_out_neg;
@@ -963,8 +970,10 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
     pp.ent_w = ent_w;
     pp.rel_w = rel_w;
     pp.slot0 = B;
-    rc = run_score(fn, KGE_SINGLE, pp, KIND_BWD_ROWS, stream);
-    if (rc) return rc;
+    if (!o.epilogue_done) {
+        rc = run_score(fn, KGE_SINGLE, pp, KIND_BWD_ROWS, stream);
+        if (rc) return rc;
+    }
     // 3. bucket the gradient events by entity
     if (!o.events_ready) {
         rc = launch_events(ev_args(pos, neg, neg_ld, B, N, nentity, mode), w, st);
@@ -1004,10 +1013,18 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
     }
     // 5. relation rows (slot order) and the pRotatE modulus
     if (nrelation > 0 || d_modulus) {
-        const int64_t rwaves = nrelation * ((rel_dim + kWave - 1) / kWave);
-        const int64_t rb = std::max<int64_t>(1, (rwaves + kWavesPerBlock - 1) / kWavesPerBlock);
+        const int64_t rb = std::max<int64_t>(1, nrelation * ((rel_dim + kWave - 1) / kWave));
+        RelAdam ra;
+        memset(&ra, 0, sizeof(ra));
+        if (adam && o.rel_p) {
+            ra.p = o.rel_p;
+            ra.m = o.rel_m;
+            ra.v = o.rel_v;
+            ra.a = *adam;
+            ra.on = 1;
+        }
         hipLaunchKernelGGL(bwd_rel_kernel, dim3((unsigned)rb), dim3(kBlock), 0, st, pos, B, nrelation, w.qg_rel, rel_w,
-                           rel_off, d_rel, rel_ld, rel_dim, w.dmod, d_modulus);
+                           rel_off, d_rel, rel_ld, rel_dim, w.dmod, d_modulus, ra);
     }
     return check_launch("kge_step_backward");
 }
@@ -1066,15 +1083,17 @@ int kge_step_backward_adam(int fn, int mode, float* ent, int64_t nentity, int64_
     float* d_rel = (float*)((char*)workspace + base);
     float* d_mod = (float*)((char*)workspace + base + align256(nrelation * rel_ld * 4));
     const AdamArgs a = adam_args(lr, beta1, beta2, eps, step, keras);
+    StepOpts o;
+    o.rel_p = rel;  // Adam on the relation table inside the relation-gradient kernel
+    o.rel_m = m_rel;
+    o.rel_v = v_rel;
     int rc = step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B,
                                 N, D, gamma, emb_range, modulus, temperature, adversarial, detach, neg_scores, ns_ld,
                                 pos_scores, d_out_neg, d_out_pos, nullptr, d_rel, modulus_param ? d_mod : nullptr,
-                                cand_stats, workspace, base, stream, &a, m_ent, v_ent);
+                                cand_stats, workspace, base, stream, &a, m_ent, v_ent, o);
     if (rc) return rc;
-    // the relation table (and the pRotatE modulus) are small: their gradients go through the dense
-    // optimizer kernel, with the same adam_update as the fused entity rows
-    rc = kge_adam_update(rel, d_rel, m_rel, v_rel, nrelation * rel_ld, lr, beta1, beta2, eps, step, keras, 0, stream);
-    if (rc) return rc;
+    // the pRotatE modulus (one element) goes through the dense optimizer kernel, with the same
+    // adam_update as the fused rows
     if (modulus_param) {
         rc = kge_adam_update(modulus_param, d_mod, m_mod, v_mod, 1, lr, beta1, beta2, eps, step, keras, 0, stream);
         if (rc) return rc;
@@ -1119,10 +1138,9 @@ int64_t kge_train_step_workspace_size(int fn, int64_t nentity, int64_t nrelation
 int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld, float* rel, int64_t nrelation,
                    int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t B,
                    int64_t N, int64_t D, float gamma, float emb_range, float temperature, int adversarial, int detach,
-                   const float* weight, float* loss, float* out_neg, float* out_pos, float* m_ent, float* v_ent,
-                   float* m_rel, float* v_rel, float lr, float beta1, float beta2, float eps, int64_t step, int keras,
-                   void* workspace, int64_t workspace_bytes, void* stream, void* aux_stream, void* fork_event,
-                   void* join_event) {
+                   const float* weight, float* loss, float* loss_sum, float* out_neg, float* out_pos,
+                   float* m_ent, float* v_ent, float* m_rel, float* v_rel, float lr, float beta1, float beta2,
+                   float eps, int64_t step, int keras, void* workspace, int64_t workspace_bytes, void* stream) {
     int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
     if (fn == KGE_PROTATE) return fail(KGE_ENOTSUP, "kge_train_step: pRotatE uses kge_step_backward_adam");
@@ -1132,9 +1150,6 @@ int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld
     if (!ent || !rel || !pos || !neg || !weight || !loss || !out_neg || !out_pos || !m_ent || !v_ent || !m_rel ||
         !v_rel)
         return fail(KGE_EINVAL, "null pointer");
-    const bool side = aux_stream && fork_event && join_event;
-    if (!side && (aux_stream || fork_event || join_event))
-        return fail(KGE_EINVAL, "aux_stream, fork_event and join_event go together");
     if (B * N + 3 * B >= (int64_t)INT32_MAX || nentity >= (int64_t)INT32_MAX)
         return fail(KGE_EINVAL, "too many gradient events for 32-bit codes");
     const TrainWs t = train_ws_layout((char*)workspace, fn, nentity, nrelation, rel_ld, B, N, D);
@@ -1143,22 +1158,15 @@ int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld
     const StepWs w = step_ws_layout((char*)workspace, nentity, B, N, D, ent_width(fn, D), rel_width(fn, D));
     float* d_rel = (float*)((char*)workspace + base);
     hipStream_t st = (hipStream_t)stream;
-
-    // 0. entity buckets of the gradient events: they depend only on the ids, so with a side stream
-    //    they are built while the forward runs
     StepOpts o;
     o.fused_dscores = true;
-    if (side) {
-        hipStream_t aux = (hipStream_t)aux_stream;
-        if (hipEventRecord((hipEvent_t)fork_event, st) != hipSuccess ||
-            hipStreamWaitEvent(aux, (hipEvent_t)fork_event, 0) != hipSuccess)
-            return check_launch("kge_train_step fork");
-        rc = launch_events(ev_args(pos, neg, neg_ld, B, N, nentity, mode), w, aux);
-        if (rc) return rc;
-        if (hipEventRecord((hipEvent_t)join_event, aux) != hipSuccess) return check_launch("kge_train_step join");
-        o.events_ready = true;
-    }
-    // 1. forward of both model calls (supervisor.py:17-18); phase 1 fused in where the accumulators fit
+    o.events_ready = true;
+    o.rel_p = rel;
+    o.rel_m = m_rel;
+    o.rel_v = v_rel;
+
+    // 1. forward of both model calls (supervisor.py:17-18); phase 1 of the backward fused in where its
+    //    accumulators fit, and the gradient events counted into their entity buckets
     ScoreParams p;
     fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D, gamma,
                  emb_range, 0.f);
@@ -1175,29 +1183,55 @@ int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld
     int V = 1, G = 1;
     rc = pick_vg(p, V, G);
     if (rc) return rc;
-    o.dq_ready = G <= kFwdGradMaxG;
-    const float* stats = nullptr;
-    if (o.dq_ready) {
-        rc = run_score(fn, mode, p, KIND_STEP_FWD_GRAD, stream);
-    } else {
-        p.cand_stats = reinterpret_cast<float2*>(t.stats);
-        stats = t.stats;
-        rc = run_score(fn, mode, p, fn == KGE_INTERHT ? KIND_STEP_FWD_STATS : KIND_STEP_FWD, stream);
-    }
-    if (rc) return rc;
-    // 2. supervisor.py:19-23: loss and dL/d(out_neg) = dL/d(out_pos) in one launch
-    hipLaunchKernelGGL(step_loss_kernel, dim3(1), dim3(kLossBlock), 0, st, out_neg, out_pos, weight, B, loss, t.d_out);
-    rc = check_launch("kge_train_step loss");
-    if (rc) return rc;
-    if (side && hipStreamWaitEvent(st, (hipEvent_t)join_event, 0) != hipSuccess)
-        return check_launch("kge_train_step join wait");
-    // 3. backward with Adam fused into the entity pass (supervisor.py:25-26), then the relation table
     const AdamArgs a = adam_args(lr, beta1, beta2, eps, step, keras);
-    rc = step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N, D,
-                            gamma, emb_range, 0.f, temperature, adversarial, detach, t.ns, N, t.ps, t.d_out, t.d_out,
-                            nullptr, d_rel, nullptr, stats, workspace, base, stream, &a, m_ent, v_ent, o);
+    if (G > kFwdGradMaxG) {
+        // fallback (D > 1024): the step forward, the loss kernel, then the backward with its own phase 1
+        o.events_ready = false;
+        p.cand_stats = reinterpret_cast<float2*>(t.stats);
+        rc = run_score(fn, mode, p, fn == KGE_INTERHT ? KIND_STEP_FWD_STATS : KIND_STEP_FWD, stream);
+        if (rc) return rc;
+        hipLaunchKernelGGL(step_loss_kernel, dim3(1), dim3(kLossBlock), 0, st, out_neg, out_pos, weight, B, loss,
+                           t.d_out);
+        if (loss_sum) hipLaunchKernelGGL(add_scalar_kernel, dim3(1), dim3(1), 0, st, loss, loss_sum);
+        rc = check_launch("kge_train_step loss");
+        if (rc) return rc;
+        return step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B,
+                                  N, D, gamma, emb_range, 0.f, temperature, adversarial, detach, t.ns, N, t.ps,
+                                  t.d_out, t.d_out, nullptr, d_rel, nullptr, t.stats, workspace, base, stream, &a,
+                                  m_ent, v_ent, o);
+    }
+    p.ev_count = w.count;  // zero on entry (the workspace contract), re-zeroed by the scan
+    rc = run_score(fn, mode, p, KIND_STEP_FWD_GRAD, stream);
     if (rc) return rc;
-    return kge_adam_update(rel, d_rel, m_rel, v_rel, nrelation * rel_ld, lr, beta1, beta2, eps, step, keras, 0, stream);
+    // 2. bucket offsets (one launch; resets the counts for the next call)
+    hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, nentity, w.off, w.cursor, 1);
+    rc = check_launch("kge_train_step scan");
+    if (rc) return rc;
+    // 3. one launch: event scatter, loss weights, score gradients, both slots' query chains, the loss
+    ScoreParams e = p;
+    e.ev_count = nullptr;
+    e.neg_scores = t.ns;
+    e.ns_ld = N;
+    e.d_ns = w.d_ns;
+    e.d_ps = w.d_ps;
+    e.qbuf = w.qbuf;
+    e.qg_ent = w.qg_ent;
+    e.qg_rel = w.qg_rel;
+    e.ent_w = ent_width(fn, D);
+    e.rel_w = rel_width(fn, D);
+    e.weight = weight;
+    e.pos_raw = t.ps;
+    e.loss = loss;
+    e.loss_sum = loss_sum;
+    e.ev_cursor = w.cursor;
+    e.ev_code_w = w.code;
+    rc = run_score(fn, mode, e, KIND_STEP_EPILOGUE, stream);
+    if (rc) return rc;
+    // 4. phase 2 with Adam fused into the entity pass, relation gradient with Adam (supervisor.py:25-26)
+    o.dq_ready = o.epilogue_done = true;
+    return step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
+                              D, gamma, emb_range, 0.f, temperature, adversarial, detach, t.ns, N, t.ps, t.d_out,
+                              t.d_out, nullptr, d_rel, nullptr, nullptr, workspace, base, stream, &a, m_ent, v_ent, o);
 }
 
 }  // extern "C"

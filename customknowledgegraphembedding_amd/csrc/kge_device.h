@@ -487,6 +487,37 @@ __device__ __forceinline__ float row_reduce(const float* row, int64_t N, float T
     return wave_sum(w) / (float)N;
 }
 
+// Backward of one row's reduction (model.py:168-171): drow[n] = go * d(row_reduce)/d s_n.
+//   d/ds_n [sum_m p_m L_m] = p_n * dL_n/ds_n + T p_n (L_n - out)   (second term: softmax not detached)
+__device__ __forceinline__ void neg_row_bwd(const float* row, int64_t N, float T, int adversarial, int detach,
+                                            float go, float* drow, int lane) {
+    if (adversarial) {
+        float m = -INFINITY;
+        for (int64_t n = lane; n < N; n += kWave) m = fmaxf(m, T * row[n]);
+        m = wave_max(m);
+        float z = 0.f, w = 0.f;
+        for (int64_t n = lane; n < N; n += kWave) {
+            const float x = row[n];
+            const float e = expf(T * x - m);
+            z += e;
+            w += e * log_sigmoid(-x);
+        }
+        z = wave_sum(z);
+        w = wave_sum(w);
+        const float outv = w / z;
+        for (int64_t n = lane; n < N; n += kWave) {
+            const float x = row[n];
+            const float pn = expf(T * x - m) / z;
+            float gsn = pn * (-sigmoidf(x));
+            if (!detach) gsn += T * pn * (log_sigmoid(-x) - outv);
+            drow[n] = go * gsn;
+        }
+    } else {
+        const float inv = 1.f / (float)N;
+        for (int64_t n = lane; n < N; n += kWave) drow[n] = go * (-sigmoidf(row[n])) * inv;
+    }
+}
+
 // One batch row's finish: the positive (h, r, t) scored with the single-mode (tail) formula, and the
 // reduction of the row's N negative scores. `pos` is the [B, 3] positive batch.
 template <int FN, int V, int G>
@@ -620,6 +651,12 @@ __global__ __launch_bounds__(kBlock) void step_fwd_grad_kernel(ScoreParams p) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int DV = p.D / V;
     const float T = p.temperature;
+    if (w == 1 && lane < 3 && p.ev_count) {
+        // the row's other events: positive candidate (tail), the negative call's query entity, the
+        // positive call's head (step_ev_key order)
+        const int64_t k = p.pos_base[b * 3 + (lane == 0 ? 2 : (lane == 1 ? (CH ? 2 : 0) : 0))];
+        if (k >= 0 && k < p.c_rows) atomicAdd(p.ev_count + k, 1);
+    }
     if (w == 0) {
         Query<FN, CH, V, G> qr;
         int64_t qi, ri;
@@ -685,7 +722,11 @@ __global__ __launch_bounds__(kBlock) void step_fwd_grad_kernel(ScoreParams p) {
         for (int64_t c0 = lo; c0 < hi; c0 += kWave) {
             const int nc = (int)min((int64_t)kWave, hi - c0);
             int64_t my_id = 0;
-            if (lane < nc) my_id = p.c_idx[b * p.c_stride + c0 + lane];
+            if (lane < nc) {
+                my_id = p.c_idx[b * p.c_stride + c0 + lane];
+                // the candidate's gradient event, counted into its entity's bucket (phase 2's counting sort)
+                if (p.ev_count && my_id >= 0 && my_id < p.c_rows) atomicAdd(p.ev_count + my_id, 1);
+            }
             float my_score = 0.f;
             Cand<FN, V, G> x0, x1;
             bool ok0, ok1;
@@ -1118,7 +1159,7 @@ __device__ __forceinline__ void load_prebuilt_query(Query<FN, CH, V, G>& q, cons
 // Phase-1 epilogue of one slot: the query chain (gradients of the raw query-entity and relation rows)
 // and the rows phase 2 reads (prebuilt query, query-entity gradient), relation gradient rows.
 template <int FN, bool CH, int V, int G>
-__device__ __forceinline__ void rows_finalize(const ScoreParams& p, int64_t b, const Query<FN, CH, V, G>& q,
+__device__ __forceinline__ void rows_finalize(const ScoreParams& p, int64_t slot, const Query<FN, CH, V, G>& q,
                                               vecf<V> (&dq0)[G], vecf<V> (&dq1)[G], vecf<V> (&dq2)[G], int64_t qi,
                                               int64_t ri, bool qok, bool rok, int lane) {
     const int D = p.D, DV = D / V;
@@ -1126,7 +1167,6 @@ __device__ __forceinline__ void rows_finalize(const ScoreParams& p, int64_t b, c
     const float* rrow = p.rel + (rok ? ri : 0) * p.r_ld + p.r_off;
     vecf<V> gea[G], geb[G], gra[G], grb[G];
     query_chain<FN, CH, V, G>(q, dq0, dq1, dq2, qrow, qok, rrow, rok, lane, D, p, gea, geb, gra, grb);
-    const int64_t slot = p.slot0 + b;
     float* qb = p.qbuf + slot * 3 * D;
     float* ge = p.qg_ent + slot * p.ent_w;
     float* gr = p.qg_rel + slot * p.rel_w;
@@ -1220,7 +1260,7 @@ __global__ __launch_bounds__(kBlock) void bwd_rows_kernel(ScoreParams p) {
             dq1[k].a[i] = s1;
             dq2[k].a[i] = s2;
         }
-    rows_finalize<FN, CH, V, G>(p, b, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
+    rows_finalize<FN, CH, V, G>(p, p.slot0 + b, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
     if (lane == 0 && p.dmod_part) {
         float m = red_mod[0];
         for (int ww = 1; ww < kWavesPerBlock; ++ww) m += red_mod[ww];
@@ -1573,7 +1613,144 @@ __global__ __launch_bounds__(kBlock) void bwd_chain_kernel(ScoreParams p) {
                 dq2[k].a[i] *= sc;
             }
     }
-    rows_finalize<FN, CH, V, G>(p, b, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
+    rows_finalize<FN, CH, V, G>(p, p.slot0 + b, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Train-step epilogue (kge_train_step; KIND_STEP_EPILOGUE): everything between the fused forward and
+// phase 2 in one launch, one wave per slot.
+//   loss weights: dL/d(out_neg_b) = dL/d(out_pos_b) = -w_b / (2 sum w)         (supervisor.py:19-23)
+//   negative slot b: the row's score gradients d_ns[b, :] (reduction backward), then the chain of the
+//     fused forward's query gradient (dqbuf, scaled by the loss weight)
+//   positive slot B + b: d_ps[b] (logsigmoid backward), the single candidate's query gradient and its
+//     chain (the positive call scores the tail, model.py:127-146)
+//   all threads: the counting sort's scatter of the gradient events (the forward counted them)
+//   an extra last block: the loss value and the running Sum metric (supervisor.py:19-23, :28)
+// ---------------------------------------------------------------------------------------------
+// Entity key of gradient event `code` of the train step (the order of kge_abi.hip's ev_key):
+//   [0, BN) candidate n of row b; then per row: positive tail, negative call's query, positive head.
+template <bool CH>
+__device__ __forceinline__ int64_t step_ev_key(const ScoreParams& p, int code) {
+    const int BN = (int)(p.B * p.N);
+    if (code < BN) {
+        const int b = code / (int)p.N;
+        return p.c_idx[(int64_t)b * p.c_stride + (code - b * (int)p.N)];
+    }
+    int b = code - BN;
+    if (b < p.B) return p.pos_base[(int64_t)b * 3 + 2];
+    b -= (int)p.B;
+    if (b < p.B) return p.pos_base[(int64_t)b * 3 + (CH ? 2 : 0)];
+    b -= (int)p.B;
+    return p.pos_base[(int64_t)b * 3];
+}
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kBlock) void step_epilogue_kernel(ScoreParams p) {
+    __shared__ float red[3][kBlock];
+    const int64_t slot = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t B = p.B;
+    const int D = p.D, DV = D / V;
+    {
+        // scatter the gradient events into their entity buckets (offsets from the scan kernel)
+        // four codes per thread per round, their key loads and cursor atomics all in flight together
+        constexpr int U = 4;
+        const int total = (int)(B * p.N + 3 * B), nl = (int)gridDim.x * kBlock;
+        for (int c0 = (int)blockIdx.x * kBlock + (int)threadIdx.x; c0 < total; c0 += U * nl) {
+            int64_t k[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) k[u] = c0 + u * nl < total ? step_ev_key<CH>(p, c0 + u * nl) : -1;
+            int at[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) at[u] = (k[u] >= 0 && k[u] < p.c_rows) ? atomicAdd(p.ev_cursor + k[u], 1) : -1;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (at[u] >= 0) p.ev_code_w[at[u]] = c0 + u * nl;
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        // the last block: the loss of supervisor.py:19-23 (fixed reduction order) and the Sum metric
+        const int t = threadIdx.x;
+        float sw = 0.f, sp = 0.f, sn = 0.f;
+        for (int64_t i = t; i < B; i += kBlock) {
+            const float wi = p.weight[i];
+            sw += wi;
+            sp += wi * p.out_pos_ls[i];
+            sn += wi * p.out_neg[i];
+        }
+        red[0][t] = sw;
+        red[1][t] = sp;
+        red[2][t] = sn;
+        __syncthreads();
+        for (int o = kBlock / 2; o > 0; o >>= 1) {
+            if (t < o) {
+                red[0][t] += red[0][t + o];
+                red[1][t] += red[1][t + o];
+                red[2][t] += red[2][t + o];
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            const float tw = red[0][0];
+            const float loss = (-red[1][0] / tw + -red[2][0] / tw) / 2.f;
+            *p.loss = loss;
+            if (p.loss_sum) *p.loss_sum += loss;
+        }
+        return;
+    }
+    if (slot >= 2 * B) return;
+    {
+        const bool negslot = slot < B;
+        const int64_t b = negslot ? slot : slot - B;
+        // sum w in a fixed order: every wave gets the same value
+        float sw = 0.f;
+        for (int64_t i = lane; i < B; i += kWave) sw += p.weight[i];
+        sw = wave_sum(sw);
+        const float wb = p.weight[b];
+        const float go = (-0.5f / sw) * wb;
+        if (negslot) {
+            neg_row_bwd(p.neg_scores + b * p.ns_ld, p.N, p.temperature, p.adversarial, p.detach, go,
+                        const_cast<float*>(p.d_ns) + b * p.N, lane);
+            Query<FN, CH, V, G> q;
+            int64_t qi, ri;
+            bool qok, rok;
+            build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+            const float* dq = p.dqbuf + b * 3 * D;
+            const uint32_t nb = (uint32_t)D * 4u;
+            const rsrc_t s0 = make_rsrc(dq, nb), s1 = make_rsrc(dq + D, nb), s2 = make_rsrc(dq + 2 * D, nb);
+            vecf<V> dq0[G], dq1[G], dq2[G];
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                dq0[k] = bload<V>(s0, goff<V>(lane, k));
+                dq1[k] = bload<V>(s1, goff<V>(lane, k));
+                dq2[k] = bload<V>(s2, goff<V>(lane, k));
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    dq0[k].a[i] *= go;
+                    dq1[k].a[i] *= go;
+                    dq2[k].a[i] *= go;
+                }
+            }
+            rows_finalize<FN, CH, V, G>(p, slot, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
+        } else {
+            const float g = go * sigmoidf(-p.pos_raw[b]);
+            if (lane == 0) const_cast<float*>(p.d_ps)[b] = g;
+            const int64_t* pr = p.pos_base + b * 3;
+            const int64_t qi = pr[0], ri = pr[1];
+            const bool qok = qi >= 0 && qi < p.q_rows, rok = ri >= 0 && ri < p.r_rows;
+            bool cok;
+            Cand<FN, V, G> c;
+            c.load(cand_row(p, pr[2], cok), cok, D, lane);
+            Query<FN, false, V, G> q;
+            q.build(p.qent + (qok ? qi : 0) * p.q_ld, qok, p.rel + (rok ? ri : 0) * p.r_ld + p.r_off, rok, D, lane, p);
+            vecf<V> dq0[G], dq1[G], dq2[G], dca[G], dcb[G];
+#pragma unroll
+            for (int k = 0; k < G; ++k) dq0[k] = dq1[k] = dq2[k] = vzero<V>();
+            float dmod = 0.f;
+            cand_grad<FN, false, V, G, true, false>(c, q, g, lane, DV, p, dq0, dq1, dq2, dca, dcb, dmod);
+            rows_finalize<FN, false, V, G>(p, slot, q, dq0, dq1, dq2, qi, ri, qok, rok, lane);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1902,6 +2079,10 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
             else
                 hipLaunchKernelGGL((step_fwd_grad_kernel<FN, CH, V, G, 2>), dim3(blocks), dim3(kBlock), 0, st, p);
         }
+    }
+    else if (kind == KIND_STEP_EPILOGUE) {
+        if constexpr (FN != KGE_PROTATE && G <= kFwdGradMaxG)
+            hipLaunchKernelGGL((step_epilogue_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     }
     else if (kind == KIND_STEP_FWD_STATS) {
         if constexpr (FN == KGE_INTERHT)

@@ -27,6 +27,7 @@ enum Kind {
     KIND_STEP_FWD_STATS = 9,
     KIND_BWD_ENT_STREAM = 10,  // phase 2, column-group streaming (one block per entity row)
     KIND_STEP_FWD_GRAD = 11,   // train-step forward with phase 1 fused (kge_train_step)
+    KIND_STEP_EPILOGUE = 12,   // kge_train_step: loss weights, score gradients, chains, loss (one wave per slot)
 };
 constexpr int kFwdGradMaxG = 4;  // the fused forward + query gradient keeps 6 accumulators per element
 
@@ -69,6 +70,14 @@ struct ScoreParams {
     int adversarial;
     int detach;                // self-adversarial weights detached (upstream) or not (TF, Q3)
     const float* dq_scale;     // [B] chain kernel: scale of the fused forward's query gradient
+    // kge_train_step epilogue
+    const float* weight;       // [B] subsampling weights
+    const float* pos_raw;      // [B] raw positive scores
+    float* loss;               // [1]
+    float* loss_sum;           // [1] running Sum metric (may be null)
+    int* ev_count;             // fused forward: per-entity event counts (atomics)
+    int* ev_cursor;            // epilogue: bucket cursors (scatter)
+    int* ev_code_w;            // epilogue: event codes grouped by entity
     float* out_neg;      // [B] reduced negative branch
     float* out_pos_raw;  // [B] raw positive score (may be null)
     float* out_pos_ls;   // [B] logsigmoid(positive score)

@@ -73,5 +73,84 @@ inline void launch_exclusive_scan(const int* count, int64_t E, int* off, int* cu
                        cursor, E, tiles);
 }
 
+// One-launch exclusive scan for the train step's entity buckets: a single block of 1024 threads.
+// The counts are read as int4 through a range-checked buffer descriptor (zero past E), 8 tiles of
+// 4096 ints at a time, every load in flight at once; each tile is scanned across the block (wave
+// shuffles, 16 wave totals in LDS) and the tiles are chained in order. With `zero` the counts are
+// reset to 0 on the way (the train step keeps its count array zero between calls, so no memset is
+// needed). off[E] = total; cursor = off. Needs 16-B aligned count/off/cursor.
+constexpr int kScanK = 8;  // tiles in flight per super-tile
+typedef int scan_i4 __attribute__((ext_vector_type(4)));
+typedef unsigned scan_u4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(kScanTile) void scan_block_kernel(int* __restrict__ count, int64_t E, int* __restrict__ off,
+                                                               int* __restrict__ cursor, int zero) {
+    constexpr int NW = kScanTile / kWave;  // 16 waves
+    __shared__ int wtot[kScanK][NW];
+    __shared__ int carry_s;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t bytes = (uint32_t)(E * 4);
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc(count, (short)0, (int)bytes, 0x00020000);
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(off, (short)0, (int)bytes, 0x00020000);
+    const auto ru = __builtin_amdgcn_make_buffer_rsrc(cursor, (short)0, (int)bytes, 0x00020000);
+    int carry = 0;
+    for (int64_t base = 0; base < E; base += (int64_t)kScanK * kScanTile * 4) {
+        scan_i4 x[kScanK];
+#pragma unroll
+        for (int r = 0; r < kScanK; ++r) {
+            const int64_t e0 = base + ((int64_t)r * kScanTile + t) * 4;
+            x[r] = e0 < E ? __builtin_bit_cast(scan_i4, __builtin_amdgcn_raw_buffer_load_b128(rc, (uint32_t)(e0 * 4), 0, 0))
+                          : scan_i4{0, 0, 0, 0};
+        }
+        int incl[kScanK];
+#pragma unroll
+        for (int r = 0; r < kScanK; ++r) {
+            int v = x[r][0] + x[r][1] + x[r][2] + x[r][3];
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const int y = __shfl_up(v, o, kWave);
+                if (lane >= o) v += y;
+            }
+            incl[r] = v;
+            if (lane == kWave - 1) wtot[r][w] = v;
+        }
+        __syncthreads();
+        // exclusive prefix of this thread's int4 in each tile, tiles chained in order
+        int tile_base = carry;
+#pragma unroll
+        for (int r = 0; r < kScanK; ++r) {
+            int before = 0, all = 0;
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) {
+                const int v = wtot[r][ww];
+                before += ww < w ? v : 0;
+                all += v;
+            }
+            int run = tile_base + before + incl[r] - (x[r][0] + x[r][1] + x[r][2] + x[r][3]);
+            scan_i4 o4;
+            o4[0] = run;
+            run += x[r][0];
+            o4[1] = run;
+            run += x[r][1];
+            o4[2] = run;
+            run += x[r][2];
+            o4[3] = run;
+            const int64_t e0 = base + ((int64_t)r * kScanTile + t) * 4;
+            if (e0 < E) {
+                const scan_u4 u = __builtin_bit_cast(scan_u4, o4);
+                __builtin_amdgcn_raw_buffer_store_b128(u, ro, (uint32_t)(e0 * 4), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u, ru, (uint32_t)(e0 * 4), 0, 0);
+                if (zero) __builtin_amdgcn_raw_buffer_store_b128(scan_u4{0u, 0u, 0u, 0u}, rc, (uint32_t)(e0 * 4), 0, 0);
+            }
+            tile_base += all;
+        }
+        carry = tile_base;
+        __syncthreads();  // wtot is rewritten by the next super-tile
+    }
+    if (t == 0) carry_s = carry;
+    __syncthreads();
+    if (t == 0) off[E] = carry_s;
+}
+
 }  // namespace
 }  // namespace kge_impl

@@ -198,24 +198,26 @@ class TFKGEModel(_KGEBase):
         return neg.unsqueeze(1), pos.unsqueeze(1)
 
 
-    def _side_stream(self, device):
-        """A side stream and two events (fork/join) for kge_train_step's event bucketing."""
-        side = getattr(self, "_side", None)
-        if side is None or side[0] != device:
-            side = (device, torch.cuda.Stream(device), _hip_event(), _hip_event())
-            self._side = side
-        return side[1:]
+    def _train_workspace(self, nbytes, device):
+        """kge_train_step's workspace: zero-filled once, then reused (each call leaves it reusable)."""
+        ws = getattr(self, "_train_ws", None)
+        if ws is None or ws.numel() < nbytes or ws.device != device:
+            ws = torch.zeros(max(nbytes, 1), dtype=torch.uint8, device=device)
+            self._train_ws = ws
+        return ws
 
     def train_step_fused(self, positive_sample, negative_sample, subsampling_weight, mode, optimizer,
-                         one_call=True):
+                         one_call=True, loss_sum=None):
         """supervisor.py:15-26 entirely in HIP. Needs `optimizer` =
         customknowledgegraphembedding_amd.optim.Adam over this model's parameters; returns the loss
         (0-dim tensor).
           one_call (default): kge_train_step — forward with phase 1 of the backward fused in (each
-            candidate row gathered once per step), loss, deterministic backward with Adam fused into
-            the entity pass; the entity bucketing runs on a side stream beside the forward.
+            candidate row gathered once per step), one epilogue launch (loss, score gradients, query
+            chains, event buckets), deterministic backward with Adam fused into the entity pass.
           one_call=False (and pRotatE): kge_step_forward, kge_step_loss, kge_step_backward_adam —
-            bitwise equal to the autograd path (kge_step_backward + kge_adam_update)."""
+            bitwise equal to the autograd path (kge_step_backward + kge_adam_update).
+          loss_sum: optional 0-dim fp32 device tensor the loss is added to (one_call only; a running
+            Sum metric updated inside the step's last kernel)."""
         from .optim import Adam
         from . import _lib
 
@@ -228,7 +230,13 @@ class TFKGEModel(_KGEBase):
         ent, rel = self.entity_embedding, self.relation_embedding
         is_p = self.model_name == "pRotatE"
         if one_call and not is_p:
-            return self._train_step_one_call(fn, m, positive_sample, negative_sample, subsampling_weight, optimizer)
+            return self._train_step_one_call(fn, m, positive_sample, negative_sample, subsampling_weight, optimizer,
+                                             loss_sum)
+        if loss_sum is not None:
+            loss = self.train_step_fused(positive_sample, negative_sample, subsampling_weight, mode, optimizer,
+                                         one_call=False)
+            loss_sum += loss
+            return loss
         modulus = float(self.modulus.reshape(-1)[0]) if is_p else 0.0
         stats = (torch.empty((negative_sample.shape[0] * negative_sample.shape[1], 2), dtype=torch.float32,
                              device=ent.device) if self.model_name == "InterHT" else None)
@@ -274,12 +282,15 @@ class TFKGEModel(_KGEBase):
             st["step"] += 1
         return group, lr, optimizer.state[self.entity_embedding]["step"]
 
-    def _train_step_one_call(self, fn, m, positive_sample, negative_sample, subsampling_weight, optimizer):
+    def _train_step_one_call(self, fn, m, positive_sample, negative_sample, subsampling_weight, optimizer,
+                             loss_sum=None):
         """kge_train_step: supervisor.py:15-26 in one C-ABI call."""
         from . import _lib
 
         ent, rel = self.entity_embedding, self.relation_embedding
         ops._need_gpu(ent, positive_sample, negative_sample, subsampling_weight)
+        if loss_sum is not None and (loss_sum.dtype != torch.float32 or loss_sum.device != ent.device):
+            raise ValueError("loss_sum must be a float32 tensor on the model's device")
         dev = ent.device
         pos = positive_sample.contiguous()
         neg = negative_sample
@@ -291,17 +302,17 @@ class TFKGEModel(_KGEBase):
         b1, b2 = group["betas"]
         lib = _lib.load()
         nbytes = lib.kge_train_step_workspace_size(fn, ent.shape[0], rel.shape[0], rel.stride(0), B, N, self._D)
-        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        ws = self._train_workspace(nbytes, dev)
         out = torch.empty(2 * B + 1, dtype=torch.float32, device=dev)  # loss | out_neg | out_pos
-        aux, fork, join = self._side_stream(dev)
         rc = lib.kge_train_step(
             fn, m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0),
             self._rel_off, pos.data_ptr(), neg.data_ptr(), neg.stride(0), B, N, self._D, self._gamma_f,
-            self._range_f, 1.0, 1, 0, w.data_ptr(), out.data_ptr(), out[1:].data_ptr(), out[1 + B:].data_ptr(),
+            self._range_f, 1.0, 1, 0, w.data_ptr(), out.data_ptr(),
+            None if loss_sum is None else loss_sum.data_ptr(), out[1:].data_ptr(), out[1 + B:].data_ptr(),
             optimizer.state[ent]["exp_avg"].data_ptr(), optimizer.state[ent]["exp_avg_sq"].data_ptr(),
             optimizer.state[rel]["exp_avg"].data_ptr(), optimizer.state[rel]["exp_avg_sq"].data_ptr(),
             float(lr), float(b1), float(b2), float(group["eps"]), int(step), int(group["semantics"] == "keras"),
-            ws.data_ptr(), ws.numel(), torch.cuda.current_stream(dev).cuda_stream, aux.cuda_stream, fork, join)
+            ws.data_ptr(), ws.numel(), torch.cuda.current_stream(dev).cuda_stream)
         _lib.check(rc, "kge_train_step")
         return out[0]
 
@@ -395,18 +406,6 @@ class KGEModel(_KGEBase):
             "loss": loss.item(),
         }
         return log
-
-
-def _hip_event():
-    """A timing-free hipEvent_t (caller-owned handle for kge_train_step's fork/join)."""
-    import ctypes
-
-    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
-    ev = ctypes.c_void_p()
-    rc = hip.hipEventCreateWithFlags(ctypes.byref(ev), ctypes.c_uint(0x2))  # hipEventDisableTiming
-    if rc != 0:
-        raise RuntimeError(f"hipEventCreateWithFlags failed ({rc})")
-    return ev.value
 
 
 def default_hidden_range(gamma, hidden_dim, epsilon=2.0):

@@ -60,6 +60,13 @@ class Sum:
         v = value.detach().to(torch.float32).reshape(())
         self._total = v.clone() if self._total is None else self._total + v
 
+    def accumulator(self, device):
+        """The running total as a 0-dim fp32 device tensor that a kernel adds into in place
+        (kge_train_step's loss_sum)."""
+        if self._total is None:
+            self._total = torch.zeros((), dtype=torch.float32, device=device)
+        return self._total
+
     def result(self):
         return torch.tensor(0.0) if self._total is None else self._total.detach().cpu()
 
@@ -108,9 +115,12 @@ class Trainer:
             mode = mode.cpu() if torch.is_tensor(mode) else mode
             if self.fused:
                 # forward + loss + deterministic backward with Adam fused into the entity pass
+                acc = (self.metrics.accumulator(dev) if self.one_call and hasattr(self.metrics, "accumulator")
+                       else None)  # single replica: the metric update happens inside the step's last kernel
                 loss = self.model.train_step_fused(positive_sample, negative_sample, subsampling_weight, mode[0],
-                                                   self.optimizer, one_call=self.one_call)
-                self.metrics.update_state(loss * self.strategy.num_replicas_in_sync)
+                                                   self.optimizer, one_call=self.one_call, loss_sum=acc)
+                if acc is None:
+                    self.metrics.update_state(loss * self.strategy.num_replicas_in_sync)
                 return loss
             self.optimizer.zero_grad(set_to_none=True)
             loss = self.loss(positive_sample, negative_sample, subsampling_weight, mode)

@@ -268,18 +268,20 @@ int kge_step_backward_adam(int fn, int mode,
  * `mode` + positive single call), the weighted loss (:19-23; weight = subsampling_weight [B]), the
  * gradient (:25) and Adam (:26; keras != 0: Keras rule, else torch.optim.Adam) on both tables, in place.
  * It replaces what the reference spreads over TFKGEModel.call (model.py:114-205), tf.GradientTape and
- * optimizer.apply_gradients.
- *   Phase 1 of the backward (each batch row's query-side gradient) is fused into the forward: the
- *   candidate rows are gathered once per step instead of twice (online-softmax running sums, valid
- *   for the TF and upstream reductions). D <= 1024 at 16-B alignment (4-B: D <= 256); larger D fall
- *   back to the separate phase 1. pRotatE -> KGE_ENOTSUP (use kge_step_backward_adam).
+ * optimizer.apply_gradients. Four launches at D <= 1024:
+ *   forward with phase 1 of the backward fused in (each candidate row gathered once per step; online-
+ *   softmax running sums, valid for the TF and upstream reductions) and the gradient events counted
+ *   per entity; the bucket scan; an epilogue (event scatter, score gradients, query chains, loss);
+ *   phase 2 with Adam fused into the entity pass, then the relation gradient with Adam.
+ *   D > 1024 (or 4-B-only alignment with D > 256) falls back to the separate phase 1.
+ *   pRotatE -> KGE_ENOTSUP (use kge_step_backward_adam).
  *   Outputs: loss [1], out_neg [B] (reduced negative branch), out_pos [B] (logsigmoid of the
- *   positive score), all device memory. Results equal kge_step_backward_adam's to fp32 rounding (the
- *   query gradient is summed in a different order); deterministic run to run.
- *   aux_stream / fork_event / join_event (hipStream_t / hipEvent_t, caller-created, all three or
- *   none): the entity bucketing of the gradient events, which depends only on the ids, runs on
- *   aux_stream while the forward runs on `stream`.
- *   workspace: kge_train_step_workspace_size(...) bytes.
+ *   positive score), all device memory; loss_sum [1] (or NULL): the running Sum metric
+ *   (supervisor.py:28 metrics.update_state), incremented by the loss on the device.
+ *   Results equal kge_step_backward_adam's to fp32 rounding (the query gradient is summed in a
+ *   different order); deterministic run to run.
+ *   workspace: kge_train_step_workspace_size(...) bytes, ZERO-FILLED before its first use; every
+ *   call leaves it reusable (the per-entity counters it keeps are zero again on return).
  */
 int64_t kge_train_step_workspace_size(int fn, int64_t nentity, int64_t nrelation, int64_t rel_ld,
                                       int64_t B, int64_t N, int64_t D);
@@ -289,11 +291,10 @@ int kge_train_step(int fn, int mode,
                    const int64_t* pos, const int64_t* neg, int64_t neg_ld,
                    int64_t B, int64_t N, int64_t D,
                    float gamma, float emb_range, float temperature, int adversarial, int detach,
-                   const float* weight, float* loss, float* out_neg, float* out_pos,
+                   const float* weight, float* loss, float* loss_sum, float* out_neg, float* out_pos,
                    float* m_ent, float* v_ent, float* m_rel, float* v_rel,
                    float lr, float beta1, float beta2, float eps, int64_t step, int keras,
-                   void* workspace, int64_t workspace_bytes, void* stream,
-                   void* aux_stream, void* fork_event, void* join_event);
+                   void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
  * TranSparse scores (tensorflow_codes/model.py:226-235, gathers at :139-142, :161-164, :187-190; tables

@@ -418,7 +418,7 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--train-steps", type=int, default=10, help="train-step side measurement (0 = skip)")
+    ap.add_argument("--train-steps", type=int, default=50, help="train-step side measurement (0 = skip)")
     ap.add_argument("--event-group", type=int, default=5,
                     help="timing events bracket groups of this many consecutive launches")
     ap.add_argument("--sharded-steps", type=int, default=20,
@@ -562,7 +562,7 @@ def main():
                      "row_reuse": (B * N + 2 * B) / max(1, uniq)},
     }
     if a.train_steps > 0:
-        line["train_step"] = train_step_bench(m, batches, a.train_steps, 2)
+        line["train_step"] = train_step_bench(m, batches, a.train_steps, 5)
     if a.sharded_steps > 0 and a.workload == "c2":
         # the north star's YAGO3-10 row-sharded configuration at this world size (weak scaling:
         # bz=512 per rank), measured beside the headline replica metric

@@ -353,6 +353,66 @@ def train_step_bench(m, batches, steps, warmup):
                     "fwd + loss + deterministic bwd (kge_step_backward) + Keras Adam (kge_adam_update)"}
 
 
+def pipeline_bench(w, a, device):
+    """run.py's input pipeline in front of the train step (run.py:40-66,86-90 -> supervisor.Trainer):
+    C2-shaped batches written as the reference's TFRecord files (compress_data/main.py:104-131 layout,
+    17 files), read back by the C++ reader (CRC verified) on a prefetch thread, moved to the GPU and
+    trained on with kge_train_step. Reports the reader alone, the train step on device-resident
+    batches, and the end-to-end rate (the slower of the two bounds it)."""
+    import shutil
+    import tempfile
+
+    from customknowledgegraphembedding_amd import tfrecord
+    from customknowledgegraphembedding_amd.optim import Adam
+    from customknowledgegraphembedding_amd.supervisor import Strategy, Sum, Trainer
+
+    m, dev_batches = make_inputs(w, 0, device)
+    B, N = w["B"], w["N"]
+    host = []
+    for i, (pos, neg) in enumerate(dev_batches):
+        wt = torch.from_numpy(np.random.RandomState(7 + i).uniform(0.1, 1.0, size=(B, 1)).astype(np.float32))
+        host.append((pos.cpu(), neg.cpu(), wt, torch.full((B,), i % 2, dtype=torch.int64)))
+    d = tempfile.mkdtemp(prefix="kge_tfrec_")
+    try:
+        paths = tfrecord.write_file_tfrecords(host * 4, d, B, split_number=17)
+        nbytes = sum(os.path.getsize(p) for p in paths)
+        # the reader alone (one pass over every file, no prefetch thread)
+        t0 = time.perf_counter()
+        nrec = sum(1 for _ in tfrecord.load_batches(paths, B, repeat=False, prefetch=0))
+        read_s = (time.perf_counter() - t0) / nrec
+        # train step on device-resident batches vs fed from the files
+        data = [(p.to(device), n.to(device), wt.to(device), md) for p, n, wt, md in host]
+
+        def cycle():
+            while True:
+                yield from data
+
+        def run(it, steps):
+            tr = Trainer(Strategy(), None, m, Adam(m.parameters(), lr=5e-5), Sum())
+            for _ in range(5):
+                tr.train_step(it)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(steps):
+                tr.train_step(it)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t) / steps
+
+        resident_s = run(cycle(), a.steps)
+        fed_s = run(iter(tfrecord.load_batches(paths, B, repeat=True, prefetch=4)), a.steps)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"metric": "scored (pos+neg) triples/sec through the train step fed from TFRecord files, "
+                      + w["name"], "value": (B * N + B) / fed_s, "unit": "triples/s", "n_gpus": 1,
+            "steps": a.steps, "warmup": 5, "ms_per_step": fed_s * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic C2 batches written as reference-layout TFRecord files (17 files), read back",
+            "config": {"workload": "run.py pipeline: " + w["name"], "global_batch": B, "n_neg": N,
+                       "parallelism": "single"},
+            "reader_ms_per_batch": read_s * 1e3, "reader_mb_per_s": nbytes / (read_s * nrec) / 1e6,
+            "train_step_resident_ms": resident_s * 1e3, "tfrecord_bytes_per_batch": nbytes / nrec}
+
+
 def cpu_baseline(w, budget_s=15.0, rows=64):
     """The oracle's torch-CPU fp32 restatement of the reference graph (model.py:114-235 with all
     three branches per call, Q2; two calls per step as supervisor.py:17-18) on a bounded sample:
@@ -415,7 +475,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS) + ["pipeline"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--train-steps", type=int, default=50, help="train-step side measurement (0 = skip)")
@@ -436,6 +496,9 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
+    if a.workload == "pipeline":
+        print(json.dumps(pipeline_bench(WORKLOADS["c2"], a, device)), flush=True)
+        return
     w = WORKLOADS[a.workload]
     fn = FN_IDS.get(w["fn"])
     B, N = w["B"], w["N"]

@@ -874,7 +874,9 @@ static int launch_events(const EvArgs& a, const StepWs& w, hipStream_t st) {
     if (hipMemsetAsync(w.count, 0, (size_t)(a.E * 4), st) != hipSuccess) return check_launch("memset");
     const unsigned eb = (unsigned)((a.total + kBlock - 1) / kBlock);
     if (a.total > 0) hipLaunchKernelGGL(ev_count_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.count);
-    if (a.E > 0) hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, a.E, w.off, w.cursor, 1);
+    if (a.E > 0)
+        hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, a.E, w.off, w.cursor, 1,
+                           a.total);
     if (a.total > 0) hipLaunchKernelGGL(ev_scatter_kernel, dim3(eb), dim3(kBlock), 0, st, a, w.cursor, w.code);
     return check_launch("kge_step_backward events");
 }
@@ -1204,7 +1206,8 @@ int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld
     rc = run_score(fn, mode, p, KIND_STEP_FWD_GRAD, stream);
     if (rc) return rc;
     // 2. bucket offsets (one launch; resets the counts for the next call)
-    hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, nentity, w.off, w.cursor, 1);
+    hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, nentity, w.off, w.cursor, 1,
+                       (int)(B * N + 3 * B));
     rc = check_launch("kge_train_step scan");
     if (rc) return rc;
     // 3. one launch: event scatter, loss weights, score gradients, both slots' query chains, the loss

@@ -1342,7 +1342,10 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
     vecf<V> acc_a[G], acc_b[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) acc_a[k] = acc_b[k] = vzero<V>();
-    const int lo = p.ev_off[e], hi = p.ev_off[e + 1];
+    // bucket bounds and codes are validated against the event count: a corrupted bucket table (a
+    // workspace that was not zero-filled) gives wrong gradients, never an out-of-range access
+    const int ntot = (int)(p.Bn * p.Nn + 3 * p.Bn);
+    const int lo = min(max(p.ev_off[e], 0), ntot), hi = min(max(p.ev_off[e + 1], lo), ntot);
     const int n = hi - lo;
     Cand<FN, V, G> c;
     if (n > 0 || p.adam.on) c.load(p.cent + e * p.c_ld, true, D, lane);
@@ -1365,8 +1368,10 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
     if (n > 0) {
         if (n <= kWave) {
             int code = lane < n ? p.ev_code[lo + lane] : INT32_MAX;
+            if ((unsigned)code >= (unsigned)ntot) code = INT32_MAX;  // never index with a stray code
+            const int nv = __popcll(__ballot(code != INT32_MAX));
             code = wave_sort_asc(code, lane);
-            for (int j = 0; j < n; ++j)
+            for (int j = 0; j < nv; ++j)
                 ent_event<FN, CH, V, G>(p, c, __builtin_amdgcn_readlane(code, j), lane, acc_a, acc_b);
         } else {
             // large bucket: extract codes in ascending order (O(n^2 / 64), rare for random ids)
@@ -1375,9 +1380,10 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_kernel(ScoreParams p) {
                 int m = INT32_MAX;
                 for (int i = lo + lane; i < hi; i += kWave) {
                     const int v = p.ev_code[i];
-                    if (v > last && v < m) m = v;
+                    if (v > last && v < m && v < ntot) m = v;
                 }
                 m = wave_min_i(m);
+                if (m == INT32_MAX) break;
                 ent_event<FN, CH, V, G>(p, c, m, lane, acc_a, acc_b);
                 last = m;
             }
@@ -1665,7 +1671,7 @@ __global__ __launch_bounds__(kBlock) void step_epilogue_kernel(ScoreParams p) {
             for (int u = 0; u < U; ++u) at[u] = (k[u] >= 0 && k[u] < p.c_rows) ? atomicAdd(p.ev_cursor + k[u], 1) : -1;
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (at[u] >= 0) p.ev_code_w[at[u]] = c0 + u * nl;
+                if (at[u] >= 0 && at[u] < total) p.ev_code_w[at[u]] = c0 + u * nl;
         }
     }
     if (blockIdx.x == gridDim.x - 1) {
@@ -1859,7 +1865,10 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
     // streamed (read-once) operands: the table row and its Adam moments. Default cache policy: nt
     // loads / sc1 stores measured no faster here (the next step's forward re-reads the table)
     auto sload = [&](rsrc_t r, uint32_t off) { return bload<V>(r, off); };
-    const int lo = p.ev_off[e], hi = p.ev_off[e + 1];
+    // bucket bounds and codes are validated against the event count: a corrupted bucket table (a
+    // workspace that was not zero-filled) gives wrong gradients, never an out-of-range access
+    const int ntot = (int)(p.Bn * p.Nn + 3 * p.Bn);
+    const int lo = min(max(p.ev_off[e], 0), ntot), hi = min(max(p.ev_off[e + 1], lo), ntot);
     const int n = hi - lo;
     // the row slice, and the Adam moments requested up front so their latency overlaps the walk
     vecf<V> ca[GW], cb[GW], mm[NH][GW], vv[NH][GW];
@@ -1960,15 +1969,17 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
         };
         if (n <= kWave) {
             int code = lane < n ? p.ev_code[lo + lane] : INT32_MAX;
+            if ((unsigned)code >= (unsigned)ntot) code = INT32_MAX;  // never index with a stray code
+            const int nv = __popcll(__ballot(code != INT32_MAX));
             code = wave_sort_asc(code, lane);
-            for (int j = 0; j < n; j += U) {
+            for (int j = 0; j < nv; j += U) {
                 vecf<V> x0[U][GW], x1[U][GW], x2[U][GW];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    if (j + u < n) load_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
+                    if (j + u < nv) load_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    if (j + u < n) apply_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
+                    if (j + u < nv) apply_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
             }
         } else {
             // large bucket: extract codes in ascending order (O(n^2 / 64), rare for random ids)
@@ -1977,9 +1988,10 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
                 int m = INT32_MAX;
                 for (int i = lo + lane; i < hi; i += kWave) {
                     const int v = p.ev_code[i];
-                    if (v > last && v < m) m = v;
+                    if (v > last && v < m && v < ntot) m = v;
                 }
                 m = wave_min_i(m);
+                if (m == INT32_MAX) break;
                 vecf<V> x0[GW], x1[GW], x2[GW];
                 load_ev(m, x0, x1, x2);
                 apply_ev(m, x0, x1, x2);

@@ -84,7 +84,7 @@ typedef int scan_i4 __attribute__((ext_vector_type(4)));
 typedef unsigned scan_u4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(kScanTile) void scan_block_kernel(int* __restrict__ count, int64_t E, int* __restrict__ off,
-                                                               int* __restrict__ cursor, int zero) {
+                                                               int* __restrict__ cursor, int zero, int cap) {
     constexpr int NW = kScanTile / kWave;  // 16 waves
     __shared__ int wtot[kScanK][NW];
     __shared__ int carry_s;
@@ -127,14 +127,14 @@ __global__ __launch_bounds__(kScanTile) void scan_block_kernel(int* __restrict__
                 all += v;
             }
             int run = tile_base + before + incl[r] - (x[r][0] + x[r][1] + x[r][2] + x[r][3]);
-            scan_i4 o4;
-            o4[0] = run;
+            scan_i4 o4;  // offsets clamped to `cap` (the number of events): corrupt counts stay in bounds
+            o4[0] = min(run, cap);
             run += x[r][0];
-            o4[1] = run;
+            o4[1] = min(run, cap);
             run += x[r][1];
-            o4[2] = run;
+            o4[2] = min(run, cap);
             run += x[r][2];
-            o4[3] = run;
+            o4[3] = min(run, cap);
             const int64_t e0 = base + ((int64_t)r * kScanTile + t) * 4;
             if (e0 < E) {
                 const scan_u4 u = __builtin_bit_cast(scan_u4, o4);
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kScanTile) void scan_block_kernel(int* __restrict__
     }
     if (t == 0) carry_s = carry;
     __syncthreads();
-    if (t == 0) off[E] = carry_s;
+    if (t == 0) off[E] = min(carry_s, cap);
 }
 
 }  // namespace

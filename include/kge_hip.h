@@ -281,7 +281,9 @@ int kge_step_backward_adam(int fn, int mode,
  *   Results equal kge_step_backward_adam's to fp32 rounding (the query gradient is summed in a
  *   different order); deterministic run to run.
  *   workspace: kge_train_step_workspace_size(...) bytes, ZERO-FILLED before its first use; every
- *   call leaves it reusable (the per-entity counters it keeps are zero again on return).
+ *   call leaves it reusable (the per-entity counters it keeps are zero again on return). A workspace
+ *   that was not zero-filled gives wrong gradients for that call (never an out-of-range access: bucket
+ *   offsets and event codes are bounds-checked) and is clean again afterwards.
  */
 int64_t kge_train_step_workspace_size(int fn, int64_t nentity, int64_t nrelation, int64_t rel_ld,
                                       int64_t B, int64_t N, int64_t D);

@@ -249,3 +249,37 @@ def test_one_call_train_step_matches_oracle_tf_step():
     np.testing.assert_allclose(losses, ref_losses, rtol=1e-4)
     assert (m.entity_embedding.detach().cpu().double() - ent).abs().max().item() <= 5e-2 * lr
     assert (m.relation_embedding.detach().cpu().double() - rel).abs().max().item() <= 5e-2 * lr
+
+
+def test_train_step_garbage_workspace_is_bounded_and_self_cleaning():
+    """kge_train_step with a workspace that was NOT zero-filled (the counters hold 0x7F7F7F7F): the
+    bounds checks keep every access in range (the call returns, the GPU does not fault) and the call
+    leaves the counters zero, so the next step with the same workspace equals a step with a fresh one."""
+    name, E, R, d, B, N = "InterHT", 70, 4, 96, 16, 24
+    g = np.random.RandomState(12)
+    data = []
+    for i in range(2):
+        pos = torch.from_numpy(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1))
+        neg = torch.from_numpy(g.randint(E, size=(B, N)))
+        data.append((pos.to(DEV), neg.to(DEV), torch.ones(B, device=DEV), i % 2))
+    m = kge.TFKGEModel(name, E, R, d, 9.0, True, False, True, device=DEV, seed=3)
+    opt = Adam(m.parameters(), lr=1e-3)
+    from customknowledgegraphembedding_amd import _lib
+    nbytes = _lib.load().kge_train_step_workspace_size(4, E, R, m.relation_embedding.stride(0), B, N, d)
+    m._train_ws = torch.full((nbytes,), 0x7F, dtype=torch.uint8, device=DEV)
+    pos, neg, w, mode = data[0]
+    m.train_step_fused(pos, neg, w, mode, opt)  # garbage buckets: wrong gradients, but in bounds
+    torch.cuda.synchronize()
+    # a twin continues from the same state with a fresh workspace
+    twin = kge.TFKGEModel(name, E, R, d, 9.0, True, False, True, device=DEV, seed=3)
+    twin.load_state_dict(m.state_dict())
+    opt2 = Adam(twin.parameters(), lr=1e-3)
+    for p_src, p_dst in zip(m.parameters(), twin.parameters()):
+        st = opt.state[p_src]
+        opt2.state[p_dst] = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+    pos, neg, w, mode = data[1]
+    la = float(m.train_step_fused(pos, neg, w, mode, opt))
+    lb = float(twin.train_step_fused(pos, neg, w, mode, opt2))
+    assert la == lb
+    for x, y in zip(m.parameters(), twin.parameters()):
+        assert torch.equal(x, y)

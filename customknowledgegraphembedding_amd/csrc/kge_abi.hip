@@ -206,7 +206,10 @@ __global__ __launch_bounds__(kBlock) void ev_scatter_kernel(EvArgs a, int* __res
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= a.total) return;
     const int64_t k = ev_key(a, i);
-    if (k >= 0 && k < a.E) code[atomicAdd(&cursor[k], 1)] = i;
+    if (k >= 0 && k < a.E) {
+        const int at = atomicAdd(&cursor[k], 1);
+        if (at >= 0 && at < a.total) code[at] = i;
+    }
 }
 
 // Relation gradient: one block per (relation, 64-column chunk). Its four waves split the slots (a

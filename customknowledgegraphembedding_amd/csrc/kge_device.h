@@ -61,6 +61,15 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
 
 // AUX: cache policy bits of the buffer instruction (gfx950: 2 = nt, 16 = sc1)
 constexpr int kAuxNT = 2, kAuxSC1 = 16;
+// cache policy of bwd_ent_stream_kernel's streamed table row and Adam moments: nt loads AND nt
+// stores (either alone measured no faster; together the C2 train step drops 0.636 -> 0.606 ms,
+// scripts/ab_cache_policy.sh). Overridable with -D for A/B builds.
+#ifndef KGE_ENT_LD_AUX
+#define KGE_ENT_LD_AUX kAuxNT
+#endif
+#ifndef KGE_ENT_ST_AUX
+#define KGE_ENT_ST_AUX kAuxNT
+#endif
 
 template <int V, int AUX = 0>
 __device__ __forceinline__ vecf<V> bload(rsrc_t r, uint32_t off) {
@@ -1862,9 +1871,8 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
         goffs[gg] = goff<V>(lane, k);
         gin[gg] = (lane + k * kWave) < DV;
     }
-    // streamed (read-once) operands: the table row and its Adam moments. Default cache policy: nt
-    // loads / sc1 stores measured no faster here (the next step's forward re-reads the table)
-    auto sload = [&](rsrc_t r, uint32_t off) { return bload<V>(r, off); };
+    // streamed (read-once) operands: the table row and its Adam moments, nontemporal (KGE_ENT_LD_AUX)
+    auto sload = [&](rsrc_t r, uint32_t off) { return bload<V, KGE_ENT_LD_AUX>(r, off); };
     // bucket bounds and codes are validated against the event count: a corrupted bucket table (a
     // workspace that was not zero-filled) gives wrong gradients, never an out-of-range access
     const int ntot = (int)(p.Bn * p.Nn + 3 * p.Bn);
@@ -2027,7 +2035,7 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
                 sb[gg].a[i] += rb[gg].a[i];
             }
     }
-    auto sstore = [&](rsrc_t r, uint32_t off, const vecf<V>& v) { bstore<V>(r, off, v); };
+    auto sstore = [&](rsrc_t r, uint32_t off, const vecf<V>& v) { bstore<V, KGE_ENT_ST_AUX>(r, off, v); };
     if (p.adam.on) {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {

@@ -3,6 +3,7 @@
 // The train step's dense Adam touches every row of the entity table: parameters, m and v are read and
 // written (fused into the entity pass: 3 reads + 3 writes), or additionally the gradient is read (the
 // standalone kernel: 4 + 3). This probe times those patterns, plus a plain copy and a read-only sum,
+// (and with nontemporal stores / loads, the `NT` variants)
 // over 327.5 MB arrays (the C2 table), each with float4 per thread and U float4 per thread per
 // iteration, grid-stride, 256 threads, `blocks` CUs x waves. Reports total bytes moved / time.
 // Build: hipcc --offload-arch=gfx950 -O3 -o stream_probe stream_probe.hip
@@ -33,21 +34,45 @@ __global__ __launch_bounds__(256) void read_k(const float4* __restrict__ a, int6
     if (s == 12345.f) out[0] = s;
 }
 
-template <int U>
+// NT: 0 plain, 1 nontemporal stores, 2 nontemporal loads and stores
+template <int NT>
+__device__ __forceinline__ void st4(float4* dst, const float4& x) {
+    if constexpr (NT >= 1) {
+        float* d = reinterpret_cast<float*>(dst);
+        __builtin_nontemporal_store(x.x, d + 0);
+        __builtin_nontemporal_store(x.y, d + 1);
+        __builtin_nontemporal_store(x.z, d + 2);
+        __builtin_nontemporal_store(x.w, d + 3);
+    } else {
+        *dst = x;
+    }
+}
+template <int NT>
+__device__ __forceinline__ float4 ld4(const float4* src) {
+    if constexpr (NT >= 2) {
+        const float* s = reinterpret_cast<const float*>(src);
+        return make_float4(__builtin_nontemporal_load(s + 0), __builtin_nontemporal_load(s + 1),
+                           __builtin_nontemporal_load(s + 2), __builtin_nontemporal_load(s + 3));
+    } else {
+        return *src;
+    }
+}
+
+template <int U, int NT = 0>
 __global__ __launch_bounds__(256) void copy_k(const float4* __restrict__ a, float4* __restrict__ b, int64_t n4) {
     for (int64_t i = (int64_t)blockIdx.x * 256 * U + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256 * U) {
         float4 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (i + u * 256 < n4) v[u] = a[i + u * 256];
+            if (i + u * 256 < n4) v[u] = ld4<NT>(a + i + u * 256);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (i + u * 256 < n4) b[i + u * 256] = v[u];
+            if (i + u * 256 < n4) st4<NT>(b + i + u * 256, v[u]);
     }
 }
 
 // Adam-shaped: NR reads (p, m, v [, g]) and 3 writes (p, m, v)
-template <int U, bool G>
+template <int U, bool G, int NT = 0>
 __global__ __launch_bounds__(256) void adam_k(float4* __restrict__ p, float4* __restrict__ m, float4* __restrict__ v,
                                               const float4* __restrict__ g, int64_t n4) {
     for (int64_t i = (int64_t)blockIdx.x * 256 * U + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256 * U) {
@@ -56,10 +81,10 @@ __global__ __launch_bounds__(256) void adam_k(float4* __restrict__ p, float4* __
         for (int u = 0; u < U; ++u) {
             const int64_t j = i + u * 256;
             if (j < n4) {
-                pp[u] = p[j];
-                mm[u] = m[j];
-                vv[u] = v[j];
-                gg[u] = G ? g[j] : make_float4(1e-3f, 1e-3f, 1e-3f, 1e-3f);
+                pp[u] = ld4<NT>(p + j);
+                mm[u] = ld4<NT>(m + j);
+                vv[u] = ld4<NT>(v + j);
+                gg[u] = G ? ld4<NT>(g + j) : make_float4(1e-3f, 1e-3f, 1e-3f, 1e-3f);
             }
         }
 #pragma unroll
@@ -73,9 +98,9 @@ __global__ __launch_bounds__(256) void adam_k(float4* __restrict__ p, float4* __
     a.X = a.X - b.X * 1e-3f / (sqrtf(c.X) + 1e-7f);
                 UPD(x) UPD(y) UPD(z) UPD(w)
 #undef UPD
-                p[j] = a;
-                m[j] = b;
-                v[j] = c;
+                st4<NT>(p + j, a);
+                st4<NT>(m + j, b);
+                st4<NT>(v + j, c);
             }
         }
     }
@@ -122,6 +147,14 @@ int main() {
                [&] { hipLaunchKernelGGL((adam_k<1, true>), dim3(blocks), dim3(256), 0, 0, a, b, c, d, n4); });
         timeit("adam dense 4r+3w U2", 7.0 * bytes,
                [&] { hipLaunchKernelGGL((adam_k<2, true>), dim3(blocks), dim3(256), 0, 0, a, b, c, d, n4); });
+        timeit("copy 1r+1w nt-store", 2.0 * bytes,
+               [&] { hipLaunchKernelGGL((copy_k<2, 1>), dim3(blocks), dim3(256), 0, 0, a, b, n4); });
+        timeit("copy 1r+1w nt-load+store", 2.0 * bytes,
+               [&] { hipLaunchKernelGGL((copy_k<2, 2>), dim3(blocks), dim3(256), 0, 0, a, b, n4); });
+        timeit("adam fused 3r+3w U2 nt-store", 6.0 * bytes,
+               [&] { hipLaunchKernelGGL((adam_k<2, false, 1>), dim3(blocks), dim3(256), 0, 0, a, b, c, d, n4); });
+        timeit("adam fused 3r+3w U2 nt-load+store", 6.0 * bytes,
+               [&] { hipLaunchKernelGGL((adam_k<2, false, 2>), dim3(blocks), dim3(256), 0, 0, a, b, c, d, n4); });
     }
     return 0;
 }

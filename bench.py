@@ -9,29 +9,35 @@ negative mode (head/tail alternating, model.py:148-199) and for mode 3 (single, 
   * logsigmoid of the positives                     -> [B, 1]   (log_sigmoid_kernel)
 Scored triples per step = B*N + B (the reference's redundant branches, Q2, are not counted).
 
-Multi-GPU: one process per GPU (torchrun); each rank scores its own batch with its own replica
-of the table (weak scaling, no collective in the data path); timing = max over ranks.
+Multi-GPU: one process per GPU; each rank scores its own batch with its own replica of the table
+(weak scaling, no collective in the data path); timing = max over ranks. `--gpus N` (N > 1) outside
+torchrun starts the N ranks itself: `python -m torch.distributed.run --nproc-per-node N` as a child
+process, before this process makes any GPU call; the parent exits with the children's status.
+Under torchrun (WORLD_SIZE set) the world size comes from the environment.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4]
+Positives: the reference's own triples where the snapshot has them (tests/golden/
+<dataset>_ids.npz, made by tests/golden/make_datasets.py): WN18RR train.txt for C2 (RandomState(0)
+permutation, read sequentially), FB15k-237 / YAGO3-10 valid+test for C3 / C4; negatives
+RandomState(2).randint(E, (B, N)).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|...] [--dry-run]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
+import torch  # importing torch makes no GPU call; the package (and its HIP library) loads in main()
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-import customknowledgegraphembedding_amd as kge  # noqa: E402
-from customknowledgegraphembedding_amd import ops  # noqa: E402
-from customknowledgegraphembedding_amd._lib import FN_IDS  # noqa: E402
 
 METRIC = "scored (pos+neg) triples/sec, WN18RR InterHT d=1000 n_neg=256, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -40,15 +46,15 @@ WORKLOADS = {
     # BASELINE.json configs[1]: the metric's config
     "c2": dict(name="WN18RR InterHT d=1000 -de -tr gamma=24 n_neg=256 bz=512", fn="InterHT",
                nentity=40943, nrelation=11, hidden_dim=1000, gamma=24.0, de=True, tr=True, dr=False,
-               B=512, N=256),
+               B=512, N=256, dataset="wn18rr"),
     # configs[2]
     "c3": dict(name="FB15k-237 RotatE d=1000 -de gamma=9 n_neg=256 bz=512", fn="RotatE",
                nentity=14541, nrelation=237, hidden_dim=1000, gamma=9.0, de=True, tr=False, dr=False,
-               B=512, N=256),
+               B=512, N=256, dataset="fb15k237"),
     # configs[3] (single-GPU replica form)
     "c4": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512", fn="DistMult",
                nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False, dr=False,
-               B=512, N=1024),
+               B=512, N=1024, dataset="yago3_10"),
     # configs[3] as the north star states it: entity table row-sharded over the ranks
     # (owner-computes, distributed.ShardedKGE; bz=512 per rank)
     # configs[4]: FB15k link-prediction eval, each query vs all 14 951 entities, filtered ranks
@@ -111,19 +117,49 @@ def algorithmic_bytes(w):
     return neg, pos
 
 
-def make_inputs(w, rank, device, n_batches=8):
-    ent_dim, rel_dim, D, _ = dims(w)
+def load_triples(w):
+    """The reference's triples of the workload's dataset (tests/golden/<dataset>_ids.npz), or None."""
+    key = w.get("dataset")
+    if not key:
+        return None
+    path = os.path.join(ROOT, "tests", "golden", f"{key}_ids.npz")
+    with np.load(path) as z:  # allow_pickle=False: plain int arrays
+        tri = z["triples"].astype(np.int64)
+        assert int(z["nentity"]) == w["nentity"] and int(z["nrelation"]) == w["nrelation"], path
+    return tri
+
+
+def positives(w, rank, n_batches, world=1):
+    """[n_batches] x [B, 3] positives: the dataset's triples in a RandomState(0) permutation, read
+    sequentially (rank r takes every world-th batch), or uniform random ids without a dataset."""
+    E, R, B = w["nentity"], w["nrelation"], w["B"]
+    tri = load_triples(w)
+    out = []
+    if tri is None:
+        for i in range(n_batches):
+            g = np.random.RandomState(1 + 1000 * rank + i)
+            out.append(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1))
+        return out, "uniform random (h, r, t)"
+    perm = np.random.RandomState(0).permutation(len(tri))
+    for i in range(n_batches):
+        k = (i * world + rank) * B
+        idx = perm[np.arange(k, k + B) % len(tri)]
+        out.append(tri[idx])
+    return out, f"reference triples tests/golden/{w['dataset']}_ids.npz (RandomState(0) permutation)"
+
+
+def make_inputs(w, rank, device, n_batches=8, world=1):
     from customknowledgegraphembedding_amd.model import TFKGEModel
     m = TFKGEModel(w["fn"], w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"],
                    double_entity_embedding=w["de"], double_relation_embedding=w["dr"],
                    triple_relation_embedding=w["tr"], device=device, seed=0)
-    E, R, B, N = w["nentity"], w["nrelation"], w["B"], w["N"]
+    E, B, N = w["nentity"], w["B"], w["N"]
+    pos_l, src = positives(w, rank, n_batches, world)
     batches = []
     for i in range(n_batches):
-        g = np.random.RandomState(1 + 1000 * rank + i)
-        pos = np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1)
         neg = np.random.RandomState(2 + 1000 * rank + i).randint(E, size=(B, N))
-        batches.append((torch.from_numpy(pos).to(device), torch.from_numpy(neg).to(device)))
+        batches.append((torch.from_numpy(pos_l[i]).to(device), torch.from_numpy(neg).to(device)))
+    m.positives_source = src
     return m, batches
 
 
@@ -470,7 +506,59 @@ def cpu_baseline(w, budget_s=15.0, rows=64):
     }
 
 
-def main():
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a, argv):
+    """`bench.py --gpus N` outside torchrun: run the N ranks as children of this process (this
+    process never touches the GPU) and return their exit status. Rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(a, world, rank):
+    """CPU rehearsal of the launcher and the multi-rank timing contract (gloo; no kernels, no GPU):
+    barrier, K timed no-op steps, max over ranks, one JSON line from rank 0."""
+    import torch
+    import torch.distributed as tdist
+    if world > 1:
+        tdist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        pass
+    if world > 1:
+        tdist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        el = float(t.item())
+        seen = torch.tensor([rank], dtype=torch.int64)
+        tdist.all_reduce(seen, op=tdist.ReduceOp.SUM)
+        ranks_seen = int(seen.item())
+    else:
+        ranks_seen = 0
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "triples/s", "n_gpus": world, "steps": a.steps,
+                          "warmup": a.warmup, "ms_per_step": el / max(1, a.steps) * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "dry run (no kernels)",
+                          "config": {"workload": "dry-run", "parallelism": f"replicas{world}"},
+                          "dry_run": True, "rank_sum": ranks_seen}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -483,11 +571,24 @@ def main():
                     help="timing events bracket groups of this many consecutive launches")
     ap.add_argument("--sharded-steps", type=int, default=20,
                     help="side measurement of the YAGO3-10 row-sharded step (c4s) at the same world size (0 = skip)")
-    a = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo rehearsal of the launcher and timing contract (no GPU, no kernels)")
+    a = ap.parse_args(argv)
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a, argv)  # before any GPU call in this process
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if a.dry_run:
+        return dry_run(a, world, rank)
+
+    global kge, ops, FN_IDS
+    import customknowledgegraphembedding_amd as kge  # noqa: F401
+    from customknowledgegraphembedding_amd import ops
+    from customknowledgegraphembedding_amd._lib import FN_IDS
     dist = world > 1
     if dist:
         import torch.distributed as tdist
@@ -609,8 +710,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: U(-(gamma+2)/d,(gamma+2)/d) tables (seed 0), uniform random (h,r,t) positives and "
-                "negatives, 8 distinct batches resident in HBM, mode alternating head/tail",
+        "data": "synthetic U(-(gamma+2)/d,(gamma+2)/d) tables (seed 0); positives: " + m.positives_source +
+                "; negatives RandomState(2).randint(E); 8 distinct batches resident in HBM, mode alternating head/tail",
         "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N, "hidden_dim": w["hidden_dim"],
                    "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -651,4 +752,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -155,6 +155,15 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float* __restrict__ p, flo
         for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += kBlock) adam_one(p[i], g[i], m[i], v[i], a);
 }
 
+// The same update for buffers that are not all 16-byte aligned (e.g. a parameter that is an offset
+// view of a larger allocation): dword accesses, grid-stride. Bitwise the same per element.
+__global__ __launch_bounds__(kBlock) void adam_scalar_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                             float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                             AdamArgs a) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        adam_one(p[i], g[i], m[i], v[i], a);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Owned-row gather of a row-sharded table: out[i] = table[ids[i*stride] - lo] if this shard owns
 // the id, else zeros (so a SUM all-reduce over shards assembles the rows exactly). One wave per row.
@@ -762,8 +771,9 @@ int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq
     if (n < 0 || step < 1) return fail(KGE_EINVAL, "bad size or step (step is 1-based)");
     if (n == 0) return ok();
     if (!param || !grad || !exp_avg || !exp_avg_sq) return fail(KGE_EINVAL, "null pointer");
-    if (!aligned(param, 16) || !aligned(grad, 16) || !aligned(exp_avg, 16) || !aligned(exp_avg_sq, 16))
-        return fail(KGE_EINVAL, "adam buffers must be 16-byte aligned");
+    if (!aligned(param, 4) || !aligned(grad, 4) || !aligned(exp_avg, 4) || !aligned(exp_avg_sq, 4))
+        return fail(KGE_EINVAL, "adam buffers must be 4-byte aligned fp32");
+    const bool vec = aligned(param, 16) && aligned(grad, 16) && aligned(exp_avg, 16) && aligned(exp_avg_sq, 16);
     const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
     const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
     AdamArgs a;
@@ -779,8 +789,12 @@ int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq
     const int64_t want = (n / 4 + per_block - 1) / per_block;
     if (want > INT32_MAX) return fail(KGE_EINVAL, "tensor too large for one launch");
     const int blocks = (int)std::max<int64_t>(1, want);
-    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, param, grad, exp_avg,
-                       exp_avg_sq, n, a);
+    if (vec)
+        hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, param, grad, exp_avg,
+                           exp_avg_sq, n, a);
+    else
+        hipLaunchKernelGGL(adam_scalar_kernel, dim3((unsigned)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, n, a);
     return check_launch("kge_adam_update");
 }
 
@@ -1217,11 +1231,15 @@ int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld
                                   t.d_out, t.d_out, nullptr, d_rel, nullptr, t.stats, workspace, base, stream, &a,
                                   m_ent, v_ent, o);
     }
-    p.ev_count = w.count;  // zero on entry (the workspace contract), re-zeroed by the scan
+    // the per-entity event counters are zeroed here, on every call: the workspace carries no state
+    // between calls, so any workspace contents (fresh, shared, or left by an aborted call) are valid
+    if (nentity > 0 && hipMemsetAsync(w.count, 0, (size_t)(nentity * 4), st) != hipSuccess)
+        return check_launch("kge_train_step memset");
+    p.ev_count = w.count;
     rc = run_score(fn, mode, p, KIND_STEP_FWD_GRAD, stream);
     if (rc) return rc;
-    // 2. bucket offsets (one launch; resets the counts for the next call)
-    hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, nentity, w.off, w.cursor, 1,
+    // 2. bucket offsets (one launch)
+    hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, nentity, w.off, w.cursor, 0,
                        (int)(B * N + 3 * B));
     rc = check_launch("kge_train_step scan");
     if (rc) return rc;

@@ -199,10 +199,11 @@ class TFKGEModel(_KGEBase):
 
 
     def _train_workspace(self, nbytes, device):
-        """kge_train_step's workspace: zero-filled once, then reused (each call leaves it reusable)."""
+        """kge_train_step's workspace, cached by size (the call zeroes the counters it keeps there
+        itself, so the contents never matter: any shape may reuse a large-enough buffer)."""
         ws = getattr(self, "_train_ws", None)
         if ws is None or ws.numel() < nbytes or ws.device != device:
-            ws = torch.zeros(max(nbytes, 1), dtype=torch.uint8, device=device)
+            ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
             self._train_ws = ws
         return ws
 
@@ -265,9 +266,13 @@ class TFKGEModel(_KGEBase):
             None if stats is None else stats.data_ptr(), ws.data_ptr(), ws.numel(),
             torch.cuda.current_stream(ent.device).cuda_stream)
         _lib.check(rc, "kge_step_backward_adam")
+        self._adam_commit(optimizer, [ent, rel] + ([self.modulus] if is_p else []))
         return loss.detach()
 
     def _adam_state(self, optimizer, params):
+        """(group, lr, step) for the next update. The step counters are NOT advanced here: the caller
+        commits them with _adam_commit only after the kernel call returned success, so a rejected
+        call leaves the bias correction where it was."""
         from .optim import resolve_lr
 
         group = optimizer.param_groups[0]
@@ -279,8 +284,12 @@ class TFKGEModel(_KGEBase):
                 st["step"] = 0
                 st["exp_avg"] = torch.zeros_like(prm)
                 st["exp_avg_sq"] = torch.zeros_like(prm)
-            st["step"] += 1
-        return group, lr, optimizer.state[self.entity_embedding]["step"]
+        return group, lr, optimizer.state[self.entity_embedding]["step"] + 1
+
+    @staticmethod
+    def _adam_commit(optimizer, params):
+        for prm in params:
+            optimizer.state[prm]["step"] += 1
 
     def _train_step_one_call(self, fn, m, positive_sample, negative_sample, subsampling_weight, optimizer,
                              loss_sum=None):
@@ -314,6 +323,7 @@ class TFKGEModel(_KGEBase):
             float(lr), float(b1), float(b2), float(group["eps"]), int(step), int(group["semantics"] == "keras"),
             ws.data_ptr(), ws.numel(), torch.cuda.current_stream(dev).cuda_stream)
         _lib.check(rc, "kge_train_step")
+        self._adam_commit(optimizer, [ent, rel])
         return out[0]
 
 

@@ -81,11 +81,11 @@ class Adam(torch.optim.Optimizer):
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
-                st["step"] += 1
                 rc = lib.kge_adam_update(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
                                          st["exp_avg_sq"].data_ptr(), p.numel(), float(lr), float(b1),
-                                         float(b2), float(group["eps"]), int(st["step"]),
+                                         float(b2), float(group["eps"]), int(st["step"]) + 1,
                                          int(group["semantics"] == "keras"), 0,
                                          torch.cuda.current_stream(p.device).cuda_stream)
                 check(rc, "kge_adam_update")
+                st["step"] += 1  # committed only once the library accepted the update
         return loss

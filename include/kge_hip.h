@@ -280,10 +280,9 @@ int kge_step_backward_adam(int fn, int mode,
  *   (supervisor.py:28 metrics.update_state), incremented by the loss on the device.
  *   Results equal kge_step_backward_adam's to fp32 rounding (the query gradient is summed in a
  *   different order); deterministic run to run.
- *   workspace: kge_train_step_workspace_size(...) bytes, ZERO-FILLED before its first use; every
- *   call leaves it reusable (the per-entity counters it keeps are zero again on return). A workspace
- *   that was not zero-filled gives wrong gradients for that call (never an out-of-range access: bucket
- *   offsets and event codes are bounds-checked) and is clean again afterwards.
+ *   workspace: kge_train_step_workspace_size(...) bytes of scratch with NO state between calls: the
+ *   call zeroes the per-entity event counters it keeps there itself (an async memset on `stream`), so
+ *   any contents (uninitialised, reused at another shape, left by an aborted call) give the same result.
  */
 int64_t kge_train_step_workspace_size(int fn, int64_t nentity, int64_t nrelation, int64_t rel_ld,
                                       int64_t B, int64_t N, int64_t D);
@@ -381,7 +380,8 @@ int kge_tfrecord_writer_close(kge_tfrecord_writer* writer);
  *                            p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t))
  *   keras == 0: torch.optim.Adam (p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps))
  *   step is the 1-based step t; zero_grad != 0 also zeroes grad in the same pass.
- * All four buffers 16-byte aligned, n floats each.
+ * n floats each, 4-byte aligned; 16-byte aligned buffers take the float4 nontemporal path, others a
+ * dword path with bitwise the same per-element result.
  */
 int kge_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                     float lr, float beta1, float beta2, float eps, int64_t step,

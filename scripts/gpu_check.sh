@@ -16,7 +16,7 @@ step() {
   return 0
 }
 [[ $STEPS == *smoke* ]] && step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *test* ]] && step pytest_gpu 900 python3 -m pytest tests -m gpu -q -x -p no:cacheprovider
+[[ $STEPS == *test* ]] && step pytest_gpu 900 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
 [[ $STEPS == *bench* ]] && step bench 600 python3 bench.py
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp

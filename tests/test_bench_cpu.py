@@ -1,0 +1,72 @@
+"""CPU tests of bench.py's contract plumbing: `--gpus N` outside torchrun starts N ranks itself
+(world-2 gloo dry run: two ranks, one JSON line from rank 0 with n_gpus = 2), and the C2/C3/C4
+positives come from the reference's own triples."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def test_gpus2_self_launches_two_ranks_one_line():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3"],
+                       capture_output=True, text=True, timeout=180, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["dry_run"]
+    assert line["rank_sum"] == 1  # ranks 0 and 1 both joined the process group
+
+
+def test_gpus1_dry_run_is_single_process():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--steps", "2"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    (line,) = _json_lines(p.stdout)
+    assert line["n_gpus"] == 1
+
+
+def test_c2_positives_are_wn18rr_train_triples():
+    w = bench.WORKLOADS["c2"]
+    pos, src = bench.positives(w, 0, 3)
+    assert "wn18rr" in src
+    tri = bench.load_triples(w)
+    assert tri.shape == (86835, 3)
+    assert all(p.shape == (512, 3) for p in pos)
+    # every positive is a real training triple, in the RandomState(0) permutation order
+    perm = np.random.RandomState(0).permutation(len(tri))
+    assert np.array_equal(pos[0], tri[perm[:512]])
+    assert np.array_equal(pos[2], tri[perm[1024:1536]])
+    assert tri[:, 0].max() < w["nentity"] and tri[:, 1].max() < w["nrelation"]
+
+
+def test_positives_split_over_ranks_are_disjoint():
+    w = bench.WORKLOADS["c2"]
+    a, _ = bench.positives(w, 0, 2, world=2)
+    b, _ = bench.positives(w, 1, 2, world=2)
+    tri = bench.load_triples(w)
+    perm = np.random.RandomState(0).permutation(len(tri))
+    assert np.array_equal(a[0], tri[perm[0:512]]) and np.array_equal(b[0], tri[perm[512:1024]])
+    assert np.array_equal(a[1], tri[perm[1024:1536]])
+
+
+def test_c3_c4_positives_from_reference_splits():
+    for key, n in (("c3", 38001), ("c4", 10000)):
+        w = bench.WORKLOADS[key]
+        tri = bench.load_triples(w)
+        assert tri.shape == (n, 3)
+        assert tri[:, 0].max() < w["nentity"] and tri[:, 2].max() < w["nentity"]
+        assert tri[:, 1].max() < w["nrelation"]

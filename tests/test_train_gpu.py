@@ -31,6 +31,25 @@ def test_adam_keras_matches_oracle(n):
     assert err <= 1e-6, err
 
 
+@pytest.mark.parametrize("offset", [1, 2, 3])
+def test_adam_on_unaligned_parameter_view(offset):
+    """a parameter that is an offset view (4-byte, not 16-byte aligned) takes the dword
+    path and gives bitwise the update of an aligned copy."""
+    g0 = torch.Generator().manual_seed(offset)
+    base = torch.randn(4099 + offset, generator=g0).to(DEV)
+    view = torch.nn.Parameter(base[offset:])  # shares storage at a 4*offset-byte offset
+    assert view.data_ptr() % 16 != 0
+    ref = torch.nn.Parameter(base[offset:].clone())
+    o1, o2 = Adam([view], lr=1e-2), Adam([ref], lr=1e-2)
+    for _ in range(3):
+        gr = torch.randn(4099, generator=g0).to(DEV)
+        view.grad, ref.grad = gr.clone(), gr.clone()
+        o1.step()
+        o2.step()
+    assert torch.equal(view.detach(), ref.detach())
+    assert o1.state[view]["step"] == 3
+
+
 def test_adam_torch_semantics_matches_torch_optim():
     torch.manual_seed(0)
     a = torch.nn.Parameter(torch.randn(5000, device=DEV))
@@ -251,35 +270,63 @@ def test_one_call_train_step_matches_oracle_tf_step():
     assert (m.relation_embedding.detach().cpu().double() - rel).abs().max().item() <= 5e-2 * lr
 
 
-def test_train_step_garbage_workspace_is_bounded_and_self_cleaning():
-    """kge_train_step with a workspace that was NOT zero-filled (the counters hold 0x7F7F7F7F): the
-    bounds checks keep every access in range (the call returns, the GPU does not fault) and the call
-    leaves the counters zero, so the next step with the same workspace equals a step with a fresh one."""
-    name, E, R, d, B, N = "InterHT", 70, 4, 96, 16, 24
+def _twin_step(name, E, R, d, B, N, ws_fill, shapes):
+    """Run `shapes` (a list of (B, N)) train steps on one model whose workspace starts filled with
+    `ws_fill` bytes, and the same steps on fresh models with fresh zero workspaces; return both."""
+    from customknowledgegraphembedding_amd import _lib
     g = np.random.RandomState(12)
     data = []
-    for i in range(2):
-        pos = torch.from_numpy(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1))
-        neg = torch.from_numpy(g.randint(E, size=(B, N)))
-        data.append((pos.to(DEV), neg.to(DEV), torch.ones(B, device=DEV), i % 2))
-    m = kge.TFKGEModel(name, E, R, d, 9.0, True, False, True, device=DEV, seed=3)
-    opt = Adam(m.parameters(), lr=1e-3)
-    from customknowledgegraphembedding_amd import _lib
-    nbytes = _lib.load().kge_train_step_workspace_size(4, E, R, m.relation_embedding.stride(0), B, N, d)
-    m._train_ws = torch.full((nbytes,), 0x7F, dtype=torch.uint8, device=DEV)
-    pos, neg, w, mode = data[0]
-    m.train_step_fused(pos, neg, w, mode, opt)  # garbage buckets: wrong gradients, but in bounds
-    torch.cuda.synchronize()
-    # a twin continues from the same state with a fresh workspace
-    twin = kge.TFKGEModel(name, E, R, d, 9.0, True, False, True, device=DEV, seed=3)
-    twin.load_state_dict(m.state_dict())
-    opt2 = Adam(twin.parameters(), lr=1e-3)
-    for p_src, p_dst in zip(m.parameters(), twin.parameters()):
-        st = opt.state[p_src]
-        opt2.state[p_dst] = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}
-    pos, neg, w, mode = data[1]
-    la = float(m.train_step_fused(pos, neg, w, mode, opt))
-    lb = float(twin.train_step_fused(pos, neg, w, mode, opt2))
+    for i, (b, n) in enumerate(shapes):
+        pos = torch.from_numpy(np.stack([g.randint(E, size=b), g.randint(R, size=b), g.randint(E, size=b)], 1))
+        neg = torch.from_numpy(g.randint(E, size=(b, n)))
+        w = torch.from_numpy(g.uniform(0.1, 1.0, size=(b,))).float()
+        data.append((pos.to(DEV), neg.to(DEV), w.to(DEV), i % 2))
+    a = kge.TFKGEModel(name, E, R, d, 9.0, True, False, True, device=DEV, seed=3)
+    oa = Adam(a.parameters(), lr=1e-3)
+    nbytes = max(_lib.load().kge_train_step_workspace_size(4, E, R, a.relation_embedding.stride(0), b, n, d)
+                 for b, n in shapes)
+    a._train_ws = torch.full((nbytes,), ws_fill, dtype=torch.uint8, device=DEV)
+    b_ = kge.TFKGEModel(name, E, R, d, 9.0, True, False, True, device=DEV, seed=3)
+    ob = Adam(b_.parameters(), lr=1e-3)
+    la, lb = [], []
+    for pos, neg, w, mode in data:
+        la.append(float(a.train_step_fused(pos, neg, w, mode, oa)))
+        b_._train_ws = torch.zeros(nbytes, dtype=torch.uint8, device=DEV)  # fresh every step
+        lb.append(float(b_.train_step_fused(pos, neg, w, mode, ob)))
+    return (la, list(a.parameters())), (lb, list(b_.parameters()))
+
+
+@pytest.mark.parametrize("fill", [0x7F, 0xFF, 0x01])
+def test_train_step_garbage_workspace_gives_correct_first_step(fill):
+    """kge_train_step keeps no state in its workspace: a workspace filled with garbage (counters
+    0x7F7F7F7F, -1, 0x01010101) gives bitwise the same first step as a zero-filled one."""
+    (la, pa), (lb, pb) = _twin_step("InterHT", 70, 4, 96, 16, 24, fill, [(16, 24), (16, 24)])
     assert la == lb
-    for x, y in zip(m.parameters(), twin.parameters()):
+    for x, y in zip(pa, pb):
         assert torch.equal(x, y)
+
+
+def test_train_step_workspace_reused_at_a_smaller_batch():
+    """the cached workspace is reused when a later call has a smaller B (the count region
+    then lands on the previous call's float data); the step must still equal a fresh-workspace step."""
+    (la, pa), (lb, pb) = _twin_step("InterHT", 70, 4, 96, 16, 24, 0,
+                                    [(16, 24), (8, 24), (16, 12), (3, 40)])
+    assert la == lb
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+
+
+def test_rejected_train_step_does_not_advance_adam_step():
+    """a call the library rejects (here: a float64 weight pointer is fine, but a
+    negative-mode check fails for mode 3) must leave the optimizer's step counters unchanged."""
+    m = kge.TFKGEModel("InterHT", 40, 3, 16, 9.0, True, False, True, device=DEV, seed=1)
+    opt = Adam(m.parameters(), lr=1e-3)
+    pos = torch.tensor([[0, 1, 2], [3, 0, 5]], device=DEV)
+    neg = torch.randint(0, 40, (2, 7), device=DEV)
+    w = torch.ones(2, device=DEV)
+    m.train_step_fused(pos, neg, w, 1, opt)
+    assert opt.state[m.entity_embedding]["step"] == 1
+    with pytest.raises(Exception):
+        m.train_step_fused(pos, neg, w, 3, opt)
+    assert opt.state[m.entity_embedding]["step"] == 1
+    assert opt.state[m.relation_embedding]["step"] == 1

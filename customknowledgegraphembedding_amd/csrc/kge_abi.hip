@@ -356,6 +356,13 @@ int pick_cpw(int64_t B, int64_t N) {
     return (int)cpw;
 }
 
+int pick_cpw_sharded(int64_t B, int64_t N) {
+    if (N <= 1) return 1;
+    int64_t cpw = 512;
+    while (cpw > 16 && B * ((N + cpw - 1) / cpw) < 8192) cpw >>= 1;
+    return (int)cpw;
+}
+
 int dispatch(int fn, const ScoreParams& p, int kind, hipStream_t st, int blocks, bool ch, int V, int G) {
     switch (fn) {
         case KGE_TRANSE: return launch_transe(p, kind, st, blocks, ch, V, G);
@@ -412,7 +419,9 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     } else if (kind == KIND_BWD_ENT_STREAM) {
         waves = p.c_rows * kWavesPerBlock;  // one block per entity row
     } else {
-        p.cpw = pick_cpw(p.B, p.N);
+        // sharded scoring compacts each wave's owned candidates: long runs (up to 512 ids, ~64 owned
+        // at 8 shards) keep the per-wave query build amortised; >= 8192 waves still fill the chip
+        p.cpw = p.skip_foreign ? pick_cpw_sharded(p.B, p.N) : pick_cpw(p.B, p.N);
         p.wpr = (int)((p.N + p.cpw - 1) / p.cpw);
         waves = p.B * p.wpr;
     }

@@ -409,18 +409,14 @@ __device__ __forceinline__ const float* cand_row(const ScoreParams& p, int64_t i
     return p.cent + (ok ? id : 0) * p.c_ld;
 }
 
-// Scores candidates [n0, n0 + nc) (nc <= 64) of batch row b against the wave's query; score n0 + j
-// is produced in lane j and stored coalesced (and, with ST, InterHT's candidate inverse half-norms).
+// Scores up to 64 candidates held one per lane (lane j: global id my_id, j < nc) against the wave's
+// query; returns candidate j's score in lane j (and, with ST, InterHT's candidate inverse half-norms
+// in my_st). Software pipeline: row j+1 is in flight while row j is reduced.
 template <int FN, bool CH, int V, int G, bool ST>
-__device__ __forceinline__ void score_run(const ScoreParams& p, const Query<FN, CH, V, G>& q, int64_t b, int64_t n0,
-                                          int nc, int lane) {
-    int64_t my_id = 0;
-    if (lane < nc) my_id = p.c_idx ? p.c_idx[b * p.c_stride + n0 + lane] : b * p.c_dense + n0 + lane;
-
-    // software pipeline: row j+1 is in flight while row j is reduced. A foreign candidate of a
-    // row-sharded table (skip_foreign) loads nothing (0-byte descriptor) and scores 0.
+__device__ __forceinline__ float score_lanes(const ScoreParams& p, const Query<FN, CH, V, G>& q, int64_t my_id, int nc,
+                                             int lane, float2& my_st) {
     float my_score = 0.f;
-    float2 my_st = make_float2(0.f, 0.f), st;
+    float2 st;
     float2* stp = ST ? &st : nullptr;
     Cand<FN, V, G> x0, x1;
     bool ok0, ok1;
@@ -436,28 +432,117 @@ __device__ __forceinline__ void score_run(const ScoreParams& p, const Query<FN, 
     for (; j + 2 < nc; j += 2) {
         row = cand_row(p, readlane64(my_id, j + 1), ok1);
         x1.load(row, ok1, p.D, lane);
-        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
-        keep(j, s0);
+        keep(j, cand_score<FN, CH, V, G>(x0, q, p, stp));
         row = cand_row(p, readlane64(my_id, j + 2), ok0);
         x0.load(row, ok0, p.D, lane);
-        const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p, stp);
-        keep(j + 1, s1);
+        keep(j + 1, cand_score<FN, CH, V, G>(x1, q, p, stp));
     }
     if (j + 1 < nc) {
         row = cand_row(p, readlane64(my_id, j + 1), ok1);
         x1.load(row, ok1, p.D, lane);
-        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
-        keep(j, s0);
-        const float s1 = (p.skip_foreign && !ok1) ? 0.f : cand_score<FN, CH, V, G>(x1, q, p, stp);
-        keep(j + 1, s1);
+        keep(j, cand_score<FN, CH, V, G>(x0, q, p, stp));
+        keep(j + 1, cand_score<FN, CH, V, G>(x1, q, p, stp));
     } else {
-        const float s0 = (p.skip_foreign && !ok0) ? 0.f : cand_score<FN, CH, V, G>(x0, q, p, stp);
-        keep(j, s0);
+        keep(j, cand_score<FN, CH, V, G>(x0, q, p, stp));
     }
+    return my_score;
+}
+
+// Scores candidates [n0, n0 + nc) (nc <= 64) of batch row b against the wave's query; score n0 + j
+// is produced in lane j and stored coalesced (and, with ST, InterHT's candidate inverse half-norms).
+template <int FN, bool CH, int V, int G, bool ST>
+__device__ __forceinline__ void score_run(const ScoreParams& p, const Query<FN, CH, V, G>& q, int64_t b, int64_t n0,
+                                          int nc, int lane) {
+    int64_t my_id = 0;
+    if (lane < nc) my_id = p.c_idx ? p.c_idx[b * p.c_stride + n0 + lane] : b * p.c_dense + n0 + lane;
+    float2 my_st = make_float2(0.f, 0.f);
+    const float my_score = score_lanes<FN, CH, V, G, ST>(p, q, my_id, nc, lane, my_st);
     if (lane < nc) p.out[b * p.out_ld + n0 + lane] = my_score;
     if constexpr (ST) {
         if (lane < nc) p.cand_stats[b * p.N + n0 + lane] = my_st;
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row-sharded tables (SURVEY §8e owner-computes): this shard holds global entity rows
+// [c_base, c_base + c_rows). A batch row's candidates are spread over every shard, so each shard
+// COMPACTS the candidates it owns before scoring: per 64 ids one coalesced load, a ballot and a few
+// lane permutes; only owned candidates take a slot of the gather pipeline. Per-shard work is then
+// O(owned candidates) + O(ids), not O(all candidates).
+// ---------------------------------------------------------------------------------------------
+// position of the k-th (0-based) set bit of m (k < popcount(m))
+__device__ __forceinline__ int kth_set_bit(uint64_t m, int k) {
+    int pos = 0;
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+        const uint64_t low = m & ((1ull << s) - 1ull);
+        const int c = __popcll(low);
+        if (k >= c) {
+            k -= c;
+            m >>= s;
+            pos += s;
+        } else {
+            m = low;
+        }
+    }
+    return pos;
+}
+
+// value of `v` in lane `src` (every lane must execute this)
+__device__ __forceinline__ int lane_pull(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+
+// Walks candidates [lo, hi) of batch row b and calls body(row, n, cnt) with the owned ones compacted
+// into lanes 0..cnt-1 (row: local shard row, n: candidate column), in candidate order; every call but
+// the last has cnt = 64. With zero_out, a foreign candidate's score slot p.out[b, n] is written 0 (the
+// partial score block a SUM over shards assembles).
+template <class Body>
+__device__ __forceinline__ void for_owned_runs(const ScoreParams& p, int64_t b, int64_t lo, int64_t hi, int lane,
+                                               bool zero_out, Body&& body) {
+    int buf_row = 0, buf_n = 0, fill = 0;
+    for (int64_t c0 = lo; c0 < hi; c0 += kWave) {
+        const int64_t n = c0 + lane;
+        int64_t row = -1;
+        if (n < hi) row = (p.c_idx ? p.c_idx[b * p.c_stride + n] : b * p.c_dense + n) - p.c_base;
+        const bool own = n < hi && row >= 0 && row < p.c_rows;
+        if (zero_out && n < hi && !own) p.out[b * p.out_ld + n] = 0.f;
+        const uint64_t m = __ballot(own);
+        const int cnt = __popcll(m);
+        if (cnt == 0) continue;  // wave-uniform
+        const int row32 = (int)row, n32 = (int)n;
+        // lanes [fill, min(fill + cnt, 64)) take the first owned candidates of this chunk
+        const int d = lane - fill;
+        const bool take = d >= 0 && d < cnt;
+        const int src = kth_set_bit(m, take ? d : 0);
+        const int r1 = lane_pull(row32, src), n1 = lane_pull(n32, src);
+        if (take) {
+            buf_row = r1;
+            buf_n = n1;
+        }
+        if (fill + cnt >= kWave) {
+            body(buf_row, buf_n, kWave);
+            // the chunk's remaining owned candidates [64 - fill, cnt) move to lanes [0, fill + cnt - 64)
+            const int rest = fill + cnt - kWave;
+            const int src2 = kth_set_bit(m, lane < rest ? (kWave - fill) + lane : 0);
+            buf_row = lane_pull(row32, src2);
+            buf_n = lane_pull(n32, src2);
+            fill = rest;
+        } else {
+            fill += cnt;
+        }
+    }
+    if (fill > 0) body(buf_row, buf_n, fill);
+}
+
+// Scores the owned candidates of [lo, hi) of row b (foreign ones score 0 in p.out): kge_score_sharded.
+template <int FN, bool CH, int V, int G>
+__device__ __forceinline__ void score_owned(const ScoreParams& p, const Query<FN, CH, V, G>& q, int64_t b, int64_t lo,
+                                            int64_t hi, int lane) {
+    for_owned_runs(p, b, lo, hi, lane, true, [&](int row, int n, int cnt) {
+        const int64_t my_id = (int64_t)row + p.c_base;
+        float2 st;
+        const float s = score_lanes<FN, CH, V, G, false>(p, q, my_id, cnt, lane, st);
+        if (lane < cnt) p.out[b * p.out_ld + n] = s;
+    });
 }
 
 template <int FN, bool CH, int V, int G, bool ST = false>
@@ -469,7 +554,10 @@ __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
     int64_t qi, ri;
     bool qok, rok;
     build_query_for<FN, CH, V, G>(p, t.b, lane, q, qi, ri, qok, rok);
-    score_run<FN, CH, V, G, ST>(p, q, t.b, t.n0, t.nc, lane);
+    if (!ST && p.skip_foreign)
+        score_owned<FN, CH, V, G>(p, q, t.b, t.n0, t.n0 + t.nc, lane);  // runs of up to cpw (> 64) candidates
+    else
+        score_run<FN, CH, V, G, ST>(p, q, t.b, t.n0, t.nc, lane);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -126,6 +126,11 @@ SIGNATURES = {
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p],
     ),
+    "kge_shard_nq": (_c_i, [_c_i]),
+    "kge_shard_train_workspace_size": (_c_i64, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
+    "kge_shard_train_forward": (_c_i, [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p]),
+    "kge_shard_train_combine": (_c_i, [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p]),
+    "kge_shard_train_backward": (_c_i, [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_f, _c_f, _c_f, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_i, _c_p, _c_i64, _c_p]),
 }
 
 _lock = threading.Lock()

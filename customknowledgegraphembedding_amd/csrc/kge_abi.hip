@@ -306,6 +306,49 @@ __global__ __launch_bounds__(kBlock) void bwd_rel_kernel(const int64_t* __restri
 }
 
 // ---------------------------------------------------------------------------------------------
+// Combine (between the two collectives; one wave per global batch row b): the merged row state and
+// this shard's share of the negative slot's query gradient, scaled by the loss weight:
+//   TF (RED 2):     go f_r (A_r - T R B_r) / Z      detached (1): go f_r A_r / Z      mean (0): go A_r / N
+// Also the forward's outputs for every row: out_neg = R (the reduced negative branch), the positive's
+// raw score and logsigmoid. Every rank computes identical merged values (same inputs, same order).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void shard_combine_kernel(ScoreParams p) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    const RowMerge r = merge_row(p, b);
+    const float go = home_loss_weight(p, b, lane);
+    const bool mean = !p.adversarial;
+    const float R = mean ? r.Ln / (float)p.N : (r.Z > 0.f ? r.Ln / r.Z : 0.f);
+    float ca = 0.f, cb = 0.f;
+    if (mean) {
+        ca = go / (float)p.N;
+    } else if (r.Z > 0.f) {
+        ca = go * r.f_me / r.Z;
+        if (!p.detach) cb = -ca * (p.temperature * R);
+    }
+    const int64_t w = (int64_t)p.nq * p.D;
+    const float* A = p.sh_A + b * w;
+    const float* Bv = p.sh_B + b * w;
+    float* dq = p.sh_dq + b * w;
+    for (int64_t i = lane; i < w; i += kWave) {
+        float v = ca * A[i];
+        if (cb != 0.f) v += cb * Bv[i];
+        dq[i] = v;
+    }
+    if (lane == 0) {
+        float* m = p.sh_merged + b * 4;
+        m[0] = r.M;
+        m[1] = r.Z;
+        m[2] = R;
+        m[3] = r.pos;
+        p.out_neg[b] = R;
+        if (p.out_pos_raw) p.out_pos_raw[b] = r.pos;
+        p.out_pos_ls[b] = log_sigmoid(r.pos);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // host helpers
 // ---------------------------------------------------------------------------------------------
 thread_local std::string g_last_error;
@@ -407,11 +450,11 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         p.wpr = 1;
         waves = p.B;
     } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM || kind == KIND_STEP_FWD ||
-               kind == KIND_STEP_FWD_STATS || kind == KIND_STEP_FWD_GRAD) {
+               kind == KIND_STEP_FWD_STATS || kind == KIND_STEP_FWD_GRAD || kind == KIND_SHARD_FWD_GRAD) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
-    } else if (kind == KIND_BWD_CHAIN) {
+    } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS) {
         waves = p.B;  // one wave per slot
-    } else if (kind == KIND_STEP_EPILOGUE) {
+    } else if (kind == KIND_STEP_EPILOGUE || kind == KIND_SHARD_EPILOGUE) {
         // one wave per slot (negative rows, then positives), then one block for the loss
         waves = (2 * p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock + kWavesPerBlock;
     } else if (kind == KIND_BWD_ENT) {
@@ -427,12 +470,14 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     }
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > INT32_MAX) return fail(KGE_EINVAL, "problem too large for one launch");
-    const bool ch = (kind != KIND_FINISH) && mode == KGE_HEAD_BATCH;
+    const bool ch = (kind != KIND_FINISH && kind != KIND_SHARD_POS) && mode == KGE_HEAD_BATCH;
     if ((kind == KIND_BWD_ROWS || kind == KIND_BWD_ENT || kind == KIND_BWD_STREAM || kind == KIND_BWD_CHAIN ||
          kind == KIND_BWD_ENT_STREAM) &&
         G > kMaxG)
         return fail(KGE_ENOTSUP, "dimension too large");
-    if ((kind == KIND_STEP_FWD_GRAD || kind == KIND_STEP_EPILOGUE) && (G > kFwdGradMaxG || fn == KGE_PROTATE))
+    if ((kind == KIND_STEP_FWD_GRAD || kind == KIND_STEP_EPILOGUE || kind == KIND_SHARD_FWD_GRAD ||
+         kind == KIND_SHARD_POS || kind == KIND_SHARD_EPILOGUE) &&
+        (G > kFwdGradMaxG || fn == KGE_PROTATE))
         return fail(KGE_ENOTSUP, "the fused forward + query gradient needs D <= 1024 and no pRotatE");
     if ((kind == KIND_BWD_STREAM || kind == KIND_BWD_ENT_STREAM) && G % kWavesPerBlock)
         return fail(KGE_ENOTSUP, "the streaming backward needs G % 4 == 0");
@@ -1277,6 +1322,210 @@ int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld
     return step_backward_impl(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
                               D, gamma, emb_range, 0.f, temperature, adversarial, detach, t.ns, N, t.ps, t.d_out,
                               t.d_out, nullptr, d_rel, nullptr, nullptr, workspace, base, stream, &a, m_ent, v_ent, o);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Row-sharded train step (owner-computes; kge_shard.h): supervisor.py:15-26 over the
+// W replicas' batches, the entity table row-sharded over the W ranks, in three calls with the
+// caller's two collectives between them.
+// ---------------------------------------------------------------------------------------------
+struct ShardWs {
+    StepWs step;
+    float *d_rel, *ns, *A, *Bv, *merged;
+    int64_t base, bytes;
+};
+
+static ShardWs shard_ws_layout(char* ws, int fn, int64_t rows, int64_t R, int64_t rel_ld, int64_t Bg, int64_t N,
+                               int64_t D) {
+    ShardWs s;
+    s.step = step_ws_layout(ws, rows, Bg, N, D, ent_width(fn, D), rel_width(fn, D));
+    s.base = s.step.bytes;
+    int64_t o = kge_step_backward_adam_workspace_size(fn, rows, R, rel_ld, Bg, N, D);
+    s.d_rel = ws ? (float*)(ws + s.base) : nullptr;
+    auto take = [&](int64_t bytes) {
+        char* q = ws ? ws + o : nullptr;
+        o += align256(bytes);
+        return (float*)q;
+    };
+    const int64_t nqd = (int64_t)shard_nq(fn) * D;
+    s.ns = take(Bg * N * 4);
+    s.A = take(Bg * nqd * 4);
+    s.Bv = take(Bg * nqd * 4);
+    s.merged = take(Bg * 4 * 4);
+    s.bytes = o;
+    return s;
+}
+
+static int shard_check(int fn, int mode, const float* shard, int64_t rows, const float* qent, const float* qent_pos,
+                       const float* rel, const int64_t* pos, const int64_t* neg, int64_t Bg, int64_t N, int64_t D,
+                       int64_t home_B, int world, int rank, const float* weight, void* ws, int64_t ws_bytes) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (fn == KGE_PROTATE) return fail(KGE_ENOTSUP, "the sharded train step has no pRotatE modulus gradient");
+    if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "the sharded train step needs a negative mode (0 or 1)");
+    if (Bg <= 0 || N <= 0 || D <= 0 || rows < 0 || world < 1 || rank < 0 || rank >= world || home_B <= 0 ||
+        home_B * world != Bg)
+        return fail(KGE_EINVAL, "bad shape: need Bg = world * home_B > 0, N, D > 0, 0 <= rank < world");
+    if (!shard || !qent || !qent_pos || !rel || !pos || !neg || !weight) return fail(KGE_EINVAL, "null pointer");
+    if (Bg * N + 3 * Bg >= (int64_t)INT32_MAX || rows >= (int64_t)INT32_MAX)
+        return fail(KGE_EINVAL, "too many gradient events for 32-bit codes");
+    if (!ws || ws_bytes < shard_ws_layout(nullptr, fn, rows, 0, 0, Bg, N, D).bytes) return fail(KGE_EINVAL, "workspace too small");
+    return 0;
+}
+
+static void shard_params(ScoreParams& p, int fn, int mode, const float* shard, int64_t rows, int64_t ent_ld,
+                         int64_t shard_lo, const float* qent, const float* qent_pos, int64_t q_ld, const float* rel,
+                         int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                         int64_t neg_ld, int64_t Bg, int64_t N, int64_t D, int64_t home_B, int world, int rank,
+                         float gamma, float emb_range, float temperature, int adversarial, int detach,
+                         const float* weight, const ShardWs& w) {
+    fill_indexed(p, fn, mode, shard, rows, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, Bg, N, D, gamma,
+                 emb_range, 0.f);
+    p.qent = qent;  // row b: the negative call's query entity (assembled by the caller)
+    p.q_idx = nullptr;
+    p.q_ld = q_ld;
+    p.q_rows = Bg;
+    p.qent_pos = qent_pos;
+    p.c_base = shard_lo;
+    p.pos_base = pos;
+    p.temperature = temperature;
+    p.adversarial = adversarial;
+    p.detach = detach;
+    p.weight = weight;
+    p.home_B = home_B;
+    p.world = world;
+    p.rank = rank;
+    p.nq = shard_nq(fn);
+    p.out = w.ns;
+    p.out_ld = N;
+    p.neg_scores = w.ns;
+    p.ns_ld = N;
+    p.d_ns = w.step.d_ns;
+    p.d_ps = w.step.d_ps;
+    p.sh_A = w.A;
+    p.sh_B = w.Bv;
+    p.sh_merged = w.merged;
+}
+
+extern "C" {
+
+int kge_shard_nq(int fn) { return (fn < KGE_TRANSE || fn > KGE_PROTATE) ? 0 : shard_nq(fn); }
+
+int64_t kge_shard_train_workspace_size(int fn, int64_t shard_rows, int64_t nrelation, int64_t rel_ld, int64_t Bg,
+                                       int64_t N, int64_t D) {
+    if (fn < KGE_TRANSE || fn > KGE_PROTATE || shard_rows < 0 || nrelation < 0 || rel_ld < 0 || Bg < 0 || N < 0 ||
+        D <= 0)
+        return -1;
+    return shard_ws_layout(nullptr, fn, shard_rows, nrelation, rel_ld, Bg, N, D).bytes;
+}
+
+int kge_shard_train_forward(int fn, int mode, const float* shard, int64_t shard_rows, int64_t ent_ld, int64_t shard_lo,
+                            const float* qent, const float* qent_pos, int64_t q_ld, const float* rel, int64_t nrelation,
+                            int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                            int64_t Bg, int64_t N, int64_t D, int64_t home_B, int world, int rank, float gamma,
+                            float emb_range, float temperature, int adversarial, int detach, const float* weight,
+                            float* stats, float* dq, void* workspace, int64_t workspace_bytes, void* stream) {
+    int rc = shard_check(fn, mode, shard, shard_rows, qent, qent_pos, rel, pos, neg, Bg, N, D, home_B, world, rank,
+                         weight, workspace, workspace_bytes);
+    if (rc) return rc;
+    if (!stats || !dq) return fail(KGE_EINVAL, "null pointer");
+    const ShardWs w = shard_ws_layout((char*)workspace, fn, shard_rows, nrelation, rel_ld, Bg, N, D);
+    if (workspace_bytes < w.bytes) return fail(KGE_EINVAL, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    // per-call state only: the local rows' event counters are zeroed here
+    if (shard_rows > 0 && hipMemsetAsync(w.step.count, 0, (size_t)(shard_rows * 4), st) != hipSuccess)
+        return check_launch("kge_shard_train_forward memset");
+    ScoreParams p;
+    shard_params(p, fn, mode, shard, shard_rows, ent_ld, shard_lo, qent, qent_pos, q_ld, rel, nrelation, rel_ld,
+                 rel_off, pos, neg, neg_ld, Bg, N, D, home_B, world, rank, gamma, emb_range, temperature, adversarial,
+                 detach, weight, w);
+    p.ev_count = w.step.count;
+    p.sh_stats = stats;
+    p.sh_dq = dq;
+    rc = run_score(fn, mode, p, KIND_SHARD_FWD_GRAD, stream);
+    if (rc) return rc;
+    p.ev_count = nullptr;
+    return run_score(fn, KGE_TAIL_BATCH, p, KIND_SHARD_POS, stream);  // owned positives (tail formula)
+}
+
+int kge_shard_train_combine(int fn, int mode, const float* shard, int64_t shard_rows, int64_t ent_ld, int64_t shard_lo,
+                            const float* qent, const float* qent_pos, int64_t q_ld, const float* rel, int64_t nrelation,
+                            int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                            int64_t Bg, int64_t N, int64_t D, int64_t home_B, int world, int rank, float gamma,
+                            float emb_range, float temperature, int adversarial, int detach, const float* weight,
+                            const float* stats_all, float* dq, float* out_neg, float* out_pos_raw, float* out_pos,
+                            void* workspace, int64_t workspace_bytes, void* stream) {
+    int rc = shard_check(fn, mode, shard, shard_rows, qent, qent_pos, rel, pos, neg, Bg, N, D, home_B, world, rank,
+                         weight, workspace, workspace_bytes);
+    if (rc) return rc;
+    if (!stats_all || !dq || !out_neg || !out_pos) return fail(KGE_EINVAL, "null pointer");
+    const ShardWs w = shard_ws_layout((char*)workspace, fn, shard_rows, nrelation, rel_ld, Bg, N, D);
+    if (workspace_bytes < w.bytes) return fail(KGE_EINVAL, "workspace too small");
+    ScoreParams p;
+    shard_params(p, fn, mode, shard, shard_rows, ent_ld, shard_lo, qent, qent_pos, q_ld, rel, nrelation, rel_ld,
+                 rel_off, pos, neg, neg_ld, Bg, N, D, home_B, world, rank, gamma, emb_range, temperature, adversarial,
+                 detach, weight, w);
+    p.sh_stats_all = stats_all;
+    p.sh_dq = dq;
+    p.out_neg = out_neg;
+    p.out_pos_raw = out_pos_raw;
+    p.out_pos_ls = out_pos;
+    const int64_t blocks = (Bg + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(shard_combine_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, p);
+    return check_launch("kge_shard_train_combine");
+}
+
+int kge_shard_train_backward(int fn, int mode, float* shard, int64_t shard_rows, int64_t ent_ld, int64_t shard_lo,
+                             const float* qent, const float* qent_pos, int64_t q_ld, float* rel, int64_t nrelation,
+                             int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                             int64_t Bg, int64_t N, int64_t D, int64_t home_B, int world, int rank, float gamma,
+                             float emb_range, float temperature, int adversarial, int detach, const float* weight,
+                             const float* dq, float* loss, float* loss_sum, float* m_ent, float* v_ent, float* m_rel,
+                             float* v_rel, float lr, float beta1, float beta2, float eps, int64_t step, int keras,
+                             void* workspace, int64_t workspace_bytes, void* stream) {
+    int rc = shard_check(fn, mode, shard, shard_rows, qent, qent_pos, rel, pos, neg, Bg, N, D, home_B, world, rank,
+                         weight, workspace, workspace_bytes);
+    if (rc) return rc;
+    if (step < 1) return fail(KGE_EINVAL, "step is 1-based");
+    if (!dq || !loss || !m_ent || !v_ent || !m_rel || !v_rel) return fail(KGE_EINVAL, "null pointer");
+    const ShardWs w = shard_ws_layout((char*)workspace, fn, shard_rows, nrelation, rel_ld, Bg, N, D);
+    if (workspace_bytes < w.bytes) return fail(KGE_EINVAL, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    // bucket offsets of the owned rows' events (counted by the forward)
+    if (shard_rows > 0)
+        hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.step.count, shard_rows, w.step.off,
+                           w.step.cursor, 0, (int)(Bg * N + 3 * Bg));
+    rc = check_launch("kge_shard_train_backward scan");
+    if (rc) return rc;
+    ScoreParams e;
+    shard_params(e, fn, mode, shard, shard_rows, ent_ld, shard_lo, qent, qent_pos, q_ld, rel, nrelation, rel_ld,
+                 rel_off, pos, neg, neg_ld, Bg, N, D, home_B, world, rank, gamma, emb_range, temperature, adversarial,
+                 detach, weight, w);
+    e.sh_dq = const_cast<float*>(dq);
+    e.qbuf = w.step.qbuf;
+    e.qg_ent = w.step.qg_ent;
+    e.qg_rel = w.step.qg_rel;
+    e.ent_w = ent_width(fn, D);
+    e.rel_w = rel_width(fn, D);
+    e.loss = loss;
+    e.loss_sum = loss_sum;
+    e.ev_cursor = w.step.cursor;
+    e.ev_code_w = w.step.code;
+    rc = run_score(fn, mode, e, KIND_SHARD_EPILOGUE, stream);
+    if (rc) return rc;
+    // phase 2 with Adam fused into the shard's rows, relation gradient with Adam (supervisor.py:25-26)
+    const AdamArgs a = adam_args(lr, beta1, beta2, eps, step, keras);
+    StepOpts o;
+    o.dq_ready = o.epilogue_done = o.events_ready = true;
+    o.rel_p = rel;
+    o.rel_m = m_rel;
+    o.rel_v = v_rel;
+    return step_backward_impl(fn, mode, shard, shard_rows, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld,
+                              Bg, N, D, gamma, emb_range, 0.f, temperature, adversarial, detach, w.ns, N, w.ns,
+                              w.step.d_ps, w.step.d_ps, nullptr, w.d_rel, nullptr, nullptr, workspace, w.base, stream,
+                              &a, m_ent, v_ent, o);
 }
 
 }  // extern "C"

@@ -2153,12 +2153,20 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
     }
 }
 
+}  // namespace kge_impl
+
+#include "kge_shard.h"
+
+namespace kge_impl {
+
 // ---------------------------------------------------------------------------------------------
 // dispatch over (kind, candidate side, vector width, groups per lane) for one score function
 // ---------------------------------------------------------------------------------------------
 template <int FN, bool CH, int V, int G>
 void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
-    if (kind == KIND_BWD)
+    if (kind == KIND_SHARD_FWD_GRAD || kind == KIND_SHARD_POS || kind == KIND_SHARD_EPILOGUE)
+        launch_shard<FN, CH, V, G>(p, kind, st, blocks);
+    else if (kind == KIND_BWD)
         hipLaunchKernelGGL((score_bwd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_BWD_ROWS)
         hipLaunchKernelGGL((bwd_rows_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);

@@ -28,7 +28,14 @@ enum Kind {
     KIND_BWD_ENT_STREAM = 10,  // phase 2, column-group streaming (one block per entity row)
     KIND_STEP_FWD_GRAD = 11,   // train-step forward with phase 1 fused (kge_train_step)
     KIND_STEP_EPILOGUE = 12,   // kge_train_step: loss weights, score gradients, chains, loss (one wave per slot)
+    KIND_SHARD_FWD_GRAD = 13,  // row-sharded train step: owned candidates' scores + partial softmax state
+    KIND_SHARD_POS = 14,       // row-sharded train step: owned positives (score, gradient, query gradient)
+    KIND_SHARD_EPILOGUE = 15,  // row-sharded train step: owned score gradients, every slot's chain, loss
 };
+// query operands a score function's gradient has (q0 always; q1 for the complex / split forms; q2 InterHT)
+constexpr int shard_nq(int fn) {
+    return fn == KGE_INTERHT ? 3 : ((fn == KGE_COMPLEX || fn == KGE_ROTATE) ? 2 : 1);
+}
 constexpr int kFwdGradMaxG = 4;  // the fused forward + query gradient keeps 6 accumulators per element
 
 // Parameters of one scoring launch. Rows are addressed as base + row * ld (floats).
@@ -98,6 +105,17 @@ struct ScoreParams {
     const float* d_ps;    // [Bn] dL/d(positive score)
     int64_t Bn, Nn;       // negative batch rows and candidates per row
     float* d_out_ent;     // [E, c_ld] entity gradient table, fully overwritten by phase 2
+    // row-sharded train step (kge_shard_train_*; kge_shard.h). Batch rows are GLOBAL: [0, B) over all
+    // W home ranks, home h owning rows [h * home_B, (h + 1) * home_B).
+    const float* qent_pos;      // [B, q_ld] the positive call's query rows (h), assembled by the caller
+    float* sh_stats;            // [B, 4] this shard's partial (M, Z, Ln, positive score)
+    const float* sh_stats_all;  // [world, B, 4] every shard's partial stats (all-gathered)
+    float* sh_dq;               // [2 B, nq D] this shard's share of each slot's query gradient (SUM-reduced)
+    float* sh_A;                // [B, nq D] online-softmax query-gradient sums of the owned candidates
+    float* sh_B;                // [B, nq D] (TF semantics only: the softmax term)
+    float* sh_merged;           // [B, 4] merged (M, Z, R, positive score): identical on every shard
+    int64_t home_B;
+    int world, rank, nq;
     // fused optimizer in phase 2 (kge_step_backward_adam): row e of the table is updated in place
     struct {
         float* m;   // [E, c_ld] first moment

@@ -89,6 +89,134 @@ class HipShardKernels:
     def log_sigmoid(x):
         return ops.log_sigmoid_raw(x)
 
+    # ---- row-sharded train step (kge_shard_train_*; include/kge_hip.h) ----
+    @staticmethod
+    def train_alloc(sk, Bg, N):
+        lib = _lib.load()
+        rel = sk.relation_embedding
+        nbytes = lib.kge_shard_train_workspace_size(sk.fn, sk.shard.shape[0], rel.shape[0], rel.stride(0), Bg, N, sk.D)
+        if nbytes < 0:
+            raise ValueError("bad shape for the sharded train step")
+        dev = sk.device
+        nq = lib.kge_shard_nq(sk.fn)
+        f32 = dict(dtype=torch.float32, device=dev)
+        return {"ws": torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev),
+                "stats": torch.empty((Bg, 4), **f32), "dq": torch.empty((2 * Bg, nq * sk.D), **f32),
+                "out_neg": torch.empty(Bg, **f32), "out_pos_raw": torch.empty(Bg, **f32),
+                "out_pos": torch.empty(Bg, **f32), "loss": torch.empty(sk.world, **f32)}
+
+    @staticmethod
+    def _prefix(sk, bufs, mode, qent, qent_pos, pos, neg, w):
+        rel = sk.relation_embedding
+        Bg, N = neg.shape
+        return (sk.fn, mode, sk.shard.data_ptr(), sk.shard.shape[0], sk.shard.stride(0), sk.lo, qent.data_ptr(),
+                qent_pos.data_ptr(), qent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), sk.rel_off,
+                pos.data_ptr(), neg.data_ptr(), neg.stride(0), Bg, N, sk.D, Bg // sk.world, sk.world, sk.rank,
+                float(sk.gamma), float(sk.emb_range), float(sk.temperature), int(sk.adversarial), int(sk.detach),
+                w.data_ptr())
+
+    @classmethod
+    def train_forward(cls, sk, bufs, mode, qent, qent_pos, pos, neg, w):
+        st = torch.cuda.current_stream(sk.device).cuda_stream
+        rc = _lib.load().kge_shard_train_forward(*cls._prefix(sk, bufs, mode, qent, qent_pos, pos, neg, w),
+                                                 bufs["stats"].data_ptr(), bufs["dq"].data_ptr(), bufs["ws"].data_ptr(),
+                                                 bufs["ws"].numel(), st)
+        check(rc, "kge_shard_train_forward")
+
+    @classmethod
+    def train_combine(cls, sk, bufs, mode, qent, qent_pos, pos, neg, w, stats_all):
+        st = torch.cuda.current_stream(sk.device).cuda_stream
+        rc = _lib.load().kge_shard_train_combine(*cls._prefix(sk, bufs, mode, qent, qent_pos, pos, neg, w),
+                                                 stats_all.data_ptr(), bufs["dq"].data_ptr(),
+                                                 bufs["out_neg"].data_ptr(), bufs["out_pos_raw"].data_ptr(),
+                                                 bufs["out_pos"].data_ptr(), bufs["ws"].data_ptr(), bufs["ws"].numel(),
+                                                 st)
+        check(rc, "kge_shard_train_combine")
+
+    @classmethod
+    def train_backward(cls, sk, bufs, mode, qent, qent_pos, pos, neg, w, step, loss_sum):
+        st = torch.cuda.current_stream(sk.device).cuda_stream
+        a = sk.adam
+        rc = _lib.load().kge_shard_train_backward(
+            *cls._prefix(sk, bufs, mode, qent, qent_pos, pos, neg, w), bufs["dq"].data_ptr(),
+            bufs["loss"].data_ptr(), None if loss_sum is None else loss_sum.data_ptr(), a["m_ent"].data_ptr(),
+            a["v_ent"].data_ptr(), a["m_rel"].data_ptr(), a["v_rel"].data_ptr(), float(a["lr"]), float(a["b1"]),
+            float(a["b2"]), float(a["eps"]), int(step), int(a["keras"]), bufs["ws"].data_ptr(), bufs["ws"].numel(), st)
+        check(rc, "kge_shard_train_backward")
+        return bufs["loss"]
+
+
+class TorchComm:
+    """Collectives of the sharded step over torch.distributed (RCCL on ROCm, gloo on CPU)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def all_gather_cat(self, t):
+        """[W, *t.shape], rank-major."""
+        W = dist.get_world_size(self.group)
+        out = torch.empty((W,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if t.is_cuda:
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        else:
+            dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
+        return out
+
+    def all_reduce_sum_(self, t):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+
+class ThreadComm:
+    """The same collectives between W threads of ONE process (one Python thread per simulated rank,
+    all on one device and stream): used to run the W-rank sharded step on a single GPU. Sums are
+    taken in rank order, as RCCL's result is the same on every rank."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self._barrier = threading.Barrier(world, timeout=120)  # a failed rank breaks it instead of hanging
+        self._slots = [None] * world
+
+    def _exchange(self, rank, t):
+        self._slots[rank] = t
+        self._barrier.wait()
+        got = list(self._slots)
+        self._barrier.wait()
+        return got
+
+    def all_gather_cat(self, t, rank):
+        return torch.stack(self._exchange(rank, t.contiguous()))
+
+    def all_reduce_sum_(self, t, rank):
+        parts = self._exchange(rank, t.clone())
+        acc = parts[0].clone()
+        for x in parts[1:]:
+            acc += x
+        t.copy_(acc)
+        return t
+
+
+def run_threads(fns):
+    """Runs fns[r]() on one thread per simulated rank; returns their results (re-raises the first error)."""
+    import threading
+    res, err = [None] * len(fns), []
+
+    def go(r):
+        try:
+            res[r] = fns[r]()
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+
+    th = [threading.Thread(target=go, args=(r,)) for r in range(len(fns))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if err:
+        raise err[0]
+    return res
+
 
 def _reduce_scatter_rows(full, world, rank, group):
     """SUM over ranks of `full` [W*B, C], returning this rank's [B, C] block. RCCL has a native
@@ -122,12 +250,18 @@ class ShardedKGE:
 
     def __init__(self, model_name, nentity, nrelation, hidden_dim, gamma, double_entity_embedding=False,
                  double_relation_embedding=False, triple_relation_embedding=False, device=None, seed=0,
-                 group=None, kernels=None, full_tables=None):
+                 group=None, kernels=None, full_tables=None, world=None, rank=None, comm=None):
+        """world / rank / comm override torch.distributed: a ThreadComm runs W simulated ranks as
+        threads of one process (single-GPU tests and measurements of the sharded step)."""
         from .model import TFKGEModel
 
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if world is None:
+            self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+            self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        else:
+            self.world, self.rank = int(world), int(rank)
+        self.comm = comm if comm is not None else (TorchComm(group) if self.world > 1 else None)
         self.kernels = kernels or HipShardKernels()
         self.model_name = model_name
         self.fn = FN_IDS[model_name]
@@ -147,6 +281,75 @@ class ShardedKGE:
         self.shard = ent[self.lo:self.hi].contiguous().to(dev)
         self.relation_embedding = rel.contiguous().to(dev)  # replicated (R rows)
         self.device = torch.device(dev)
+        # train-step options (supervisor.py:15-26 TF semantics by default: self-adversarial, T = 1,
+        # softmax not detached; Keras Adam) and state
+        self.temperature, self.adversarial, self.detach = 1.0, True, False
+        self.adam = None
+        self.step = 0
+        self.loss_sum = None
+        self._bufs = {}
+
+    def configure_optimizer(self, lr=5e-5, betas=(0.9, 0.999), eps=None, semantics="keras"):
+        """Adam over this rank's shard and the replicated relation table (supervisor.py:26; run.py:111
+        Keras Adam by default). Every rank applies the same relation update, so the replicas stay equal."""
+        if eps is None:
+            eps = 1e-7 if semantics == "keras" else 1e-8
+        self.adam = {"m_ent": torch.zeros_like(self.shard), "v_ent": torch.zeros_like(self.shard),
+                     "m_rel": torch.zeros_like(self.relation_embedding),
+                     "v_rel": torch.zeros_like(self.relation_embedding),
+                     "lr": lr, "b1": betas[0], "b2": betas[1], "eps": eps, "keras": semantics == "keras"}
+        self.step = 0
+        return self
+
+    def _coll(self, name, t):
+        if self.world == 1:
+            return t.unsqueeze(0) if name == "gather" else t
+        if isinstance(self.comm, ThreadComm):
+            return self.comm.all_gather_cat(t, self.rank) if name == "gather" else self.comm.all_reduce_sum_(t, self.rank)
+        return self.comm.all_gather_cat(t) if name == "gather" else self.comm.all_reduce_sum_(t)
+
+    def assemble_queries(self, pos_g, mode):
+        """The query-entity rows of every global batch row: (qent [Bg, ent_dim] = E[pos[:, 2 if head
+        else 0]], qent_pos [Bg, ent_dim] = E[pos[:, 0]]): owners gather their rows, one SUM all-reduce."""
+        Bg = pos_g.shape[0]
+        cols = [2, 0] if mode == HEAD_BATCH else [0]
+        rows = torch.empty((len(cols), Bg, self.entity_dim), dtype=torch.float32, device=self.device)
+        for i, c in enumerate(cols):
+            self.kernels.gather_rows(self.shard, self.lo, pos_g[:, c:], 3, Bg, rows[i])
+        rows = self._coll("sum", rows)
+        return rows[0], rows[-1]
+
+    def train_step(self, pos_g, neg_g, weight_g, mode):
+        """One row-sharded train step (supervisor.py:15-26 over the W replicas' batches, SUM gradient
+        aggregation): pos_g [Bg, 3], neg_g [Bg, N], weight_g [Bg] — the global batch (home rank h's
+        replica batch is rows [h Bg/W, (h+1) Bg/W)), identical on every rank. Updates this rank's
+        shard and the relation table in place; returns this rank's replica loss (0-dim tensor).
+        Collectives per step: one SUM all-reduce of the query rows, one all-gather of [Bg, 4] row
+        statistics, one SUM all-reduce of the [2 Bg, nq D] query gradients."""
+        if self.adam is None:
+            self.configure_optimizer()
+        mode = ops.mode_id(mode)
+        if mode not in (HEAD_BATCH, TAIL_BATCH):
+            raise ValueError("train_step needs a negative mode (0 or 1)")
+        Bg, N = neg_g.shape
+        if Bg % self.world:
+            raise ValueError("global batch must split evenly over ranks")
+        w = weight_g.reshape(-1).to(torch.float32).contiguous()
+        k = self.kernels
+        key = (Bg, N)
+        if key not in self._bufs:
+            self._bufs = {key: k.train_alloc(self, Bg, N)}
+        bufs = self._bufs[key]
+        if self.loss_sum is None:
+            self.loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
+        qent, qent_pos = self.assemble_queries(pos_g, mode)
+        k.train_forward(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w)
+        stats_all = self._coll("gather", bufs["stats"])
+        k.train_combine(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w, stats_all)
+        self._coll("sum", bufs["dq"])
+        loss = k.train_backward(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w, self.step + 1, self.loss_sum)
+        self.step += 1
+        return loss[self.rank]
 
     def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None):
         """pos_g [W*B, 3], neg_g [W*B, N] (the global batch, identical on every rank) ->

@@ -298,6 +298,57 @@ int kge_train_step(int fn, int mode,
                    void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
+ * Row-sharded train step (owner-computes): supervisor.py:15-26 (`train_step_fn`) over the
+ * batches of W replicas (tf.distribute: each replica's loss on its own batch, gradients SUM-aggregated
+ * by `apply_gradients`, metric += loss * num_replicas_in_sync), with the ENTITY TABLE ROW-SHARDED over
+ * the W ranks instead of replicated. Rank r holds rows [shard_lo, shard_lo + shard_rows) (ent_ld
+ * stride; updated in place, with its Adam moments m_ent / v_ent), the replicated relation table (every
+ * rank applies the identical relation update), and the GLOBAL batch of Bg = W * home_B rows (pos [Bg,3],
+ * neg [Bg,N], weight [Bg]; home rank h's replica batch is rows [h home_B, (h+1) home_B)), identical on
+ * every rank. Candidate rows never leave their owner. Three calls, with the caller's collectives between:
+ *   kge_shard_train_forward   owned candidates: scores, per-row partial softmax state -> stats [Bg*4];
+ *                             owned positives' query gradients -> dq rows [Bg, 2Bg)
+ *   (caller) all-gather stats -> stats_all [W*Bg*4] (rank-major)
+ *   kge_shard_train_combine   merged row state; this rank's share of each negative slot's query
+ *                             gradient -> dq rows [0, Bg); out_neg [Bg] (reduced negative branch),
+ *                             out_pos_raw / out_pos [Bg] (positive score, logsigmoid)
+ *   (caller) SUM all-reduce of dq [2*Bg*nq*D floats], nq = kge_shard_nq(fn)
+ *   kge_shard_train_backward  owned score gradients, every slot's query chain, deterministic phase 2
+ *                             with Adam on the shard, relation gradient with Adam; loss [W] (each
+ *                             replica's loss), *loss_sum += W * sum(loss) (may be NULL)
+ * qent [Bg, q_ld]: row b = entity row pos[b, mode == head ? 2 : 0]; qent_pos [Bg, q_ld]: row b = entity
+ * row pos[b, 0] (the same buffer in tail-batch mode) — e.g. kge_gather_rows on every shard + SUM all-reduce.
+ * The same argument prefix goes to all three calls; workspace (kge_shard_train_workspace_size bytes)
+ * carries the step from forward to backward (no state between steps). Deterministic for a fixed W.
+ * Out-of-range ids have no owner: they are dropped (the unsharded path scores them on a zero row).
+ * D <= 1024 (per half), no pRotatE (KGE_ENOTSUP).
+ */
+int kge_shard_nq(int fn);
+int64_t kge_shard_train_workspace_size(int fn, int64_t shard_rows, int64_t nrelation, int64_t rel_ld, int64_t Bg,
+                                       int64_t N, int64_t D);
+int kge_shard_train_forward(int fn, int mode, const float* shard, int64_t shard_rows, int64_t ent_ld, int64_t shard_lo,
+                            const float* qent, const float* qent_pos, int64_t q_ld, const float* rel, int64_t nrelation,
+                            int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                            int64_t Bg, int64_t N, int64_t D, int64_t home_B, int world, int rank, float gamma,
+                            float emb_range, float temperature, int adversarial, int detach, const float* weight,
+                            float* stats, float* dq, void* workspace, int64_t workspace_bytes, void* stream);
+int kge_shard_train_combine(int fn, int mode, const float* shard, int64_t shard_rows, int64_t ent_ld, int64_t shard_lo,
+                            const float* qent, const float* qent_pos, int64_t q_ld, const float* rel, int64_t nrelation,
+                            int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                            int64_t Bg, int64_t N, int64_t D, int64_t home_B, int world, int rank, float gamma,
+                            float emb_range, float temperature, int adversarial, int detach, const float* weight,
+                            const float* stats_all, float* dq, float* out_neg, float* out_pos_raw, float* out_pos,
+                            void* workspace, int64_t workspace_bytes, void* stream);
+int kge_shard_train_backward(int fn, int mode, float* shard, int64_t shard_rows, int64_t ent_ld, int64_t shard_lo,
+                             const float* qent, const float* qent_pos, int64_t q_ld, float* rel, int64_t nrelation,
+                             int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld,
+                             int64_t Bg, int64_t N, int64_t D, int64_t home_B, int world, int rank, float gamma,
+                             float emb_range, float temperature, int adversarial, int detach, const float* weight,
+                             const float* dq, float* loss, float* loss_sum, float* m_ent, float* v_ent, float* m_rel,
+                             float* v_rel, float lr, float beta1, float beta2, float eps, int64_t step, int keras,
+                             void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
  * TranSparse scores (tensorflow_codes/model.py:226-235, gathers at :139-142, :161-164, :187-190; tables
  * :96-106) on the fp32 matrix cores. W and mask are [nrel, d, d] row-major contiguous; the score reads the
  * whole relation row (d floats, rel_ld stride) and needs entity_dim == relation_dim == d.

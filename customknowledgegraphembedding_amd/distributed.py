@@ -289,6 +289,31 @@ class ShardedKGE:
         self.loss_sum = None
         self._bufs = {}
 
+    @classmethod
+    def from_model(cls, model, group=None, kernels=None, world=None, rank=None, comm=None):
+        """A sharded view of an existing TFKGEModel / KGEModel: this rank's shard IS rows [lo, hi) of the
+        model's entity table (a view: updates land in the model's own storage) and the relation table
+        is the model's (updated identically on every rank). Rows outside the shard go stale during
+        training until `sync_entity_table` re-broadcasts every rank's block."""
+        ent = model.entity_embedding.data
+        rel = model.relation_embedding.data
+        modulus = float(model.modulus.reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0
+        return cls(model.model_name, model.nentity, model.nrelation, model.hidden_dim, model._gamma_f,
+                   device=ent.device, group=group, kernels=kernels, world=world, rank=rank, comm=comm,
+                   full_tables=(ent, rel, model._gamma_f, model._range_f, modulus))
+
+    def sync_entity_table(self, table):
+        """Every rank's block of rows -> `table` [E, ent_dim] on every rank (one broadcast per rank)."""
+        if self.world == 1:
+            return table
+        for r in range(self.world):
+            lo, hi = shard_bounds(self.nentity, self.world, r)
+            blk = table[lo:hi]
+            if r == self.rank and blk.data_ptr() != self.shard.data_ptr():
+                blk.copy_(self.shard)
+            dist.broadcast(blk, src=r, group=self.group)
+        return table
+
     def configure_optimizer(self, lr=5e-5, betas=(0.9, 0.999), eps=None, semantics="keras"):
         """Adam over this rank's shard and the replicated relation table (supervisor.py:26; run.py:111
         Keras Adam by default). Every rank applies the same relation update, so the replicas stay equal."""
@@ -349,6 +374,7 @@ class ShardedKGE:
         self._coll("sum", bufs["dq"])
         loss = k.train_backward(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w, self.step + 1, self.loss_sum)
         self.step += 1
+        self.last_losses = loss  # every replica's loss [W] (identical on every rank)
         return loss[self.rank]
 
     def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None):

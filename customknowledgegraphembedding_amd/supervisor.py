@@ -6,10 +6,13 @@ as one fused `TFKGEModel.step_forward` (2 HIP launches), the loss is supervisor.
 backward runs the HIP backward kernels, and the optimizer (customknowledgegraphembedding_amd.optim.Adam)
 runs the HIP Adam kernel.
 
-Multi-replica (torch.distributed, one process per GPU): the dense table gradients are summed across
-ranks with all-reduce before the optimizer step, as tf.distribute aggregates replica gradients with
-SUM in `apply_gradients` (supervisor.py:26); `metrics` receives `loss * num_replicas_in_sync`
-(supervisor.py:28).
+Multi-replica (torch.distributed, one process per GPU): the step is the same math as tf.distribute's
+(supervisor.py:26-28): each replica's loss on its own batch, the replicas' gradients SUM-aggregated
+by `apply_gradients`, `metrics` += loss * num_replicas_in_sync. With the fused optimizer the entity
+table is ROW-SHARDED over the replicas for the step (distributed.ShardedKGE.train_step: owner-computes,
+each rank updates its block of rows in place, collectives of O(batch) size instead of a dense
+all-reduce of the whole table's gradient); the replicas' batches are all-gathered (ids and weights).
+Otherwise the dense table gradients are summed with all-reduce before the optimizer step.
 """
 from __future__ import annotations
 
@@ -77,25 +80,33 @@ class Sum:
 class Trainer:
     """supervisor.py:5-58."""
 
-    def __init__(self, strategy, dataloader, model, optimizer, metrics, fused=None):
+    def __init__(self, strategy, dataloader, model, optimizer, metrics, fused=None, shard_kernels=None):
         self.dataloader = dataloader
         self.model = model
         self.optimizer = optimizer
         self.metrics = metrics
         self.strategy = strategy
+        replicas = strategy.num_replicas_in_sync
         if fused is None:
-            # the fused optimizer never materialises gradients, so it needs a single replica and
-            # this package's Adam over exactly the model's parameters in one group
+            # the fused optimizer never materialises gradients: it needs this package's Adam over
+            # exactly the model's parameters in one group (and, across replicas, no pRotatE modulus)
             from .optim import Adam
-            fused = (isinstance(optimizer, Adam) and strategy.num_replicas_in_sync == 1
+            fused = (isinstance(optimizer, Adam)
                      and hasattr(model, "train_step_fused") and getattr(model, "supports_fused_step", False)
                      and len(optimizer.param_groups) == 1
                      and {id(p) for p in optimizer.param_groups[0]["params"] if p.requires_grad}
-                     == {id(p) for p in model.parameters() if p.requires_grad})
+                     == {id(p) for p in model.parameters() if p.requires_grad}
+                     and (replicas == 1 or model.model_name != "pRotatE"))
         # fused="split": the three-call form (kge_step_forward, kge_step_loss, kge_step_backward_adam),
         # bitwise equal to the autograd path; otherwise the single kge_train_step call
         self.one_call = fused != "split"
         self.fused = bool(fused)
+        self.sharded = None
+        if self.fused and replicas > 1:
+            if fused == "split":
+                raise ValueError("fused='split' is single-replica only")
+            from .distributed import ShardedKGE
+            self.sharded = ShardedKGE.from_model(model, kernels=shard_kernels)
 
     def loss(self, positive_sample, negative_sample, subsampling_weight, mode):
         """supervisor.py:17-23 — both calls fused, then the weighted loss (one HIP launch each)."""
@@ -113,6 +124,8 @@ class Trainer:
             negative_sample = negative_sample.to(dev, non_blocking=True)
             subsampling_weight = subsampling_weight.to(dev, non_blocking=True)
             mode = mode.cpu() if torch.is_tensor(mode) else mode
+            if self.sharded is not None:
+                return self._sharded_step(positive_sample, negative_sample, subsampling_weight, mode)
             if self.fused:
                 # forward + loss + deterministic backward with Adam fused into the entity pass
                 acc = (self.metrics.accumulator(dev) if self.one_call and hasattr(self.metrics, "accumulator")
@@ -131,6 +144,49 @@ class Trainer:
             return loss
 
         return self.strategy.run(train_step_fn, next(data_iter))
+
+    def _sharded_step(self, pos, neg, w, mode):
+        """supervisor.py:15-28 across the replicas with the entity table row-sharded: the replicas'
+        batches are all-gathered (every replica must be in the same negative mode this step), then
+        ShardedKGE.train_step (Keras/torch Adam from this optimizer's group, in place on the model)."""
+        from . import ops
+        from .optim import resolve_lr
+
+        sk = self.sharded
+        comm = sk.comm
+        m0 = ops.mode_id(int(mode[0]) if torch.is_tensor(mode) or isinstance(mode, (list, tuple)) else mode)
+        modes = comm.all_gather_cat(torch.tensor([m0], dtype=torch.int64, device=pos.device)).reshape(-1)
+        if bool((modes != modes[0]).any()):
+            raise ValueError(f"replicas are in different negative modes this step: {modes.tolist()}")
+        pos_g = comm.all_gather_cat(pos.contiguous()).reshape(-1, 3)
+        neg_g = comm.all_gather_cat(neg.contiguous())
+        neg_g = neg_g.reshape(-1, neg_g.shape[-1])
+        w_g = comm.all_gather_cat(w.reshape(-1).to(torch.float32).contiguous()).reshape(-1)
+        ent, rel = self.model.entity_embedding, self.model.relation_embedding
+        group = self.optimizer.param_groups[0]
+        for prm in (ent, rel):
+            st = self.optimizer.state[prm]
+            if not st:
+                st["step"] = 0
+                st["exp_avg"] = torch.zeros_like(prm)
+                st["exp_avg_sq"] = torch.zeros_like(prm)
+        st_e, st_r = self.optimizer.state[ent], self.optimizer.state[rel]
+        sk.adam = {"m_ent": st_e["exp_avg"][sk.lo:sk.hi], "v_ent": st_e["exp_avg_sq"][sk.lo:sk.hi],
+                   "m_rel": st_r["exp_avg"], "v_rel": st_r["exp_avg_sq"],
+                   "lr": resolve_lr(group["lr"], st_e["step"]), "b1": group["betas"][0], "b2": group["betas"][1],
+                   "eps": group["eps"], "keras": group["semantics"] == "keras"}
+        sk.step = st_e["step"]
+        loss = sk.train_step(pos_g, neg_g, w_g, m0)
+        st_e["step"] += 1
+        st_r["step"] += 1
+        # supervisor.py:28: every replica adds loss * num_replicas_in_sync to the (cross-replica SUM) metric
+        self.metrics.update_state(sk.last_losses.sum() * self.strategy.num_replicas_in_sync)
+        return loss
+
+    def sync_model(self):
+        """After sharded training: every rank's block of entity rows back into the model's table."""
+        if self.sharded is not None:
+            self.sharded.sync_entity_table(self.model.entity_embedding.data)
 
     def training(self, steps_per_tpu_call, epochs, steps_per_epoch):
         """supervisor.py:32-58. Reproduces the reference loop, including its step accounting
@@ -152,4 +208,5 @@ class Trainer:
             self.metrics.reset_states()
             if epoch >= epochs:
                 break
+        self.sync_model()
         print("DONE")

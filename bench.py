@@ -69,11 +69,11 @@ WORKLOADS = {
                B=512, N=256, transparse=True),
     "c4s": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512/rank, row-sharded owner-computes",
                 fn="DistMult", nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False,
-                dr=False, B=512, N=1024, sharded=True),
+                dr=False, B=512, N=1024, sharded=True, dataset="yago3_10"),
     # the same, with the all-to-all row-fetch scheme (both schemes, measured side by side)
     "c4g": dict(name="YAGO3-10 DistMult d=500 gamma=24 n_neg=1024 bz=512/rank, row-sharded all-to-all row fetch",
                 fn="DistMult", nentity=123182, nrelation=37, hidden_dim=500, gamma=24.0, de=False, tr=False,
-                dr=False, B=512, N=1024, sharded=True, scheme="gather"),
+                dr=False, B=512, N=1024, sharded=True, scheme="gather", dataset="yago3_10"),
 }
 
 
@@ -176,24 +176,44 @@ def run_step(m, pos, neg, mode, fn, ev=None):
     return out
 
 
-def sharded_bench(w, a, world, rank, device, dist_on):
-    """c4s: ShardedKGE.step_forward on the global batch (replicated by seed on every rank); the
-    timed step includes the two RCCL collectives. Returns (elapsed_s, per-step kernel-free info)."""
+def _global_batches(w, world, n, device):
+    """n global batches of world x B rows (identical on every rank: the replicas' batches replicated
+    by seed): YAGO3-10 positives (RandomState(0) permutation), RandomState negatives."""
+    E, B, N = w["nentity"], w["B"], w["N"]
+    WB = world * B
+    tri = load_triples(w)
+    perm = np.random.RandomState(0).permutation(len(tri))
+    out = []
+    for i in range(n):
+        idx = perm[np.arange(i * WB, (i + 1) * WB) % len(tri)]
+        neg = np.random.RandomState(200 + i).randint(E, size=(WB, N))
+        wt = np.random.RandomState(300 + i).uniform(0.1, 1.0, size=WB).astype(np.float32)
+        out.append((torch.from_numpy(tri[idx]).to(device), torch.from_numpy(neg).to(device),
+                    torch.from_numpy(wt).to(device)))
+    return out
+
+
+def sharded_bench(w, a, world, rank, device, dist_on, train=False):
+    """c4s: ShardedKGE.step_forward (or, with train, ShardedKGE.train_step: the whole row-sharded
+    train step with Keras Adam) on the global batch; the timed step includes every collective.
+    Returns the elapsed seconds of a.steps steps (this rank)."""
     from customknowledgegraphembedding_amd.distributed import ShardedKGE
     sk = ShardedKGE(w["fn"], w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"],
                     double_entity_embedding=w["de"], double_relation_embedding=w["dr"],
                     triple_relation_embedding=w["tr"], device=device, seed=0)
-    E, R, B, N = w["nentity"], w["nrelation"], w["B"], w["N"]
-    WB = world * B
-    batches = []
-    for i in range(4):
-        g = np.random.RandomState(100 + i)  # same seed on every rank: the global batch is replicated
-        pos = np.stack([g.randint(E, size=WB), g.randint(R, size=WB), g.randint(E, size=WB)], 1)
-        neg = np.random.RandomState(200 + i).randint(E, size=(WB, N))
-        batches.append((torch.from_numpy(pos).to(device), torch.from_numpy(neg).to(device)))
-    step = sk.step_forward_gather if w.get("scheme") == "gather" else sk.step_forward
+    batches = _global_batches(w, world, 4, device)
+    if train:
+        sk.configure_optimizer(lr=5e-5)
+
+        def step(b, i):
+            return sk.train_step(b[0], b[1], b[2], i % 2)
+    else:
+        fwd = sk.step_forward_gather if w.get("scheme") == "gather" else sk.step_forward
+
+        def step(b, i):
+            return fwd(b[0], b[1], i % 2)
     for i in range(a.warmup):
-        step(*batches[i % 4], i % 2)
+        step(batches[i % 4], i)
     torch.cuda.synchronize()
     if dist_on:
         import torch.distributed as tdist
@@ -201,11 +221,84 @@ def sharded_bench(w, a, world, rank, device, dist_on):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(*batches[i % 4], i % 2)
+        step(batches[i % 4], i)
     torch.cuda.synchronize()
     if dist_on:
         tdist.barrier()
     return time.perf_counter() - t0
+
+
+def shard_sim_bench(device, world=8, reps=10):
+    """Single-GPU evidence for the row-sharded scaling at the full C4 size (YAGO3-10
+    DistMult d=500, E=123182, N=1024): ONE rank's kernels of a simulated `world`-way split, on the
+    global batch of world x 512 rows, timed with events on the launch stream, against the unsharded
+    kernel on the same global batch (what one GPU holding the whole table would run)."""
+    from customknowledgegraphembedding_amd.distributed import HipShardKernels, ShardedKGE
+    from customknowledgegraphembedding_amd.model import TFKGEModel
+    w = WORKLOADS["c4s"]
+    E, d, N = w["nentity"], w["hidden_dim"], w["N"]
+    pos, neg, wt = _global_batches(w, world, 1, device)[0]
+    Bg = pos.shape[0]
+    full = TFKGEModel("DistMult", E, w["nrelation"], d, w["gamma"], device=device, seed=0)
+    ent, rel = full.entity_embedding.detach(), full.relation_embedding.detach()
+    sk = ShardedKGE("DistMult", E, w["nrelation"], d, w["gamma"], device=device, seed=0, world=world, rank=0)
+    fn = FN_IDS["DistMult"]
+    qent = ent[pos[:, 2]].contiguous()  # head-batch query rows (assembled by the all-reduce on N GPUs)
+    qpos = ent[pos[:, 0]].contiguous()
+    out = torch.empty((Bg, N), dtype=torch.float32, device=device)
+
+    def timed(f):
+        f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3  # us
+
+    unsharded_us = timed(lambda: ops.score_indexed_raw(fn, 0, ent, rel, 0, pos, neg, d, full._gamma_f, full._range_f))
+    shard_us = timed(lambda: HipShardKernels.score_sharded(fn, 0, qent, rel, 0, sk.shard, sk.lo, pos, neg, d,
+                                                           full._gamma_f, full._range_f, 0.0, out))
+    sk.configure_optimizer()
+    bufs = HipShardKernels.train_alloc(sk, Bg, N)
+    train_fwd_us = timed(lambda: HipShardKernels.train_forward(sk, bufs, 0, qent, qpos, pos, neg, wt))
+    # the whole sharded train step of a simulated world: `world` ranks as threads on this GPU (ThreadComm),
+    # then rank 0's three calls timed on their own (kernels only; the collectives are priced from their sizes)
+    from customknowledgegraphembedding_amd.distributed import ThreadComm, run_threads
+    comm = ThreadComm(world)
+    ranks = [ShardedKGE("DistMult", E, w["nrelation"], d, w["gamma"], device=device, seed=0, world=world, rank=r,
+                        comm=comm).configure_optimizer(lr=5e-5) for r in range(world)]
+    for i in range(2):
+        run_threads([lambda sk=x: sk.train_step(pos, neg, wt, i % 2) for x in ranks])
+    torch.cuda.synchronize()
+    r0 = ranks[0]
+    b0 = r0._bufs[(Bg, N)]
+    HK = HipShardKernels
+    qa, qb = qent, qpos
+    stats_all = torch.stack([x._bufs[(Bg, N)]["stats"] for x in ranks])
+    t_fwd = timed(lambda: HK.train_forward(r0, b0, 0, qa, qb, pos, neg, wt))
+    t_comb = timed(lambda: HK.train_combine(r0, b0, 0, qa, qb, pos, neg, wt, stats_all))
+    t_bwd = timed(lambda: HK.train_backward(r0, b0, 0, qa, qb, pos, neg, wt, 3, None))
+    del ranks, comm
+    coll_bytes = {"query_rows_allreduce": 2 * Bg * d * 4, "stats_allgather": world * Bg * 16,
+                  "query_grad_allreduce": 2 * Bg * d * 4}
+    owned = (((neg >= sk.lo) & (neg < sk.hi)).sum().item())
+    per_cand = 4 * d + 12
+    return {"workload": f"C4 YAGO3-10 DistMult d=500 N=1024, global batch {world} x 512, one rank of a simulated "
+                        f"{world}-way row split (rows [{sk.lo}, {sk.hi}))",
+            "unsharded_global_kernel_us": unsharded_us, "rank_score_kernel_us": shard_us,
+            "rank_over_unsharded": shard_us / unsharded_us,
+            "rank_train_forward_kernels_us": train_fwd_us,
+            "rank_train_step_kernels_us": {"forward": t_fwd, "combine": t_comb, "backward": t_bwd,
+                                           "total": t_fwd + t_comb + t_bwd},
+            "rank_train_triples_per_s_kernels_only": world * 512 * (N + 1) / ((t_fwd + t_comb + t_bwd) * 1e-6),
+            "collective_bytes_per_step": coll_bytes,
+            "owned_candidates": owned, "owned_fraction": owned / (Bg * N),
+            "rank_score_kernel_gbs": owned * per_cand / (shard_us * 1e-6) / 1e9,
+            "what": "kge_score_sharded (owned candidates compacted per wave) vs kge_score_indexed over the whole "
+                    "global batch; kge_shard_train_forward = the sharded train step's gather pass"}
 
 
 def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
@@ -571,6 +664,7 @@ def main(argv=None):
                     help="timing events bracket groups of this many consecutive launches")
     ap.add_argument("--sharded-steps", type=int, default=20,
                     help="side measurement of the YAGO3-10 row-sharded step (c4s) at the same world size (0 = skip)")
+    ap.add_argument("--sharded-train", action="store_true", help="c4s/c4g: time the row-sharded TRAIN step")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of the launcher and timing contract (no GPU, no kernels)")
     a = ap.parse_args(argv)
@@ -612,7 +706,7 @@ def main(argv=None):
             tdist.destroy_process_group()
         return
     if w.get("sharded"):
-        elapsed = sharded_bench(w, a, world, rank, device, dist)
+        elapsed = sharded_bench(w, a, world, rank, device, dist, train=a.sharded_train)
         if dist:
             t = torch.tensor([elapsed], device=device, dtype=torch.float64)
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -742,7 +836,23 @@ def main(argv=None):
             "triples_per_s": (ws["B"] * ws["N"] + ws["B"]) * world * sa.steps / el,
             "ms_per_step": el / sa.steps * 1e3, "steps": sa.steps,
             "what": "distributed.ShardedKGE.step_forward: entity table row-sharded over the ranks, owner-computes "
-                    "scoring, chunk-pipelined RCCL all-reduce (queries) + reduce-scatter (scores)"}
+                    "scoring (owned candidates compacted), chunk-pipelined RCCL all-reduce (queries) + "
+                    "reduce-scatter (scores)"}
+        el = sharded_bench(ws, sa, world, rank, device, dist, train=True)
+        if dist:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            el = float(t.item())
+        line["yago3_10_rowshard_train"] = {
+            "workload": ws["name"] + ", train step", "n_gpus": world, "global_batch": ws["B"] * world,
+            "n_neg": ws["N"], "triples_per_s": (ws["B"] * ws["N"] + ws["B"]) * world * sa.steps / el,
+            "ms_per_step": el / sa.steps * 1e3, "steps": sa.steps,
+            "what": "distributed.ShardedKGE.train_step: supervisor.py:15-26 over the replicas' batches (SUM "
+                    "gradients, Keras Adam) with the entity table row-sharded: owned candidates only, one gather "
+                    "per candidate row, RCCL all-reduce of query rows, all-gather of [Bg,4] row stats, all-reduce "
+                    "of query gradients; Adam on the shard"}
+        if world == 1:
+            line["yago3_10_shard_sim8"] = shard_sim_bench(device)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w, a.cpu_budget)
     if rank == 0:

@@ -52,13 +52,17 @@ __global__ __launch_bounds__(kBlock) void eval_query_kernel(ScoreParams p, float
 // MFMA tiles, independent accumulators -> back-to-back issue), K staged through LDS in chunks of 16,
 // double buffered (next chunk's global loads in registers while the current chunk is multiplied).
 // LDS images are k-major ([k][m]) so a wave's fragment read (lanes 0-31 one k, 32-63 the next)
-// is 32 consecutive dwords per half-wave: conflict-free ds_read_b32.
+// is 32 consecutive dwords per half-wave: conflict-free ds_read_b32. The staging stores are the
+// transpose: lane l writes k-row 4 (l % 4) + c, column l / 4, so a half-wave's 32 dwords land on
+// banks 4 (l % 4) LD + l / 4 (mod 32); a row pitch LD = 2 (mod 8) spreads them over all 32 banks
+// (a pitch of BM + 4 put k-rows 0 and 8 on the same banks: 2-way conflicts on every store, which
+// was every SQ_LDS_BANK_CONFLICT cycle the kernel had).
 // BN = 64 halves the tile for grids too small to give every one of the 256 CUs a 128 x 128 tile.
 // ---------------------------------------------------------------------------------------------
 constexpr int GBM = 128, GBK = 16;  // BK = 32 measured 92 vs 96 TFLOP/s at C5
 constexpr int GTPR = GBK / 4;       // threads per staged row
 constexpr int GRPP = kBlock / GTPR;  // rows staged per unit
-constexpr int GLD = GBM + 4;         // padded LDS row (floats)
+constexpr int GLD = GBM + 2;         // padded LDS row (floats): 2 (mod 8), conflict-free stores
 
 template <int BN>
 __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
@@ -67,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __rest
     constexpr int JN = BN / 64;               // 32-wide MFMA tiles per wave in N
     constexpr int AU = GBM * GBK / 4 / kBlock;  // float4 per thread for A
     constexpr int BU = BN * GBK / 4 / kBlock;   // float4 per thread for B
-    constexpr int BLD = BN + 4;
+    constexpr int BLD = BN + 2;  // 2 (mod 8) as GLD
     __shared__ __attribute__((aligned(16))) float As[2][GBK][GLD];
     __shared__ __attribute__((aligned(16))) float Bs[2][GBK][BLD];
     const int t = threadIdx.x;

@@ -50,7 +50,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int TBM = 128, TBN = 128, TBK = 32;
 constexpr int NU = TBK / 8;  // float4 per thread per operand and K chunk
-constexpr int TLD = TBN + 4;
+constexpr int TLD = TBN + 4;  // row pitch of images stored with 16-B (ds_write_b128) rows: 16-B aligned
+// row pitch of images stored TRANSPOSED (lane l writes k-row 4 (l % 8) + c, column l / 8 with
+// ds_write_b32): a pitch of 1 (mod 8) puts a half-wave's 32 dwords on 32 distinct banks (the old
+// TBM + 4 gave 4-way conflicts on every transposed store)
+constexpr int ALD = TBM + 1;
 constexpr int kMaxTsDim = 8192;
 enum TsOp { TS_FWD = 0, TS_GP = 1, TS_DH = 2 };
 
@@ -140,8 +144,9 @@ __device__ __forceinline__ int acc_row(int wm, int i, int r, int half) {
 // ---------------------------------------------------------------------------------------------
 template <int OP, int VEC>
 __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
-    __shared__ __attribute__((aligned(16))) float As[2][TBK][TLD];
-    __shared__ __attribute__((aligned(16))) float Bs[2][TBK][TLD];
+    constexpr int BLD = OP == TS_DH ? ALD : TLD;  // TS_DH stages M_r transposed like A
+    __shared__ __attribute__((aligned(16))) float As[2][TBK][ALD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][TBK][BLD];
     __shared__ const float* rowp[TBM];
     __shared__ int rb[TBM], rn[TBM];  // (b, n) of each row; rb = -1 for padding rows
     __shared__ float2 red[TBM];

@@ -155,12 +155,9 @@ class TorchComm:
     def all_gather_cat(self, t):
         """[W, *t.shape], rank-major."""
         W = dist.get_world_size(self.group)
-        out = torch.empty((W,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        if t.is_cuda:
-            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
-        else:
-            dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
-        return out
+        parts = [torch.empty_like(t) for _ in range(W)]
+        dist.all_gather(parts, t.contiguous(), group=self.group)  # any backend (RCCL, gloo), any device
+        return torch.stack(parts)
 
     def all_reduce_sum_(self, t):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)

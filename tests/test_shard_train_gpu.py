@@ -158,3 +158,4 @@ def test_sharded_c4_full_size_step_runs_and_matches_sampled_oracle_loss():
                                gamma, ref._range_f).item()
         assert la[0][h] == pytest.approx(want, rel=1e-4)
     assert all(sk.shard.shape[0] == shard_bounds(E, W, sk.rank)[1] - shard_bounds(E, W, sk.rank)[0] for sk in ranks)
+

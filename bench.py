@@ -77,20 +77,37 @@ WORKLOADS = {
 }
 
 
-def pmc_traffic(workload, kernel_prefix):
-    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 --pmc summary of this
+def library_sha256():
+    import hashlib
+    path = os.path.join(ROOT, "customknowledgegraphembedding_amd", "libkge_hip.so")
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_traffic(workload, kernel_prefixes):
+    """HBM bytes per step of the kernels `kernel_prefixes` (each: the mean over its head/tail
+    instantiations, summed over the prefixes) from the committed rocprofv3 --pmc summary of this
     workload (profiles/pmc_<workload>.json, scripts/pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x 2
-    + WRITE_SIZE, the gfx950 corrections). None when no summary was committed."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"pmc_{workload}.json")
+    + WRITE_SIZE, the gfx950 corrections). (None, reason) when no summary was committed, or when it
+    was measured on another build of libkge_hip.so than the one loaded now (stale)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     try:
         with open(path) as f:
-            rows = json.load(f)["kernels"]
+            summ = json.load(f)
+        rows = summ["kernels"]
     except (OSError, ValueError, KeyError):
-        return None, None
-    for row in rows:
-        if row.get("kernel", "").startswith(kernel_prefix) and "hbm_read_bytes_corrected" in row:
-            return row["hbm_read_bytes_corrected"] + row.get("hbm_write_bytes", 0.0), os.path.relpath(path)
-    return None, None
+        return None, "no PMC summary committed"
+    if summ.get("library_sha256") != library_sha256():
+        return None, f"stale: {os.path.relpath(path, ROOT)} was measured on another libkge_hip.so build"
+    total = 0.0
+    for pre in kernel_prefixes:
+        got = [r["hbm_read_bytes_corrected"] + r.get("hbm_write_bytes", 0.0) for r in rows
+               if r.get("kernel", "").startswith(pre + "<") or r.get("kernel", "") == pre]
+        got = [g for g in got if g == g]
+        if not got:
+            return None, f"{os.path.relpath(path, ROOT)} has no {pre}"
+        total += sum(got) / len(got)
+    return total, os.path.relpath(path, ROOT)
 
 
 def dims(w):
@@ -782,7 +799,9 @@ def main(argv=None):
 
     neg_bytes, pos_bytes = algorithmic_bytes(w)
     step_bytes = neg_bytes + pos_bytes  # the fused kernel moves both calls' bytes
-    traffic, traffic_src = pmc_traffic(a.workload, "step_fwd_kernel")
+    xcd = bool(kge.load().kge_step_forward_order(w["nentity"], N))
+    step_kernels = ["step_fwd_xcd_kernel", "neg_rows_kernel"] if xcd else ["step_fwd_kernel"]
+    traffic, traffic_src = pmc_traffic(a.workload, step_kernels)
     kern_avg_s = statistics.mean(kern_ms) / 1e3
     # head and tail reported separately (steps alternate head, tail, ...)
     # unique-row bytes of one step (row reuse inside a batch; the algorithmic bytes count every gather)
@@ -809,9 +828,11 @@ def main(argv=None):
         "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N, "hidden_dim": w["hidden_dim"],
                    "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/step",
                      "traffic_source": traffic_src,
-                     "kernel": "step_fwd_kernel (negatives + positives + row reductions, one launch)",
+                     "kernel": ("step_fwd_xcd_kernel + neg_rows_kernel (the step's two launches: negatives and "
+                                "positives gathered in XCD-sliced ascending-id order, then the row reductions)" if xcd
+                                else "step_fwd_kernel (negatives + positives + row reductions, one launch)"),
                      "kernel_avg_us": kern_avg_s * 1e6,
                      "kernel_avg_us_head_batch": head_ms[0] * 1e3,
                      "kernel_avg_us_tail_batch": tail_ms[0] * 1e3,

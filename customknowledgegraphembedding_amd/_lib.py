@@ -35,6 +35,7 @@ SIGNATURES = {
     "kge_abi_version": (_c_i, []),
     "kge_last_error": (ctypes.c_char_p, []),
     "kge_max_dim": (_c_i64, [_c_i]),
+    "kge_step_forward_order": (_c_i, [_c_i64, _c_i64]),
     "kge_score_indexed": (
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,

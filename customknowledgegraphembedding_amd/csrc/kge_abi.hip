@@ -22,8 +22,18 @@ __global__ __launch_bounds__(kBlock) void neg_reduce_kernel(const float* __restr
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (b >= B) return;
     const int lane = threadIdx.x & 63;
-    const float res = row_reduce(s + b * ld, N, T, adversarial, lane);
+    const float res = row_reduce_fast(s + b * ld, N, T, adversarial, lane);
     if (lane == 0) out[b] = res;
+}
+
+// kge_step_forward's XCD-sliced form: the row reductions after step_fwd_xcd_kernel (one wave per row)
+__global__ __launch_bounds__(kBlock) void neg_rows_kernel(ScoreParams p) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    const float* row = p.out + b * p.out_ld;
+    const float r = row_reduce_fast(row, p.N, p.temperature, p.adversarial, lane);
+    if (lane == 0) p.out_neg[b] = r;
 }
 
 // With `ps` set it also writes the positive branch's d_ps[b] = d_out_pos[b] * sigmoid(-ps[b])
@@ -452,6 +462,8 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM || kind == KIND_STEP_FWD ||
                kind == KIND_STEP_FWD_STATS || kind == KIND_STEP_FWD_GRAD || kind == KIND_SHARD_FWD_GRAD) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
+    } else if (kind == KIND_STEP_FWD_XCD) {
+        waves = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock * 8;  // 8 slice blocks per 4 rows
     } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS) {
         waves = p.B;  // one wave per slot
     } else if (kind == KIND_STEP_EPILOGUE || kind == KIND_SHARD_EPILOGUE) {
@@ -556,6 +568,19 @@ void fill_dense(ScoreParams& p, int fn, int mode, const float* head, int64_t hea
 
 bool empty(int64_t B, int64_t N) { return B == 0 || N == 0; }
 
+// kge_step_forward's candidate order: XCD-sliced ascending ids (KIND_STEP_FWD_XCD) or batch-row-major
+// (KIND_STEP_FWD). KGE_STEP_ORDER=xcd|row overrides the choice (A/B runs).
+bool use_xcd_order(int64_t nentity, int64_t N) {
+    static const int forced = [] {
+        const char* s = getenv("KGE_STEP_ORDER");
+        if (!s) return -1;
+        return strcmp(s, "xcd") == 0 ? 1 : (strcmp(s, "row") == 0 ? 0 : -1);
+    }();
+    if (nentity >= (int64_t)8 << 25) return false;  // sort keys hold (id - slice start) << 6
+    if (forced >= 0) return forced == 1;
+    return N >= 128;
+}
+
 }  // namespace
 
 int set_error(int code, const char* msg) { return fail(code, msg); }
@@ -576,6 +601,8 @@ int64_t kge_max_dim(int fn) {
     if (fn < KGE_TRANSE || fn > KGE_PROTATE) return 0;
     return (int64_t)kMaxG * kWave * 4;
 }
+
+int kge_step_forward_order(int64_t nentity, int64_t N) { return use_xcd_order(nentity, N) ? 1 : 0; }
 
 int kge_score_indexed(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
                       int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
@@ -643,6 +670,15 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
     p.out_neg = out_neg;
     p.out_pos_raw = pos_scores;
     p.out_pos_ls = out_pos;
+    if (!(cand_stats && fn == KGE_INTERHT) && use_xcd_order(nentity, N)) {
+        // two launches: the negatives (and the positives) in XCD-sliced ascending-id order, then the rows'
+        // self-adversarial reductions
+        rc = run_score(fn, mode, p, KIND_STEP_FWD_XCD, stream);
+        if (rc) return rc;
+        const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
+        hipLaunchKernelGGL(neg_rows_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, p);
+        return check_launch("kge_step_forward row reductions");
+    }
     // one launch: negatives + the per-row finish (positive, reduction)
     return run_score(fn, mode, p, (cand_stats && fn == KGE_INTERHT) ? KIND_STEP_FWD_STATS : KIND_STEP_FWD, stream);
 }

@@ -18,6 +18,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 #include "kge_internal.h"
 
 namespace kge_impl {
@@ -157,6 +159,25 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int j) {
 
 __device__ __forceinline__ float readlanef(float v, int j) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+// ascending bitonic sort of one int per lane across the wave
+__device__ __forceinline__ int wave_sort_asc(int v, int lane) {
+#pragma unroll
+    for (int k = 2; k <= kWave; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int o = __shfl_xor(v, j, kWave);
+            const bool keep_min = ((lane & k) == 0) == ((lane & j) == 0);
+            v = keep_min ? min(v, o) : max(v, o);
+        }
+    return v;
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
+    return v;
 }
 
 __device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
@@ -412,12 +433,48 @@ __device__ __forceinline__ const float* cand_row(const ScoreParams& p, int64_t i
 // Scores up to 64 candidates held one per lane (lane j: global id my_id, j < nc) against the wave's
 // query; returns candidate j's score in lane j (and, with ST, InterHT's candidate inverse half-norms
 // in my_st). Software pipeline: row j+1 is in flight while row j is reduced.
-template <int FN, bool CH, int V, int G, bool ST>
-__device__ __forceinline__ float score_lanes(const ScoreParams& p, const Query<FN, CH, V, G>& q, int64_t my_id, int nc,
-                                             int lane, float2& my_st) {
+// Query with InterHT's third operand (the relation's middle third, shared by every candidate) read
+// from a wave-private LDS image: 4 x G fewer VGPRs per lane (the XCD-sliced kernel then holds 4 waves
+// per SIMD at D = 1000). fresh() launders the LDS index before each candidate so the reads are not
+// hoisted back into loop-invariant registers.
+template <int FN, bool CH, int V, int G>
+struct QueryL2 {
+    vecf<V> q0[G], q1[G];
+    LdsOperand<V> q2;
+};
+template <class Q>
+__device__ __forceinline__ const Q& fresh(const Q& q) {
+    return q;
+}
+template <int FN, bool CH, int V, int G>
+__device__ __forceinline__ QueryL2<FN, CH, V, G> fresh(const QueryL2<FN, CH, V, G>& q) {
+    QueryL2<FN, CH, V, G> r = q;
+    int li = q.q2.idx;
+    asm volatile("" : "+v"(li));
+    r.q2.idx = li;
+    return r;
+}
+
+template <int FN, bool CH, int V, int G, bool ST, class Q, int DEPTH = 2>
+__device__ __forceinline__ float score_lanes(const ScoreParams& p, const Q& q, int64_t my_id, int nc, int lane,
+                                             float2& my_st) {
     float my_score = 0.f;
     float2 st;
     float2* stp = ST ? &st : nullptr;
+    if constexpr (DEPTH == 1) {
+        // one row in registers at a time: fewer VGPRs, more waves per SIMD hide the gather latency
+        for (int j = 0; j < nc; ++j) {
+            Cand<FN, V, G> x;
+            bool ok;
+            x.load(cand_row(p, readlane64(my_id, j), ok), ok, p.D, lane);
+            const float sc = cand_score<FN, CH, V, G>(x, fresh(q), p, stp);
+            if (lane == j) {
+                my_score = sc;
+                if constexpr (ST) my_st = st;
+            }
+        }
+        return my_score;
+    }
     Cand<FN, V, G> x0, x1;
     bool ok0, ok1;
     const float* row = cand_row(p, readlane64(my_id, 0), ok0);
@@ -432,18 +489,18 @@ __device__ __forceinline__ float score_lanes(const ScoreParams& p, const Query<F
     for (; j + 2 < nc; j += 2) {
         row = cand_row(p, readlane64(my_id, j + 1), ok1);
         x1.load(row, ok1, p.D, lane);
-        keep(j, cand_score<FN, CH, V, G>(x0, q, p, stp));
+        keep(j, cand_score<FN, CH, V, G>(x0, fresh(q), p, stp));
         row = cand_row(p, readlane64(my_id, j + 2), ok0);
         x0.load(row, ok0, p.D, lane);
-        keep(j + 1, cand_score<FN, CH, V, G>(x1, q, p, stp));
+        keep(j + 1, cand_score<FN, CH, V, G>(x1, fresh(q), p, stp));
     }
     if (j + 1 < nc) {
         row = cand_row(p, readlane64(my_id, j + 1), ok1);
         x1.load(row, ok1, p.D, lane);
-        keep(j, cand_score<FN, CH, V, G>(x0, q, p, stp));
-        keep(j + 1, cand_score<FN, CH, V, G>(x1, q, p, stp));
+        keep(j, cand_score<FN, CH, V, G>(x0, fresh(q), p, stp));
+        keep(j + 1, cand_score<FN, CH, V, G>(x1, fresh(q), p, stp));
     } else {
-        keep(j, cand_score<FN, CH, V, G>(x0, q, p, stp));
+        keep(j, cand_score<FN, CH, V, G>(x0, fresh(q), p, stp));
     }
     return my_score;
 }
@@ -545,6 +602,130 @@ __device__ __forceinline__ void score_owned(const ScoreParams& p, const Query<FN
     });
 }
 
+// ---------------------------------------------------------------------------------------------
+// XCD-sliced scoring (kge_step_forward's negatives, KIND_STEP_FWD_XCD). The entity table is cut into 8
+// slices of S = ceil(E / 8) rows; block i scores, for the 4 batch rows b = 4 (i / 8) + w, only the
+// candidates whose id falls in slice x = i % 8. Blocks i and i + 8 share an XCD (round-robin dispatch),
+// so every gather of an entity row is issued by one XCD, and each wave walks its candidates in
+// ascending id order: the XCD's waves sweep their slice together and the repeat gathers of a row (row
+// reuse ~3.4x at C2) hit that XCD's L2 or the Infinity Cache instead of HBM (tools/locality_probe.hip:
+// the same gathers run 0.84-0.86x the time of the batch-row-major order). The scores are those of
+// step_fwd_kernel bitwise (same query build, same per-candidate code).
+// ---------------------------------------------------------------------------------------------
+// Walks the ids of batch row b, compacting the candidates of slice [e_lo, e_hi) (and, with
+// take_invalid, every id outside [0, c_rows), which scores against a zero row) into lanes; calls
+// body(id32, n, cnt) with up to 64 of them, sorted by id (id32 = id, or -1 for an invalid one; n its
+// candidate column).
+template <class Body>
+__device__ __forceinline__ void for_slice_runs_sorted(const ScoreParams& p, int64_t b, int64_t e_lo, int64_t e_hi,
+                                                      bool take_invalid, int lane, Body&& body) {
+    int buf_key = INT32_MAX, buf_id = -1, buf_n = 0, fill = 0;
+    auto flush = [&](int cnt) {
+        // sort key: (id - e_lo) << 6 | source lane (invalid ids first, as id - e_lo = 0)
+        const int key = wave_sort_asc(lane < cnt ? buf_key : INT32_MAX, lane);
+        const int src = key & (kWave - 1);
+        const int id = lane_pull(buf_id, src), n = lane_pull(buf_n, src);
+        body(id, n, cnt);
+    };
+    for (int64_t c0 = 0; c0 < p.N; c0 += kWave) {
+        const int64_t n = c0 + lane;
+        int64_t id = -1;
+        if (n < p.N) id = p.c_idx[b * p.c_stride + n];
+        const bool valid = id >= 0 && id < p.c_rows;
+        const bool own = n < p.N && (valid ? (id >= e_lo && id < e_hi) : take_invalid);
+        const uint64_t m = __ballot(own);
+        const int cnt = __popcll(m);
+        if (cnt == 0) continue;  // wave-uniform
+        const int id32 = valid ? (int)id : -1, n32 = (int)n, rl = valid ? (int)(id - e_lo) : 0;
+        const int d = lane - fill;
+        const bool take = d >= 0 && d < cnt;
+        const int src = kth_set_bit(m, take ? d : 0);
+        const int i1 = lane_pull(id32, src), n1 = lane_pull(n32, src), r1 = lane_pull(rl, src);
+        if (take) {
+            buf_id = i1;
+            buf_n = n1;
+            buf_key = (r1 << 6) | lane;
+        }
+        if (fill + cnt >= kWave) {
+            flush(kWave);
+            const int rest = fill + cnt - kWave;
+            const int src2 = kth_set_bit(m, lane < rest ? (kWave - fill) + lane : 0);
+            buf_id = lane_pull(id32, src2);
+            buf_n = lane_pull(n32, src2);
+            buf_key = (lane_pull(rl, src2) << 6) | lane;
+            fill = rest;
+        } else {
+            fill += cnt;
+        }
+    }
+    if (fill > 0) flush(fill);
+}
+
+// The XCD-sliced kernel also scores the row's positive triple (single mode, tail formula, model.py:127-146):
+// the wave whose slice holds the positive's tail does it (slice 0 for an out-of-range tail). The row's
+// self-adversarial reduction needs every slice's scores and runs in neg_rows_kernel after it.
+// One candidate row in registers at a time (score_lanes<DEPTH = 1>) and 4 waves per SIMD up to D = 1024:
+// every wave of a C2-sized launch (8 x 512) is resident at once, so the XCDs' sweeps stay together
+// (2-deep pipelining at 3 waves per SIMD measured 140 us against 133 us for this form at C2).
+template <int FN, bool CH, int V, int G>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(G <= 4 ? 4 : 1))) void
+step_fwd_xcd_kernel(ScoreParams p) {
+    __shared__ vecf<V> q2img[kWavesPerBlock][FN == KGE_INTERHT ? G * kWave : 1];
+    const int x = blockIdx.x & 7;
+    const int w = threadIdx.x >> 6;
+    const int64_t b = (int64_t)(blockIdx.x >> 3) * kWavesPerBlock + w;
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t S = (p.c_rows + 7) / 8;
+    const int64_t e_lo = min((int64_t)x * S, p.c_rows), e_hi = min(p.c_rows, e_lo + S);
+    const int64_t t = p.pos_base[b * 3 + 2];
+    const bool t_here = (t >= 0 && t < p.c_rows) ? (t >= e_lo && t < e_hi) : x == 0;
+    Query<FN, CH, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+    auto run = [&](const auto& qq) {
+        for_slice_runs_sorted(p, b, e_lo, e_hi, x == 0, lane, [&](int id, int n, int cnt) {
+            float2 st;
+            const float s = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, 1>(p, qq, (int64_t)id, cnt, lane, st);
+            if (lane < cnt) p.out[b * p.out_ld + n] = s;
+        });
+        if (!t_here) return;  // wave-uniform
+        bool ok;
+        Cand<FN, V, G> c;
+        c.load(cand_row(p, t, ok), ok, p.D, lane);
+        float s;
+        if constexpr (!CH) {  // tail-batch: the positive's query (h, r) is the negatives' query
+            s = cand_score<FN, false, V, G>(c, fresh(qq), p);
+        } else {
+            Query<FN, false, V, G> qp;
+            const int64_t hi = p.pos_base[b * 3], rj = p.pos_base[b * 3 + 1];
+            const bool hok = hi >= 0 && hi < p.q_rows, rjok = rj >= 0 && rj < p.r_rows;
+            qp.build(p.qent + (hok ? hi : 0) * p.q_ld, hok, p.rel + (rjok ? rj : 0) * p.r_ld + p.r_off, rjok, p.D,
+                     lane, p);
+            s = cand_score<FN, false, V, G>(c, qp, p);
+        }
+        if (lane == 0) {
+            if (p.out_pos_raw) p.out_pos_raw[b] = s;
+            p.out_pos_ls[b] = log_sigmoid(s);
+        }
+    };
+    if constexpr (FN == KGE_INTERHT) {
+        QueryL2<FN, CH, V, G> ql;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            q2img[w][lane + k * kWave] = q.q2[k];
+            ql.q0[k] = q.q0[k];
+            ql.q1[k] = q.q1[k];
+        }
+        ql.q2 = LdsOperand<V>{q2img[w], lane};
+        run(ql);
+    } else {
+        run(q);
+    }
+}
+
+
 template <int FN, bool CH, int V, int G, bool ST = false>
 __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
     WaveTask t;
@@ -582,6 +763,47 @@ __device__ __forceinline__ float row_reduce(const float* row, int64_t N, float T
     float w = 0.f;
     for (int64_t n = lane; n < N; n += kWave) w += log_sigmoid(-row[n]);
     return wave_sum(w) / (float)N;
+}
+
+// The row reduction of kge_step_forward's XCD-sliced form: out_neg[b] = sum softmax(T s) logsigmoid(-s)
+// or mean logsigmoid(-s) over row b's scores (model.py:168-171), one wave per row. The row is loaded
+// into registers in one round (N <= 64 NR) and reduced in row_reduce's exact order (bitwise its result).
+template <int NR>
+__device__ __forceinline__ float row_reduce_regs(const float* row, int64_t N, float T, int adversarial, int lane) {
+    float v[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const int64_t n = lane + (int64_t)k * kWave;
+        v[k] = n < N ? row[n] : 0.f;
+    }
+    if (adversarial) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+            if (lane + (int64_t)k * kWave < N) m = fmaxf(m, T * v[k]);
+        m = wave_max(m);
+        float z = 0.f, wsum = 0.f;
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+            if (lane + (int64_t)k * kWave < N) {
+                const float e = expf(T * v[k] - m);
+                z += e;
+                wsum += e * log_sigmoid(-v[k]);
+            }
+        return wave_sum(wsum) / wave_sum(z);
+    }
+    float wsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+        if (lane + (int64_t)k * kWave < N) wsum += log_sigmoid(-v[k]);
+    return wave_sum(wsum) / (float)N;
+}
+
+// row_reduce with the row loaded in one round for N <= 1024 (bitwise row_reduce's result)
+__device__ __forceinline__ float row_reduce_fast(const float* row, int64_t N, float T, int adversarial, int lane) {
+    if (N <= 4 * kWave) return row_reduce_regs<4>(row, N, T, adversarial, lane);
+    if (N <= 16 * kWave) return row_reduce_regs<16>(row, N, T, adversarial, lane);
+    return row_reduce(row, N, T, adversarial, lane);
 }
 
 // Backward of one row's reduction (model.py:168-171): drow[n] = go * d(row_reduce)/d s_n.
@@ -630,7 +852,7 @@ __device__ __forceinline__ void finish_row(const ScoreParams& p, const int64_t* 
     const int64_t qi = pos[b * 3], ri = pos[b * 3 + 1];
     const bool qok = qi >= 0 && qi < p.q_rows, rok = ri >= 0 && ri < p.r_rows;
     q.build(p.qent + (qok ? qi : 0) * p.q_ld, qok, p.rel + (rok ? ri : 0) * p.r_ld + p.r_off, rok, p.D, lane, p);
-    const float red = row_reduce(scores, n_neg, p.temperature, p.adversarial, lane);
+    const float red = row_reduce_fast(scores, n_neg, p.temperature, p.adversarial, lane);
     const float s = cand_score<FN, false, V, G>(c, q, p);
     if (lane == 0) {
         if (p.out_pos_raw) p.out_pos_raw[b] = s;
@@ -1363,25 +1585,6 @@ __global__ __launch_bounds__(kBlock) void bwd_rows_kernel(ScoreParams p) {
         for (int ww = 1; ww < kWavesPerBlock; ++ww) m += red_mod[ww];
         p.dmod_part[p.slot0 + b] = m;
     }
-}
-
-// ascending bitonic sort of one int per lane across the wave
-__device__ __forceinline__ int wave_sort_asc(int v, int lane) {
-#pragma unroll
-    for (int k = 2; k <= kWave; k <<= 1)
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const int o = __shfl_xor(v, j, kWave);
-            const bool keep_min = ((lane & k) == 0) == ((lane & j) == 0);
-            v = keep_min ? min(v, o) : max(v, o);
-        }
-    return v;
-}
-
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
-    return v;
 }
 
 template <int FN, bool CH, int V, int G>
@@ -2186,6 +2389,8 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
     }
     else if (kind == KIND_STEP_FWD)
         hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, false>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_STEP_FWD_XCD)
+        hipLaunchKernelGGL((step_fwd_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_STEP_FWD_GRAD) {
         if constexpr (FN != KGE_PROTATE && G <= kFwdGradMaxG) {
             if (!p.adversarial)

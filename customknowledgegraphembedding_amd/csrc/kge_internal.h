@@ -31,6 +31,7 @@ enum Kind {
     KIND_SHARD_FWD_GRAD = 13,  // row-sharded train step: owned candidates' scores + partial softmax state
     KIND_SHARD_POS = 14,       // row-sharded train step: owned positives (score, gradient, query gradient)
     KIND_SHARD_EPILOGUE = 15,  // row-sharded train step: owned score gradients, every slot's chain, loss
+    KIND_STEP_FWD_XCD = 16,    // kge_step_forward's negatives, XCD-sliced entity table, ascending ids per wave
 };
 // query operands a score function's gradient has (q0 always; q1 for the complex / split forms; q2 InterHT)
 constexpr int shard_nq(int fn) {

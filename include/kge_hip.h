@@ -65,6 +65,10 @@ const char* kge_last_error(void);
 /* Largest per-half width D the forward kernels accept for a score function (in floats). */
 int64_t kge_max_dim(int fn);
 
+/* Which form kge_step_forward (without cand_stats) uses for a table of nentity rows and N negatives
+ * per batch row: 0 = one launch, batch-row-major; 1 = two launches, XCD-sliced (see kge_step_forward). */
+int kge_step_forward_order(int64_t nentity, int64_t N);
+
 /*
  * Fused gather + score (replaces model.py:127-137,148-159,174-185 gathers + model_func calls at
  * :139-144,161-166,187-192; upstream KGEModel.forward gathers + model_func).
@@ -84,8 +88,13 @@ int kge_score_indexed(int fn, int mode,
 
 /*
  * Fused forward of one TF train step (supervisor.py:17-18): the negative call
- * model(((pos, neg), mode)) and the positive call model(((pos, neg), 3)) in ONE launch: a block per batch
- * row scores its negatives, then finishes the row (positive, reduction).
+ * model(((pos, neg), mode)) and the positive call model(((pos, neg), 3)). Two forms, chosen per call by
+ * kge_step_forward_order (results bitwise identical):
+ *   0: ONE launch: a block per batch row scores its negatives, then finishes the row (positive, reduction);
+ *   1: TWO launches: the negatives and positives in XCD-sliced order (each XCD gathers only the rows of
+ *      one eighth of the table, every wave in ascending id order, so repeat gathers of a row hit the
+ *      XCD's L2 / the Infinity Cache), then one wave per row reduces it. Used for N >= 128 unless
+ *      KGE_STEP_ORDER=row|xcd overrides; without cand_stats only.
  *   mode       KGE_HEAD_BATCH or KGE_TAIL_BATCH (the batch's negative mode)
  *   neg_scores [B,N] raw negative scores (out, row stride ns_ld) — kept for the backward
  *   out_neg    [B]   reduced negative branch: adversarial != 0 -> sum softmax(T s) logsigmoid(-s)

@@ -9,6 +9,9 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc/c2"
 json_out = sys.argv[2] if len(sys.argv) > 2 else None
+# the library the passes ran: bench.py reports the traffic only while the in-tree library is this build
+lib = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                           "customknowledgegraphembedding_amd", "libkge_hip.so")
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
@@ -37,5 +40,7 @@ for line in out:
 if json_out:
     import json
     with open(json_out, "w") as f:
-        json.dump({"source": root, "correction": "FETCH_SIZE kB x 1024 x 2 (gfx950, MI355X_MICROARCH.md HBM); "
+        import hashlib
+        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
+        json.dump({"source": root, "library_sha256": sha, "correction": "FETCH_SIZE kB x 1024 x 2 (gfx950, MI355X_MICROARCH.md HBM); "
                    "WRITE_SIZE kB x 1024", "kernels": out}, f, indent=1)

@@ -1,0 +1,374 @@
+// locality_probe.hip — does the order of the candidate gathers change the memory-system ceiling of the
+// scoring kernel (C2: 131 072 random 8 000-B rows of a 327 MB table per launch, row reuse ~3.2x)?
+//
+// Every variant gathers exactly the same (batch row, candidate) pairs with trivial compute; only the
+// assignment of candidates to waves and their order inside a wave change:
+//   rowmajor        wave = (batch row, quarter of its candidates), candidate order   (= step_fwd_kernel)
+//   rowmajor-sorted same waves, each wave's 64 ids ascending
+//   xcd             wave = (batch row, entity slice x of E/8 ids); block i holds 4 batch rows of slice
+//                   x = i % 8, so every gather of an entity row is issued by the same XCD (blocks b and
+//                   b + 8 share an XCD), ids in candidate order
+//   xcd-sorted      the same, ids ascending: the XCD's waves sweep their slice together, so the repeat
+//                   gathers of a row land close in time (L2 / Infinity Cache hits)
+// Build: hipcc --offload-arch=gfx950 -O3 -o locality_probe locality_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#define CHECK(x)                                                                      \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                  \
+        }                                                                             \
+    } while (0)
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+constexpr int G = 8;  // float4 groups per lane: 2000 floats = 500 float4 (last group partial, range-checked)
+struct Row {
+    float a[G][4];
+};
+
+__device__ __forceinline__ void load_row(Row& r, const float* base, int lane, uint32_t bytes) {
+    const rsrc_t s = make_rsrc(base, bytes);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b128(s, (uint32_t)((lane + 64 * k) * 16), 0, 0);
+        r.a[k][0] = __uint_as_float(u[0]);
+        r.a[k][1] = __uint_as_float(u[1]);
+        r.a[k][2] = __uint_as_float(u[2]);
+        r.a[k][3] = __uint_as_float(u[3]);
+    }
+}
+
+__device__ __forceinline__ float row_sum(const Row& r) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < G; ++k) s += (r.a[k][0] + r.a[k][1]) + (r.a[k][2] + r.a[k][3]);
+    return s;
+}
+
+// wave gw gathers list wl[gw] = ids[off[l], off[l+1]) in runs of 64, two rows in flight
+__global__ __launch_bounds__(256) void gather_lists(const float* __restrict__ tab, int64_t rowf, uint32_t row_bytes,
+                                                    const int* __restrict__ off, const int* __restrict__ ids,
+                                                    const int* __restrict__ wl, int nw, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (gw >= nw) return;
+    const int l = wl[gw];
+    if (l < 0) return;
+    const int lo = off[l], hi = off[l + 1];
+    for (int c0 = lo; c0 < hi; c0 += 64) {
+        const int nc = min(64, hi - c0);
+        const int my = lane < nc ? ids[c0 + lane] : 0;
+        Row r0, r1;
+        float mine = 0.f;
+        load_row(r0, tab + (int64_t)__builtin_amdgcn_readlane(my, 0) * rowf, lane, row_bytes);
+        int j = 0;
+        for (; j + 2 < nc; j += 2) {
+            load_row(r1, tab + (int64_t)__builtin_amdgcn_readlane(my, j + 1) * rowf, lane, row_bytes);
+            float s = row_sum(r0);
+            if (lane == j) mine = s;
+            load_row(r0, tab + (int64_t)__builtin_amdgcn_readlane(my, j + 2) * rowf, lane, row_bytes);
+            s = row_sum(r1);
+            if (lane == j + 1) mine = s;
+        }
+        if (j + 1 < nc) {
+            load_row(r1, tab + (int64_t)__builtin_amdgcn_readlane(my, j + 1) * rowf, lane, row_bytes);
+            float s = row_sum(r0);
+            if (lane == j) mine = s;
+            s = row_sum(r1);
+            if (lane == j + 1) mine = s;
+        } else {
+            const float s = row_sum(r0);
+            if (lane == j) mine = s;
+        }
+        if (lane < nc) out[c0 + lane] = mine;
+    }
+}
+
+
+// entity-major: wave gw walks the (entity, batch row) pairs of list wl[gw] (sorted by entity): an entity
+// row is loaded once per run of equal entities and kept in registers; every pair also loads its batch
+// row's query (q0, q1: 2 x HALF floats of qbuf [B, 2 HALF]) and relation row (rel [11, HALF]) — the
+// operands an entity-major InterHT score reads. Two pairs in flight.
+constexpr int GH = 4;  // float4 groups per lane per half row (HALF = 1000 floats = 250 float4)
+struct Half {
+    float a[GH][4];
+};
+__device__ __forceinline__ void load_half(Half& r, const float* base, int lane, uint32_t bytes) {
+    const rsrc_t s = make_rsrc(base, bytes);
+#pragma unroll
+    for (int k = 0; k < GH; ++k) {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b128(s, (uint32_t)((lane + 64 * k) * 16), 0, 0);
+        r.a[k][0] = __uint_as_float(u[0]);
+        r.a[k][1] = __uint_as_float(u[1]);
+        r.a[k][2] = __uint_as_float(u[2]);
+        r.a[k][3] = __uint_as_float(u[3]);
+    }
+}
+struct Pair {
+    Half ea, eb, q0, q1, q2;
+};
+__device__ __forceinline__ float pair_score(const Pair& p) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < GH; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s += fabsf(p.q0.a[k][i] * p.eb.a[k][i] - p.ea.a[k][i] * p.q1.a[k][i] + p.q2.a[k][i]);
+    return s;
+}
+__global__ __launch_bounds__(256) void gather_pairs(const float* __restrict__ tab, const float* __restrict__ qbuf,
+                                                    const float* __restrict__ rel, const int* __restrict__ off,
+                                                    const int* __restrict__ pe, const int* __restrict__ pb,
+                                                    const int* __restrict__ wl, int nw, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (gw >= nw) return;
+    const int l = wl[gw];
+    if (l < 0) return;
+    const int lo = off[l], hi = off[l + 1];
+    const uint32_t hb = 1000 * 4;
+    for (int c0 = lo; c0 < hi; c0 += 64) {
+        const int nc = min(64, hi - c0);
+        const int my_e = lane < nc ? pe[c0 + lane] : 0, my_b = lane < nc ? pb[c0 + lane] : 0;
+        float mine = 0.f;
+        Pair cur, nxt;
+        int e = __builtin_amdgcn_readlane(my_e, 0), b = __builtin_amdgcn_readlane(my_b, 0);
+        load_half(cur.ea, tab + (int64_t)e * 2000, lane, hb);
+        load_half(cur.eb, tab + (int64_t)e * 2000 + 1000, lane, hb);
+        load_half(cur.q0, qbuf + (int64_t)b * 2000, lane, hb);
+        load_half(cur.q1, qbuf + (int64_t)b * 2000 + 1000, lane, hb);
+        load_half(cur.q2, rel + (int64_t)(b % 11) * 1000, lane, hb);
+        for (int j = 0; j < nc; ++j) {
+            if (j + 1 < nc) {
+                const int e1 = __builtin_amdgcn_readlane(my_e, j + 1), b1 = __builtin_amdgcn_readlane(my_b, j + 1);
+                if (e1 != e) {
+                    load_half(nxt.ea, tab + (int64_t)e1 * 2000, lane, hb);
+                    load_half(nxt.eb, tab + (int64_t)e1 * 2000 + 1000, lane, hb);
+                } else {
+                    nxt.ea = cur.ea;
+                    nxt.eb = cur.eb;
+                }
+                load_half(nxt.q0, qbuf + (int64_t)b1 * 2000, lane, hb);
+                load_half(nxt.q1, qbuf + (int64_t)b1 * 2000 + 1000, lane, hb);
+                load_half(nxt.q2, rel + (int64_t)(b1 % 11) * 1000, lane, hb);
+                e = e1;
+            }
+            float s = pair_score(cur);
+            s += __shfl_xor(s, 1);
+            if (lane == j) mine = s;
+            cur = nxt;
+        }
+        if (lane < nc) out[c0 + lane] = mine;
+    }
+}
+
+struct Lists {
+    std::vector<int> off, ids, wl;
+};
+
+static double run(const char* name, const Lists& L, const float* tab, int64_t rowf, float* out, double bytes) {
+    int *off, *ids, *wl;
+    CHECK(hipMalloc(&off, L.off.size() * 4));
+    CHECK(hipMalloc(&ids, L.ids.size() * 4));
+    CHECK(hipMalloc(&wl, L.wl.size() * 4));
+    CHECK(hipMemcpy(off, L.off.data(), L.off.size() * 4, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(ids, L.ids.data(), L.ids.size() * 4, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(wl, L.wl.data(), L.wl.size() * 4, hipMemcpyHostToDevice));
+    const int nw = (int)L.wl.size(), blocks = (nw + 3) / 4;
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    const int reps = 20;
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL(gather_lists, dim3(blocks), dim3(256), 0, 0, tab, rowf, (uint32_t)(rowf * 4), off, ids, wl, nw, out);
+    CHECK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL(gather_lists, dim3(blocks), dim3(256), 0, 0, tab, rowf, (uint32_t)(rowf * 4), off, ids, wl, nw, out);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    ms /= reps;
+    printf("%-44s %8.1f us  %7.0f GB/s (gathered bytes)\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+    CHECK(hipFree(off));
+    CHECK(hipFree(ids));
+    CHECK(hipFree(wl));
+    return ms;
+}
+
+int main() {
+    const int64_t E = 40943, ROWF = 2000, B = 512, N = 256;
+    std::vector<float> h((size_t)(E * ROWF));
+    std::mt19937 g(0);
+    std::uniform_real_distribution<float> U(-1.f, 1.f);
+    for (auto& x : h) x = U(g);
+    std::vector<int> neg((size_t)(B * N));
+    std::uniform_int_distribution<int> I(0, (int)E - 1);
+    for (auto& x : neg) x = I(g);
+    float *tab, *out;
+    CHECK(hipMalloc(&tab, h.size() * 4));
+    CHECK(hipMalloc(&out, B * N * 4));
+    CHECK(hipMemcpy(tab, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    const double bytes = (double)B * N * ROWF * 4;
+
+    for (int sorted = 0; sorted < 2; ++sorted) {  // row-major: wave = (b, quarter)
+        Lists L;
+        L.off.push_back(0);
+        for (int64_t b = 0; b < B; ++b)
+            for (int q = 0; q < 4; ++q) {
+                std::vector<int> v(neg.begin() + b * N + q * 64, neg.begin() + b * N + q * 64 + 64);
+                if (sorted) std::sort(v.begin(), v.end());
+                L.ids.insert(L.ids.end(), v.begin(), v.end());
+                L.off.push_back((int)L.ids.size());
+                L.wl.push_back((int)L.wl.size());
+            }
+        run(sorted ? "rowmajor-sorted (4 waves per batch row)" : "rowmajor (4 waves per batch row)", L, tab, ROWF,
+            out, bytes);
+    }
+    const int64_t slice = (E + 7) / 8;
+    for (int sorted = 0; sorted < 2; ++sorted) {
+        for (int spread = 0; spread < 2; ++spread) {
+            // list (b, x) = row b's candidates in entity slice x
+            Lists L;
+            L.off.push_back(0);
+            for (int64_t b = 0; b < B; ++b)
+                for (int x = 0; x < 8; ++x) {
+                    std::vector<int> v;
+                    for (int64_t n = 0; n < N; ++n)
+                        if (neg[b * N + n] / slice == x) v.push_back(neg[b * N + n]);
+                    if (sorted) std::sort(v.begin(), v.end());
+                    L.ids.insert(L.ids.end(), v.begin(), v.end());
+                    L.off.push_back((int)L.ids.size());
+                }
+            // block i: slice x = i % 8, batch rows 4 (i / 8) .. + 3 (spread: slice x = (i / 64) % 8, no XCD affinity)
+            const int nblk = (int)(B / 4 * 8);
+            for (int i = 0; i < nblk; ++i)
+                for (int w = 0; w < 4; ++w) {
+                    const int x = spread ? (i / 64) % 8 : i % 8;
+                    const int grp = spread ? (i % 64) + 64 * (i / 512) : i / 8;
+                    const int b = 4 * grp + w;
+                    L.wl.push_back(b < B ? (int)(b * 8 + x) : -1);
+                }
+            char nm[96];
+            snprintf(nm, sizeof nm, "%s%s", spread ? "slices, no XCD affinity" : "xcd slices",
+                     sorted ? " sorted" : "");
+            run(nm, L, tab, ROWF, out, bytes);
+        }
+    }
+    {
+        // slice x's (b, e) pairs sorted by e, cut into lists of 32 consecutive pairs, dealt to slice x's
+        // XCD: repeat gathers of a row fall in one wave's list (the gather side of an entity-major walk)
+        Lists L;
+        L.off.push_back(0);
+        std::vector<std::vector<int>> per(8);
+        for (int64_t i = 0; i < B * N; ++i) per[neg[i] / slice].push_back(neg[i]);
+        std::vector<std::vector<int>> lists_of(8);
+        for (int x = 0; x < 8; ++x) {
+            std::sort(per[x].begin(), per[x].end());
+            for (size_t c = 0; c < per[x].size(); c += 32) {
+                lists_of[x].push_back((int)L.off.size() - 1);
+                const size_t e = std::min(per[x].size(), c + 32);
+                L.ids.insert(L.ids.end(), per[x].begin() + c, per[x].begin() + e);
+                L.off.push_back((int)L.ids.size());
+            }
+        }
+        size_t mx = 0;
+        for (int x = 0; x < 8; ++x) mx = std::max(mx, lists_of[x].size());
+        const int nblk = (int)(8 * ((mx + 3) / 4));
+        for (int i = 0; i < nblk; ++i)
+            for (int w = 0; w < 4; ++w) {
+                const size_t k = 4 * (size_t)(i / 8) + w;
+                const int x = i % 8;
+                L.wl.push_back(k < lists_of[x].size() ? lists_of[x][k] : -1);
+            }
+        run("xcd slices, entity-sorted chunks of 32", L, tab, ROWF, out, bytes);
+    }
+    {
+        // entity-major with queries: (e, b) pairs of entity slice x (x = XCD group, or spread), sorted by
+        // e, in lists of 32 pairs that never split an entity's run unless it is longer than 32
+        float *qbuf, *rel;
+        CHECK(hipMalloc(&qbuf, (size_t)B * 2000 * 4));
+        CHECK(hipMalloc(&rel, (size_t)11 * 1000 * 4));
+        CHECK(hipMemcpy(qbuf, h.data(), (size_t)B * 2000 * 4, hipMemcpyHostToDevice));
+        CHECK(hipMemcpy(rel, h.data(), (size_t)11 * 1000 * 4, hipMemcpyHostToDevice));
+        for (int halves : {1, 2}) {
+            // halves = 2: slice group = (batch half, entity quarter): each XCD sees 256 batch rows' queries
+            const int nsl = 8 / halves;
+            const int64_t sl = (E + nsl - 1) / nsl;
+            std::vector<std::vector<std::pair<int, int>>> per(8);
+            for (int64_t i = 0; i < B * N; ++i) {
+                const int e = neg[i], b = (int)(i / N);
+                const int x = (int)(e / sl) + nsl * (halves == 2 ? (b >= B / 2) : 0);
+                per[x].push_back({e, b});
+            }
+            std::vector<int> off{0}, pe, pb;
+            std::vector<std::vector<int>> lists_of(8);
+            for (int x = 0; x < 8; ++x) {
+                std::sort(per[x].begin(), per[x].end());
+                size_t c = 0;
+                while (c < per[x].size()) {
+                    size_t e = std::min(per[x].size(), c + 32);
+                    while (e < per[x].size() && e > c + 1 && per[x][e].first == per[x][e - 1].first && e - c > 24) --e;
+                    lists_of[x].push_back((int)off.size() - 1);
+                    for (size_t k = c; k < e; ++k) {
+                        pe.push_back(per[x][k].first);
+                        pb.push_back(per[x][k].second);
+                    }
+                    off.push_back((int)pe.size());
+                    c = e;
+                }
+            }
+            size_t mx = 0;
+            for (int x = 0; x < 8; ++x) mx = std::max(mx, lists_of[x].size());
+            std::vector<int> wl;
+            const int nblk = (int)(8 * ((mx + 3) / 4));
+            for (int i = 0; i < nblk; ++i)
+                for (int w = 0; w < 4; ++w) {
+                    const size_t k = 4 * (size_t)(i / 8) + w;
+                    wl.push_back(k < lists_of[i % 8].size() ? lists_of[i % 8][k] : -1);
+                }
+            int *doff, *dpe, *dpb, *dwl;
+            CHECK(hipMalloc(&doff, off.size() * 4));
+            CHECK(hipMalloc(&dpe, pe.size() * 4));
+            CHECK(hipMalloc(&dpb, pb.size() * 4));
+            CHECK(hipMalloc(&dwl, wl.size() * 4));
+            CHECK(hipMemcpy(doff, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+            CHECK(hipMemcpy(dpe, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+            CHECK(hipMemcpy(dpb, pb.data(), pb.size() * 4, hipMemcpyHostToDevice));
+            CHECK(hipMemcpy(dwl, wl.data(), wl.size() * 4, hipMemcpyHostToDevice));
+            const int nw = (int)wl.size(), blocks = (nw + 3) / 4;
+            hipEvent_t a, bb;
+            CHECK(hipEventCreate(&a));
+            CHECK(hipEventCreate(&bb));
+            for (int i = 0; i < 3; ++i)
+                hipLaunchKernelGGL(gather_pairs, dim3(blocks), dim3(256), 0, 0, tab, qbuf, rel, doff, dpe, dpb, dwl, nw, out);
+            CHECK(hipEventRecord(a));
+            for (int i = 0; i < 20; ++i)
+                hipLaunchKernelGGL(gather_pairs, dim3(blocks), dim3(256), 0, 0, tab, qbuf, rel, doff, dpe, dpb, dwl, nw, out);
+            CHECK(hipEventRecord(bb));
+            CHECK(hipEventSynchronize(bb));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, a, bb));
+            ms /= 20;
+            printf("%-44s %8.1f us  %7.0f GB/s (gathered bytes)\n",
+                   halves == 1 ? "entity-major + 12 KB query/pair, 8 slices" : "entity-major + query, 2 halves x 4 slices",
+                   ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+        }
+    }
+    return 0;
+}

@@ -761,6 +761,18 @@ int kge_gemm_nt(const float* A, int64_t lda, const float* Bm, int64_t ldb, float
     return check_launch("kge_gemm_nt");
 }
 
+int kge_gemm_nt_bf16x3(const float* A, int64_t lda, const float* Bm, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                      int64_t N, int64_t K, void* stream) {
+    if (M < 0 || N < 0 || K < 0) return fail(KGE_EINVAL, "bad shape");
+    if (M == 0 || N == 0) return ok();
+    if (!A || !Bm || !C) return fail(KGE_EINVAL, "null pointer");
+    if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return fail(KGE_EINVAL, "shape exceeds int32");
+    if (K % 4 || lda % 4 || ldb % 4 || !aligned(A, 16) || !aligned(Bm, 16))
+        return fail(KGE_ENOTSUP, "kge_gemm_nt_bf16x3 needs K, lda, ldb multiples of 4 and 16-byte aligned A, B");
+    launch_gemm_nt_f32x3(A, Bm, C, (int)M, (int)N, (int)K, lda, ldb, ldc, (hipStream_t)stream);
+    return check_launch("kge_gemm_nt_bf16x3");
+}
+
 int kge_rank_filtered(const float* scores, int64_t M, int64_t N, int64_t ld, const int64_t* truth,
                       const int64_t* filter_ptr, const int64_t* filter_ids, int64_t* ranks, void* stream) {
     if (M < 0 || N < 0) return fail(KGE_EINVAL, "bad shape");

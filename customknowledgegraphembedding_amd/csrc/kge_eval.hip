@@ -173,6 +173,136 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __rest
 }
 
 // ---------------------------------------------------------------------------------------------
+// fp32-accurate GEMM on the bf16 matrix cores: bf16x3 split, six products.
+// Each fp32 operand x is split into three bf16 terms x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0),
+// x2 = bf16(x - x0 - x1); round-to-nearest-even; 24 significant bits, |x - x0 - x1 - x2| <= 2^-27 |x|),
+// and A.B^T = sum of the six products Ai.Bj^T with i + j <= 2 (the three dropped ones are each
+// <= 2^-26 |a||b| per term). v_mfma_f32_32x32x16_bf16 forms the bf16 products exactly and accumulates
+// in fp32: the result is as close to the fp64 product as the fp32 MFMA path's (tests/test_eval_gpu.py),
+// at 6 x 32 = 192 MFMA cycles per 16 k against 8 x 64 = 512 for v_mfma_f32_32x32x2_f32.
+// ---------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int XBM = 128;
+
+// The split is done on the fly: A and B tiles are staged through LDS as fp32, and each lane converts its
+// fragment values to the three bf16 terms in registers (v_cvt_pk_bf16_f32, RNE) right before the MFMAs
+// (pre-split bf16 planes staged instead moved 6 B per element and measured 1190 us against 920 us at C5). Block 128 x 128, 4 waves
+// of 64 x 64, K in chunks of 32 double-buffered (LDS rows of 34 dwords: the ds_read_b64 fragment reads of
+// 32 rows hit 32 distinct bank pairs; 70 KB per block, 2 blocks per CU). Non-finite inputs give NaN.
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+constexpr int YBK = 32, YLD = 34;
+
+__device__ __forceinline__ void split3(const f32x8& v, bf16x8& a0, bf16x8& a1, bf16x8& a2) {
+    a0 = __builtin_convertvector(v, bf16x8);
+    const f32x8 r1 = v - __builtin_convertvector(a0, f32x8);
+    a1 = __builtin_convertvector(r1, bf16x8);
+    a2 = __builtin_convertvector(r1 - __builtin_convertvector(a1, f32x8), bf16x8);
+}
+
+__global__ __launch_bounds__(kBlock) void gemm_nt_f32x3_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
+                                                               float* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                               int64_t ldb, int64_t ldc) {
+    __shared__ __attribute__((aligned(16))) float As[2][XBM * YLD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][XBM * YLD];
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int ntn = (N + XBM - 1) / XBM, ntm = (M + XBM - 1) / XBM;
+    const int nblk = ntn * ntm;
+    int bid = blockIdx.x;
+    {  // XCD-aware bijective remap: each XCD walks a contiguous run of N tiles (entity rows)
+        const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    }
+    const int tn = bid / ntm, tm = bid % ntm;
+    const int m0 = tm * XBM, n0 = tn * XBM;
+    // staging: float4 f = t + 256 u (u < 4) of each 128 x 32 tile: row f >> 3, k 4 (f & 7)
+    float4 ra[4], rb[4];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int f = t + kBlock * u, row = f >> 3, k = k0 + 4 * (f & 7);
+            const int gm = m0 + row, gn = n0 + row;
+            ra[u] = (gm < M && k < K) ? *reinterpret_cast<const float4*>(A + (int64_t)gm * lda + k)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+            rb[u] = (gn < N && k < K) ? *reinterpret_cast<const float4*>(Bm + (int64_t)gn * ldb + k)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int f = t + kBlock * u, o = (f >> 3) * YLD + 4 * (f & 7);
+            *reinterpret_cast<float2*>(&As[buf][o]) = make_float2(ra[u].x, ra[u].y);
+            *reinterpret_cast<float2*>(&As[buf][o + 2]) = make_float2(ra[u].z, ra[u].w);
+            *reinterpret_cast<float2*>(&Bs[buf][o]) = make_float2(rb[u].x, rb[u].y);
+            *reinterpret_cast<float2*>(&Bs[buf][o + 2]) = make_float2(rb[u].z, rb[u].w);
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nk = (K + YBK - 1) / YBK;
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    const int r32 = lane & 31, half = lane >> 5;
+    constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+    for (int kc = 0; kc < nk; ++kc) {
+        const int buf = kc & 1;
+        if (kc + 1 < nk) gload((kc + 1) * YBK);  // next chunk in flight during the MFMAs
+#pragma unroll
+        for (int s = 0; s < YBK / 16; ++s) {
+            bf16x8 a[2][3], b[2][3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float* pa = &As[buf][(wm * 64 + i * 32 + r32) * YLD + 16 * s + 8 * half];
+                const float* pb = &Bs[buf][(wn * 64 + i * 32 + r32) * YLD + 16 * s + 8 * half];
+                f32x8 va, vb;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float2 x = *reinterpret_cast<const float2*>(pa + 2 * q);
+                    const float2 y = *reinterpret_cast<const float2*>(pb + 2 * q);
+                    va[2 * q] = x.x;
+                    va[2 * q + 1] = x.y;
+                    vb[2 * q] = y.x;
+                    vb[2 * q + 1] = y.y;
+                }
+                split3(va, a[i][0], a[i][1], a[i][2]);
+                split3(vb, b[i][0], b[i][1], b[i][2]);
+            }
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] =
+                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][PA[q]], b[j][PB[q]], acc[i][j], 0, 0, 0);
+        }
+        if (kc + 1 < nk) {
+            sstore(buf ^ 1);
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int gn = n0 + wn * 64 + j * 32 + r32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (gm < M && gn < N) C[(int64_t)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Filtered rank of the true entity in each score row (one block per query row):
 //   rank = 1 + #{ e != true : S[e] > S[true] } - #{ f in filt[q], f != true : S[f] > S[true] }
 // The filter list of a row must hold distinct ids (the host dedups). Integer counts: exact.
@@ -252,6 +382,14 @@ int launch_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K
     else
         hipLaunchKernelGGL(gemm_nt_f32_kernel<128>, dim3((unsigned)t128), dim3(kBlock), 0, st, A, B, C, M, N, K, lda,
                            ldb, ldc);
+    return 0;
+}
+
+int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                         int64_t ldc, hipStream_t st) {
+    const int64_t tiles = (int64_t)((M + XBM - 1) / XBM) * ((N + XBM - 1) / XBM);
+    hipLaunchKernelGGL(gemm_nt_f32x3_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, st, A, B, C, M, N, K, lda, ldb,
+                       ldc);
     return 0;
 }
 

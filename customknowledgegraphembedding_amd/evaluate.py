@@ -4,7 +4,8 @@ triple and mode, a candidate list over every entity in which the other true trip
 the positive with bias -1; ranks come from argsort). BASELINE config C5.
 
 The scores of a query batch against all E entities are computed on the GPU:
-  * DistMult / ComplEx: S = Q . E^T on the fp32 matrix cores (kge_eval_query + kge_gemm_nt);
+  * DistMult / ComplEx: S = Q . E^T at fp32 accuracy on the bf16 matrix cores (kge_eval_query +
+    kge_gemm_nt_bf16x3: bf16x3 split in registers, six products, fp32 accumulation);
   * every other score function: the fused VALU scorer with candidate ids 0..E-1 (row stride 0).
 Ranks are exact integers from kge_rank_filtered: rank = 1 + #(unfiltered e != truth with
 s_e > s_truth). Ties count in the positive's favour; upstream's unstable argsort leaves them
@@ -73,8 +74,9 @@ def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor
         check(lib.kge_eval_query(FN_IDS[model.model_name], m, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(),
                                  rel.shape[0], rel.stride(0), positive_sample.data_ptr(), B, model._D, Q.data_ptr(),
                                  Q.stride(0), st), "kge_eval_query")
-        check(lib.kge_gemm_nt(Q.data_ptr(), Q.stride(0), ent.data_ptr(), ent.stride(0), out.data_ptr(), out.stride(0),
-                              B, E, K, st), "kge_gemm_nt")
+        # S = Q . E^T at fp32 accuracy on the bf16 matrix cores (bf16x3 split in registers, six products)
+        check(lib.kge_gemm_nt_bf16x3(Q.data_ptr(), Q.stride(0), ent.data_ptr(), ent.stride(0), out.data_ptr(),
+                                     out.stride(0), B, E, K, st), "kge_gemm_nt_bf16x3")
         return out
     cand = torch.arange(E, device=dev, dtype=torch.int64).unsqueeze(0).expand(B, E)  # row stride 0
     modulus = float(model.modulus.reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0

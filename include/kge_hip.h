@@ -173,6 +173,15 @@ int kge_eval_query(int fn, int mode,
                    float* Q, int64_t ldq, void* stream);
 int kge_gemm_nt(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                 int64_t M, int64_t N, int64_t K, void* stream);
+/*
+ * kge_gemm_nt_bf16x3: the same contraction (arguments as kge_gemm_nt) at fp32 accuracy on the bf16 matrix
+ *   cores: each fp32 operand is split in registers into three bf16 terms x = x0 + x1 + x2 (RNE, 24
+ *   significant bits) and C = sum of the six products A_i . B_j^T with i + j <= 2 (v_mfma_f32_32x32x16_bf16,
+ *   fp32 accumulation). Error vs the fp64 product: the fp32 MFMA path's (tests/test_eval_gpu.py).
+ *   Non-finite inputs give NaN.
+ */
+int kge_gemm_nt_bf16x3(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                       int64_t M, int64_t N, int64_t K, void* stream);
 int kge_rank_filtered(const float* scores, int64_t M, int64_t N, int64_t ld, const int64_t* truth,
                       const int64_t* filter_ptr, const int64_t* filter_ids, int64_t* ranks,
                       void* stream);

@@ -39,6 +39,50 @@ def test_gemm_asymmetric_identity_layout():
     assert torch.equal(C, Bm.T.contiguous())  # I . B^T is exact in a k-ordered fma chain
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 1, 4), (37, 300, 64), (128, 128, 16), (129, 257, 1000), (1024, 1500, 2000),
+                                   (5, 14951, 1000), (300, 131, 12), (64, 64, 36)])
+def test_gemm_nt_bf16x3_matches_fp32_accuracy(M, N, K):
+    """kge_gemm_nt_bf16x3 (fp32 operands split into three bf16 terms in registers, six products on the bf16
+    MFMA) is as close to the fp64 product as the fp32 MFMA GEMM: per element |C - C64| <= 4e-7 * sum_k |a b|
+    (the fp32 path's bound is ~1.5e-7), and never more than 3x the fp32 path's worst error + 1e-7."""
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64) * torch.logspace(-2, 2, K, dtype=torch.float64)
+    Bm = torch.randn(N, K, generator=g, dtype=torch.float64)
+    a, b = A.float().to(DEV), Bm.float().to(DEV)
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    C = torch.empty(M, N, device=DEV)
+    assert lib.kge_gemm_nt_bf16x3(a.data_ptr(), K, b.data_ptr(), K, C.data_ptr(), N, M, N, K, st) == 0
+    ref = a.double().cpu() @ b.double().cpu().T
+    scale = (a.double().cpu().abs() @ b.double().cpu().abs().T).clamp_min(1e-30)
+    err_x3 = float(((C.double().cpu() - ref).abs() / scale).max())
+    assert err_x3 <= 4e-7, err_x3
+    C32 = torch.empty(M, N, device=DEV)
+    assert lib.kge_gemm_nt(a.data_ptr(), K, b.data_ptr(), K, C32.data_ptr(), N, M, N, K, st) == 0
+    err_32 = float(((C32.double().cpu() - ref).abs() / scale).max())
+    assert err_x3 <= 3 * err_32 + 1e-7, (err_x3, err_32)
+
+
+def test_gemm_bf16x3_asymmetric_identity_layout():
+    """A = I with an asymmetric B catches a transposed C write or a swapped k half (guide §3)."""
+    K = 48
+    A = torch.eye(64, K, device=DEV)
+    Bm = torch.arange(200 * K, dtype=torch.float32, device=DEV).reshape(200, K) % 97
+    C = torch.empty(64, 200, device=DEV)
+    assert _lib.load().kge_gemm_nt_bf16x3(A.data_ptr(), K, Bm.data_ptr(), K, C.data_ptr(), 200, 64, 200, K,
+                                          torch.cuda.current_stream().cuda_stream) == 0
+    want = torch.zeros(64, 200, device=DEV)
+    want[:K] = Bm.T  # row m < K of I . B^T is column m of B^T, exact
+    assert torch.equal(C, want)
+
+
+def test_gemm_bf16x3_rejects_unaligned_k():
+    a = torch.zeros(4, 6, device=DEV)
+    rc = _lib.load().kge_gemm_nt_bf16x3(a.data_ptr(), 6, a.data_ptr(), 6, a.data_ptr(), 4, 4, 4, 6,
+                                        torch.cuda.current_stream().cuda_stream)
+    assert rc != 0 and b"multiples of 4" in _lib.load().kge_last_error()
+
+
 CFG = {"DistMult": (False, False, False), "ComplEx": (True, True, False), "TransE": (False, False, False),
        "RotatE": (True, False, False), "InterHT": (True, False, True), "pRotatE": (False, False, False)}
 

@@ -190,6 +190,19 @@ __device__ __forceinline__ float sigmoidf(float x) {
     return e / (1.f + e);
 }
 
+// fp32 -> three bf16 terms, x = x0 + x1 + x2 to 24 significant bits (RNE v_cvt_pk_bf16_f32 each): the
+// operand form of the fp32-accurate products on the bf16 matrix cores (kge_eval.hip, kge_transparse.hip).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split3_bf16(const f32x8& v, bf16x8& a0, bf16x8& a1, bf16x8& a2) {
+    a0 = __builtin_convertvector(v, bf16x8);
+    const f32x8 r1 = v - __builtin_convertvector(a0, f32x8);
+    a1 = __builtin_convertvector(r1, bf16x8);
+    a2 = __builtin_convertvector(r1 - __builtin_convertvector(a1, f32x8), bf16x8);
+}
+// the six products A_i . B_j (i + j <= 2), smallest first
+constexpr int kX3A[6] = {2, 1, 0, 1, 0, 0}, kX3B[6] = {0, 1, 2, 0, 1, 0};
+
 // One Adam update (supervisor.py:26; run.py:111 Keras Adam, or torch.optim.Adam), shared by the
 // dense optimizer kernel and the fused backward so both give bitwise-identical results.
 //   keras: m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2); p -= m * alpha / (sqrt(v) + eps)

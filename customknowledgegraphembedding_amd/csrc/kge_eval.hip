@@ -181,7 +181,6 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32_kernel(const float* __rest
 // in fp32: the result is as close to the fp64 product as the fp32 MFMA path's (tests/test_eval_gpu.py),
 // at 6 x 32 = 192 MFMA cycles per 16 k against 8 x 64 = 512 for v_mfma_f32_32x32x2_f32.
 // ---------------------------------------------------------------------------------------------
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int XBM = 128;
 
 // The split is done on the fly: A and B tiles are staged through LDS as fp32, and each lane converts its
@@ -189,15 +188,7 @@ constexpr int XBM = 128;
 // (pre-split bf16 planes staged instead moved 6 B per element and measured 1190 us against 920 us at C5). Block 128 x 128, 4 waves
 // of 64 x 64, K in chunks of 32 double-buffered (LDS rows of 34 dwords: the ds_read_b64 fragment reads of
 // 32 rows hit 32 distinct bank pairs; 70 KB per block, 2 blocks per CU). Non-finite inputs give NaN.
-typedef float f32x8 __attribute__((ext_vector_type(8)));
 constexpr int YBK = 32, YLD = 34;
-
-__device__ __forceinline__ void split3(const f32x8& v, bf16x8& a0, bf16x8& a1, bf16x8& a2) {
-    a0 = __builtin_convertvector(v, bf16x8);
-    const f32x8 r1 = v - __builtin_convertvector(a0, f32x8);
-    a1 = __builtin_convertvector(r1, bf16x8);
-    a2 = __builtin_convertvector(r1 - __builtin_convertvector(a1, f32x8), bf16x8);
-}
 
 __global__ __launch_bounds__(kBlock) void gemm_nt_f32x3_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
                                                                float* __restrict__ C, int M, int N, int K, int64_t lda,
@@ -251,7 +242,6 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32x3_kernel(const float* __re
     sstore(0);
     __syncthreads();
     const int r32 = lane & 31, half = lane >> 5;
-    constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
         if (kc + 1 < nk) gload((kc + 1) * YBK);  // next chunk in flight during the MFMAs
@@ -272,8 +262,8 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32x3_kernel(const float* __re
                     vb[2 * q] = y.x;
                     vb[2 * q + 1] = y.y;
                 }
-                split3(va, a[i][0], a[i][1], a[i][2]);
-                split3(vb, b[i][0], b[i][1], b[i][2]);
+                split3_bf16(va, a[i][0], a[i][1], a[i][2]);
+                split3_bf16(vb, b[i][0], b[i][1], b[i][2]);
             }
 #pragma unroll
             for (int q = 0; q < 6; ++q)
@@ -282,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void gemm_nt_f32x3_kernel(const float* __re
 #pragma unroll
                     for (int j = 0; j < 2; ++j)
                         acc[i][j] =
-                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][PA[q]], b[j][PB[q]], acc[i][j], 0, 0, 0);
+                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], b[j][kX3B[q]], acc[i][j], 0, 0, 0);
         }
         if (kc + 1 < nk) {
             sstore(buf ^ 1);

@@ -142,11 +142,10 @@ __device__ __forceinline__ int acc_row(int wm, int i, int r, int half) {
 // ---------------------------------------------------------------------------------------------
 // Row-block kernel: forward scores (TS_FWD), dL/dp rows (TS_GP) or dL/dh rows (TS_DH).
 // ---------------------------------------------------------------------------------------------
-template <int OP, int VEC>
-__global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
-    constexpr int BLD = OP == TS_DH ? ALD : TLD;  // TS_DH stages M_r transposed like A
-    __shared__ __attribute__((aligned(16))) float As[2][TBK][ALD];
-    __shared__ __attribute__((aligned(16))) float Bs[2][TBK][BLD];
+template <int OP, int VEC, bool X3 = false>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(X3 ? 2 : 1))) void
+ts_rows_kernel(TsParams p) {
+    static_assert(!X3 || (OP == TS_FWD && VEC == 4), "the bf16x3 form is the forward with float4 rows");
     __shared__ const float* rowp[TBM];
     __shared__ int rb[TBM], rn[TBM];  // (b, n) of each row; rb = -1 for padding rows
     __shared__ float2 red[TBM];
@@ -255,58 +254,6 @@ __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
     const float* Mr = (rok && !p.Mpre) ? p.mask + r * (int64_t)d * d : nullptr;
     __syncthreads();
 
-    // ---- staging --------------------------------------------------------------------------------
-    // A (rows): 128 rows x TBK k, NU float4 per thread, transposed into As[k][row].
-    // B: FWD/GP: M_r[k][col] row segments (natural k-major); DH: M_r[col][k] (transposed like A).
-    // thread t, unit u: A row = (t >> 3) + 32 u, k offset (t & 7) * 4; B k row = (t >> 5) + 8 u, col (t & 31) * 4
-    const int akq = (t & 7) * 4, bjq = (t & 31) * 4;
-    const float* arow[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) arow[u] = rowp[(t >> 3) + 32 * u];
-    float4 ra[NU], rbv[NU];
-    auto gload = [&](int ct, int k0) {
-        const int ka = k0 + akq;
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            ra[u] = arow[u] ? ld4<VEC>(arow[u], ka, d - ka) : make_float4(0.f, 0.f, 0.f, 0.f);
-            if constexpr (OP == TS_DH) {
-                const int c = ct * TBN + (t >> 3) + 32 * u;
-                if (Wr && c < d) {
-                    const int64_t off = (int64_t)c * d + ka;
-                    rbv[u] = Mr ? mul4(ld4<VEC>(Wr, off, d - ka), ld4<VEC>(Mr, off, d - ka)) : ld4<VEC>(Wr, off, d - ka);
-                } else {
-                    rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-            } else {
-                const int kb = k0 + (t >> 5) + 8 * u, j = ct * TBN + bjq;
-                if (Wr && kb < d) {
-                    const int64_t off = (int64_t)kb * d + j;
-                    rbv[u] = Mr ? mul4(ld4<VEC>(Wr, off, d - j), ld4<VEC>(Mr, off, d - j)) : ld4<VEC>(Wr, off, d - j);
-                } else {
-                    rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-            }
-        }
-    };
-    auto sstore = [&](int buf) {
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int ar = (t >> 3) + 32 * u;
-            As[buf][akq + 0][ar] = ra[u].x;
-            As[buf][akq + 1][ar] = ra[u].y;
-            As[buf][akq + 2][ar] = ra[u].z;
-            As[buf][akq + 3][ar] = ra[u].w;
-            if constexpr (OP == TS_DH) {
-                Bs[buf][akq + 0][ar] = rbv[u].x;
-                Bs[buf][akq + 1][ar] = rbv[u].y;
-                Bs[buf][akq + 2][ar] = rbv[u].z;
-                Bs[buf][akq + 3][ar] = rbv[u].w;
-            } else {
-                *reinterpret_cast<float4*>(&Bs[buf][(t >> 5) + 8 * u][bjq]) = rbv[u];
-            }
-        }
-    };
-
     // wave w: rows [32 w, 32 w + 32) x all 128 columns of the tile (four 32 x 32 MFMA accumulators);
     // C/D map: row = 32 w + (r & 3) + 8 (r >> 2) + 4 (lane >> 5), column = 32 j + (lane & 31)
     f32x16 acc[4];
@@ -323,80 +270,220 @@ __global__ __launch_bounds__(kBlock) void ts_rows_kernel(TsParams p) {
     const int nrows = s_rows;
     const int nk = (d + TBK - 1) / TBK, nct = (d + TBN - 1) / TBN;
     const int iters = nk * nct;
-    gload(0, 0);
-    sstore(0);
-    __syncthreads();
-    for (int it = 0; it < iters; ++it) {
-        const int buf = it & 1;
-        const int ct = it / nk, kc = it - ct * nk;
-        if (it + 1 < iters) {
-            const int ct1 = (it + 1) / nk;
-            gload(ct1, ((it + 1) - ct1 * nk) * TBK);
+    // folds a finished column tile into the per-row sums of p^2 and |p c| (forward)
+    auto fold = [&](int ct) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int cg = ct * TBN + j * 32 + col;
+            const float c = cg < d ? cs[cg] : 0.f;
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) {
+                const float v = acc[j][r2];
+                sq[r2] = fmaf(v, v, sq[r2]);
+                ab[r2] += fabsf(v * c);
+                acc[j][r2] = 0.f;
+            }
         }
-#pragma unroll
-        for (int s2 = 0; s2 < TBK / 2; ++s2) {
-            const int kk = 2 * s2 + half;
-            const float a = As[buf][kk][wave * 32 + col];
-            float bv[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bv[j] = Bs[buf][kk][j * 32 + col];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv[j], acc[j], 0, 0, 0);
-        }
-        if (kc == nk - 1) {
-            if constexpr (OP == TS_FWD) {
-                // fold the column tile into the per-row sums
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int cg = ct * TBN + j * 32 + col;
-                    const float c = cg < d ? cs[cg] : 0.f;
-#pragma unroll
-                    for (int r2 = 0; r2 < 16; ++r2) {
-                        const float v = acc[j][r2];
-                        sq[r2] = fmaf(v, v, sq[r2]);
-                        ab[r2] += fabsf(v * c);
-                        acc[j][r2] = 0.f;
-                    }
+    };
+    if constexpr (X3) {
+        // ---- bf16x3 forward: P = H . M_r at fp32 accuracy on v_mfma_f32_32x32x16_bf16 ------------------
+        // Each fp32 fragment value is split in registers into three bf16 terms (split3_bf16) and the six
+        // products with i + j <= 2 accumulate in fp32 (kge_gemm_nt_bf16x3's numerics). LDS images hold the
+        // tiles with k contiguous per row / per column (rows of 34 dwords: a fragment read, ds_read_b64 x 4 of
+        // 32 rows, hits 32 distinct bank pairs): A = the 128 gathered rows [row][k]; B = the M_r tile stored
+        // transposed [col][k] (lane l stages k = l & 31, so the transposing ds_write_b32 are conflict-free).
+        constexpr int XLD = 34;
+        __shared__ __attribute__((aligned(16))) float Ax[2][TBM * XLD];
+        __shared__ __attribute__((aligned(16))) float Bx[2][TBN * XLD];
+        const float* arow[NU];
+    #pragma unroll
+        for (int u = 0; u < NU; ++u) arow[u] = rowp[(t + kBlock * u) >> 3];
+        float4 ra[NU], rbv[NU];
+        auto gload = [&](int ct, int k0) {
+    #pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int f = t + kBlock * u, ka = k0 + 4 * (f & 7);
+                ra[u] = arow[u] ? ld4<4>(arow[u], ka, d - ka) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const int kb = k0 + (lane & 31), j = ct * TBN + 4 * ((lane >> 5) + 2 * (wave + 4 * u));
+                if (Wr && kb < d) {
+                    const int64_t off = (int64_t)kb * d + j;
+                    rbv[u] = Mr ? mul4(ld4<4>(Wr, off, d - j), ld4<4>(Mr, off, d - j)) : ld4<4>(Wr, off, d - j);
+                } else {
+                    rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
-            } else if constexpr (OP == TS_GP) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int cg = ct * TBN + j * 32 + col;
-                    const bool cin = cg < d;
-                    const float c = cin ? cs[cg] : 0.f;
-                    float up = 0.f;
-#pragma unroll
-                    for (int r2 = 0; r2 < 16; ++r2) {
-                        const int m = row_of(r2);
-                        const float v = acc[j][r2];
-                        const float a = sa[m];
-                        if (cin && m < nrows)
-                            p.gp[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = a * (v * sbv[m] - sgnf(v * c) * c);
-                        up += a * fabsf(v);
-                        acc[j][r2] = 0.f;
-                    }
-                    up += __shfl_xor(up, 32, kWave);
-                    if (half == 0) colred[wave][j * 32 + col] = up;
-                }
+            }
+        };
+        auto sstore = [&](int buf) {
+    #pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int f = t + kBlock * u, o = (f >> 3) * XLD + 4 * (f & 7);
+                *reinterpret_cast<float2*>(&Ax[buf][o]) = make_float2(ra[u].x, ra[u].y);
+                *reinterpret_cast<float2*>(&Ax[buf][o + 2]) = make_float2(ra[u].z, ra[u].w);
+                const int kb = lane & 31, cg = 4 * ((lane >> 5) + 2 * (wave + 4 * u));
+                Bx[buf][(cg + 0) * XLD + kb] = rbv[u].x;
+                Bx[buf][(cg + 1) * XLD + kb] = rbv[u].y;
+                Bx[buf][(cg + 2) * XLD + kb] = rbv[u].z;
+                Bx[buf][(cg + 3) * XLD + kb] = rbv[u].w;
+            }
+        };
+        auto frag = [&](const float* base) {
+            f32x8 v;
+    #pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float2 x = *reinterpret_cast<const float2*>(base + 2 * q);
+                v[2 * q] = x.x;
+                v[2 * q + 1] = x.y;
+            }
+            return v;
+        };
+        gload(0, 0);
+        sstore(0);
+        __syncthreads();
+        for (int it = 0; it < iters; ++it) {
+            const int buf = it & 1;
+            const int ct = it / nk, kc = it - ct * nk;
+            if (it + 1 < iters) {
+                const int ct1 = (it + 1) / nk;
+                gload(ct1, ((it + 1) - ct1 * nk) * TBK);
+            }
+    #pragma unroll
+            for (int s2 = 0; s2 < TBK / 16; ++s2) {
+                const int ko = 16 * s2 + 8 * half;
+                bf16x8 a[3], b[4][3];
+                split3_bf16(frag(&Ax[buf][(wave * 32 + col) * XLD + ko]), a[0], a[1], a[2]);
+    #pragma unroll
+                for (int j = 0; j < 4; ++j) split3_bf16(frag(&Bx[buf][(j * 32 + col) * XLD + ko]), b[j][0], b[j][1], b[j][2]);
+    #pragma unroll
+                for (int q = 0; q < 6; ++q)
+    #pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kX3A[q]], b[j][kX3B[q]], acc[j], 0, 0, 0);
+            }
+            if (kc == nk - 1) fold(ct);
+            if (it + 1 < iters) {
+                sstore(buf ^ 1);
                 __syncthreads();
-                if (t < TBN && ct * TBN + t < d)
-                    p.upart[blk * d + ct * TBN + t] = (colred[0][t] + colred[1][t]) + (colred[2][t] + colred[3][t]);
-            } else {  // TS_DH
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int cg = ct * TBN + j * 32 + col;
-#pragma unroll
-                    for (int r2 = 0; r2 < 16; ++r2) {
-                        const int m = row_of(r2);
-                        if (cg < d && m < nrows) p.dh[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = acc[j][r2];
-                        acc[j][r2] = 0.f;
+            }
+        }
+    } else {
+        // ---- staging --------------------------------------------------------------------------------
+        constexpr int BLD = OP == TS_DH ? ALD : TLD;  // TS_DH stages M_r transposed like A
+        __shared__ __attribute__((aligned(16))) float As[2][TBK][ALD];
+        __shared__ __attribute__((aligned(16))) float Bs[2][TBK][BLD];
+        // A (rows): 128 rows x TBK k, NU float4 per thread, transposed into As[k][row].
+        // B: FWD/GP: M_r[k][col] row segments (natural k-major); DH: M_r[col][k] (transposed like A).
+        // thread t, unit u: A row = (t >> 3) + 32 u, k offset (t & 7) * 4; B k row = (t >> 5) + 8 u, col (t & 31) * 4
+        const int akq = (t & 7) * 4, bjq = (t & 31) * 4;
+        const float* arow[NU];
+    #pragma unroll
+        for (int u = 0; u < NU; ++u) arow[u] = rowp[(t >> 3) + 32 * u];
+        float4 ra[NU], rbv[NU];
+        auto gload = [&](int ct, int k0) {
+            const int ka = k0 + akq;
+    #pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                ra[u] = arow[u] ? ld4<VEC>(arow[u], ka, d - ka) : make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (OP == TS_DH) {
+                    const int c = ct * TBN + (t >> 3) + 32 * u;
+                    if (Wr && c < d) {
+                        const int64_t off = (int64_t)c * d + ka;
+                        rbv[u] = Mr ? mul4(ld4<VEC>(Wr, off, d - ka), ld4<VEC>(Mr, off, d - ka)) : ld4<VEC>(Wr, off, d - ka);
+                    } else {
+                        rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                } else {
+                    const int kb = k0 + (t >> 5) + 8 * u, j = ct * TBN + bjq;
+                    if (Wr && kb < d) {
+                        const int64_t off = (int64_t)kb * d + j;
+                        rbv[u] = Mr ? mul4(ld4<VEC>(Wr, off, d - j), ld4<VEC>(Mr, off, d - j)) : ld4<VEC>(Wr, off, d - j);
+                    } else {
+                        rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
                     }
                 }
             }
-        }
-        if (it + 1 < iters) {
-            sstore(buf ^ 1);
-            __syncthreads();
+        };
+        auto sstore = [&](int buf) {
+    #pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int ar = (t >> 3) + 32 * u;
+                As[buf][akq + 0][ar] = ra[u].x;
+                As[buf][akq + 1][ar] = ra[u].y;
+                As[buf][akq + 2][ar] = ra[u].z;
+                As[buf][akq + 3][ar] = ra[u].w;
+                if constexpr (OP == TS_DH) {
+                    Bs[buf][akq + 0][ar] = rbv[u].x;
+                    Bs[buf][akq + 1][ar] = rbv[u].y;
+                    Bs[buf][akq + 2][ar] = rbv[u].z;
+                    Bs[buf][akq + 3][ar] = rbv[u].w;
+                } else {
+                    *reinterpret_cast<float4*>(&Bs[buf][(t >> 5) + 8 * u][bjq]) = rbv[u];
+                }
+            }
+        };
+
+        gload(0, 0);
+        sstore(0);
+        __syncthreads();
+        for (int it = 0; it < iters; ++it) {
+            const int buf = it & 1;
+            const int ct = it / nk, kc = it - ct * nk;
+            if (it + 1 < iters) {
+                const int ct1 = (it + 1) / nk;
+                gload(ct1, ((it + 1) - ct1 * nk) * TBK);
+            }
+    #pragma unroll
+            for (int s2 = 0; s2 < TBK / 2; ++s2) {
+                const int kk = 2 * s2 + half;
+                const float a = As[buf][kk][wave * 32 + col];
+                float bv[4];
+    #pragma unroll
+                for (int j = 0; j < 4; ++j) bv[j] = Bs[buf][kk][j * 32 + col];
+    #pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv[j], acc[j], 0, 0, 0);
+            }
+            if (kc == nk - 1) {
+                if constexpr (OP == TS_FWD) {
+                    fold(ct);
+                } else if constexpr (OP == TS_GP) {
+    #pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int cg = ct * TBN + j * 32 + col;
+                        const bool cin = cg < d;
+                        const float c = cin ? cs[cg] : 0.f;
+                        float up = 0.f;
+    #pragma unroll
+                        for (int r2 = 0; r2 < 16; ++r2) {
+                            const int m = row_of(r2);
+                            const float v = acc[j][r2];
+                            const float a = sa[m];
+                            if (cin && m < nrows)
+                                p.gp[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = a * (v * sbv[m] - sgnf(v * c) * c);
+                            up += a * fabsf(v);
+                            acc[j][r2] = 0.f;
+                        }
+                        up += __shfl_xor(up, 32, kWave);
+                        if (half == 0) colred[wave][j * 32 + col] = up;
+                    }
+                    __syncthreads();
+                    if (t < TBN && ct * TBN + t < d)
+                        p.upart[blk * d + ct * TBN + t] = (colred[0][t] + colred[1][t]) + (colred[2][t] + colred[3][t]);
+                } else {  // TS_DH
+    #pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int cg = ct * TBN + j * 32 + col;
+    #pragma unroll
+                        for (int r2 = 0; r2 < 16; ++r2) {
+                            const int m = row_of(r2);
+                            if (cg < d && m < nrows) p.dh[((int64_t)rb[m] * p.N + rn[m]) * d + cg] = acc[j][r2];
+                            acc[j][r2] = 0.f;
+                        }
+                    }
+                }
+            }
+            if (it + 1 < iters) {
+                sstore(buf ^ 1);
+                __syncthreads();
+            }
         }
     }
 
@@ -734,6 +821,18 @@ template <int OP>
 void launch_rows(const TsParams& p, hipStream_t st) {
     const unsigned blocks = (unsigned)row_blocks(p);
     const size_t lds = OP == TS_DH ? 0 : (size_t)p.d * sizeof(float);
+    if constexpr (OP == TS_FWD) {
+        // the forward runs the bf16x3 form (fp32 accuracy, 2.67x the fp32 MFMA rate) when rows take float4s;
+        // KGE_TS_F32=1 forces the fp32 MFMA form (A/B runs)
+        static const bool f32 = [] {
+            const char* e = getenv("KGE_TS_F32");
+            return e && e[0] == '1';
+        }();
+        if (use_v4(p) && !f32) {
+            hipLaunchKernelGGL((ts_rows_kernel<OP, 4, true>), dim3(blocks), dim3(kBlock), lds, st, p);
+            return;
+        }
+    }
     if (use_v4(p))
         hipLaunchKernelGGL((ts_rows_kernel<OP, 4>), dim3(blocks), dim3(kBlock), lds, st, p);
     else

@@ -308,7 +308,20 @@ __global__ __launch_bounds__(kBlock) void rank_kernel(const float* __restrict__ 
     const bool tok = tr >= 0 && tr < N;
     const float st = tok ? row[tr] : -INFINITY;
     unsigned long long cnt = 0;
-    for (int64_t e = threadIdx.x; e < N; e += kBlock) cnt += (e != tr && row[e] > st) ? 1ull : 0ull;
+    // a scalar head up to the first 16-B boundary, 16-B loads for the body, a scalar tail (the true
+    // entity's own score is never > st, so the body needs no e != tr test)
+    const int64_t head = min<int64_t>(N, (int64_t)((16 - ((uintptr_t)row & 15)) & 15) / 4);
+    const int64_t nv = (N - head) / 4;
+    for (int64_t e = threadIdx.x; e < head; e += kBlock) cnt += (e != tr && row[e] > st) ? 1ull : 0ull;
+    {
+        const rsrc_t rs = make_rsrc(row + head, (uint32_t)(nv * 16));
+        for (int64_t g = threadIdx.x; g < nv; g += kBlock) {
+            const vecf<4> v = bload<4>(rs, (uint32_t)(g * 16));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cnt += v.a[i] > st ? 1ull : 0ull;
+        }
+    }
+    for (int64_t e = head + nv * 4 + threadIdx.x; e < N; e += kBlock) cnt += (e != tr && row[e] > st) ? 1ull : 0ull;
     if (fptr) {
         for (int64_t i = fptr[q] + threadIdx.x; i < fptr[q + 1]; i += kBlock) {
             const int64_t f = fids[i];

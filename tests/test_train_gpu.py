@@ -231,9 +231,12 @@ def test_one_call_train_step_matches_split_path(name, d):
         assert float((x - y).abs().max()) <= 1e-4 * scale, name
 
 
-def test_one_call_train_step_matches_oracle_tf_step():
-    """kge_train_step against the oracle's fp64 TF-semantics step (loss graph + Keras Adam)."""
-    name, E, R, d, B, N, gamma, lr = "InterHT", 60, 4, 200, 6, 24, 12.0, 1e-3
+@pytest.mark.parametrize("E,B,N", [(60, 6, 24), (12, 48, 200), (3, 40, 160)])
+def test_one_call_train_step_matches_oracle_tf_step(E, B, N):
+    """kge_train_step against the oracle's fp64 TF-semantics step (loss graph + Keras Adam). E = 12 puts
+    ~800 events in each entity bucket (phase 2's block-wide LDS sort), E = 3 ~2 200 (past the sort's 2 048:
+    the ordered-extraction fallback)."""
+    name, R, d, gamma, lr = "InterHT", 4, 200, 12.0, 1e-3
     m = kge.TFKGEModel(name, E, R, d, gamma, double_entity_embedding=True, triple_relation_embedding=True,
                        device=DEV, seed=13)
     ent = m.entity_embedding.detach().cpu().double()

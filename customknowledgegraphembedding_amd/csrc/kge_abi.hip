@@ -462,7 +462,7 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM || kind == KIND_STEP_FWD ||
                kind == KIND_STEP_FWD_STATS || kind == KIND_STEP_FWD_GRAD || kind == KIND_SHARD_FWD_GRAD) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
-    } else if (kind == KIND_STEP_FWD_XCD) {
+    } else if (kind == KIND_STEP_FWD_XCD || kind == KIND_SCORE_SHARD_XCD) {
         waves = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock * 8;  // 8 slice blocks per 4 rows
     } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS) {
         waves = p.B;  // one wave per slot
@@ -706,6 +706,9 @@ int kge_score_sharded(int fn, int mode, const float* qent, int64_t q_ld, const f
     p.skip_foreign = 1;
     p.out = scores;
     p.out_ld = scores_ld;
+    if (mode != KGE_SINGLE && shard_lo >= 0 && shard_lo + shard_rows < ((int64_t)1 << 31) &&
+        use_xcd_order(shard_rows, N))
+        return run_score(fn, mode, p, KIND_SCORE_SHARD_XCD, stream);  // XCD-sliced order over the shard
     return run_score(fn, mode, p, KIND_FWD, stream);
 }
 

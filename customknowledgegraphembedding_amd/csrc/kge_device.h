@@ -629,9 +629,12 @@ __device__ __forceinline__ void score_owned(const ScoreParams& p, const Query<FN
 // take_invalid, every id outside [0, c_rows), which scores against a zero row) into lanes; calls
 // body(id32, n, cnt) with up to 64 of them, sorted by id (id32 = id, or -1 for an invalid one; n its
 // candidate column).
+// Ids are global: the table holds rows [c_base, c_base + c_rows) (a shard, or the whole table with c_base
+// = 0); e_lo, e_hi are global too. With zero_foreign, the score of every id outside the table is written 0
+// (the sharded scorer's partial block, which a SUM over the shards assembles).
 template <class Body>
 __device__ __forceinline__ void for_slice_runs_sorted(const ScoreParams& p, int64_t b, int64_t e_lo, int64_t e_hi,
-                                                      bool take_invalid, int lane, Body&& body) {
+                                                      bool take_invalid, bool zero_foreign, int lane, Body&& body) {
     int buf_key = INT32_MAX, buf_id = -1, buf_n = 0, fill = 0;
     auto flush = [&](int cnt) {
         // sort key: (id - e_lo) << 6 | source lane (invalid ids first, as id - e_lo = 0)
@@ -644,8 +647,9 @@ __device__ __forceinline__ void for_slice_runs_sorted(const ScoreParams& p, int6
         const int64_t n = c0 + lane;
         int64_t id = -1;
         if (n < p.N) id = p.c_idx[b * p.c_stride + n];
-        const bool valid = id >= 0 && id < p.c_rows;
+        const bool valid = id >= p.c_base && id < p.c_base + p.c_rows;
         const bool own = n < p.N && (valid ? (id >= e_lo && id < e_hi) : take_invalid);
+        if (zero_foreign && n < p.N && !valid) p.out[b * p.out_ld + n] = 0.f;
         const uint64_t m = __ballot(own);
         const int cnt = __popcll(m);
         if (cnt == 0) continue;  // wave-uniform
@@ -698,7 +702,7 @@ step_fwd_xcd_kernel(ScoreParams p) {
     bool qok, rok;
     build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
     auto run = [&](const auto& qq) {
-        for_slice_runs_sorted(p, b, e_lo, e_hi, x == 0, lane, [&](int id, int n, int cnt) {
+        for_slice_runs_sorted(p, b, e_lo, e_hi, x == 0, false, lane, [&](int id, int n, int cnt) {
             float2 st;
             const float s = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, 1>(p, qq, (int64_t)id, cnt, lane, st);
             if (lane < cnt) p.out[b * p.out_ld + n] = s;
@@ -738,6 +742,47 @@ step_fwd_xcd_kernel(ScoreParams p) {
     }
 }
 
+
+// Row-sharded scoring in the XCD-sliced order (kge_score_sharded, N >= 128): this shard's rows [c_base,
+// c_base + c_rows) are cut into 8 slices and scored as step_fwd_xcd_kernel scores the whole table; a
+// candidate outside the shard scores 0 (written by the slice-0 wave). At the north star's 8-way split of
+// YAGO3-10 a slice is 3.9 MB, so each XCD's L2 holds its whole slice while its waves sweep it.
+template <int FN, bool CH, int V, int G>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(G <= 4 ? 4 : 1))) void
+score_sharded_xcd_kernel(ScoreParams p) {
+    __shared__ vecf<V> q2img[kWavesPerBlock][FN == KGE_INTERHT ? G * kWave : 1];
+    const int x = blockIdx.x & 7;
+    const int w = threadIdx.x >> 6;
+    const int64_t b = (int64_t)(blockIdx.x >> 3) * kWavesPerBlock + w;
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t S = (p.c_rows + 7) / 8;
+    const int64_t e_lo = p.c_base + min((int64_t)x * S, p.c_rows), e_hi = p.c_base + min(p.c_rows, (int64_t)(x + 1) * S);
+    Query<FN, CH, V, G> q;
+    int64_t qi, ri;
+    bool qok, rok;
+    build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+    auto run = [&](const auto& qq) {
+        for_slice_runs_sorted(p, b, e_lo, e_hi, false, x == 0, lane, [&](int id, int n, int cnt) {
+            float2 st;
+            const float s = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, 1>(p, qq, (int64_t)id, cnt, lane, st);
+            if (lane < cnt) p.out[b * p.out_ld + n] = s;
+        });
+    };
+    if constexpr (FN == KGE_INTERHT) {
+        QueryL2<FN, CH, V, G> ql;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            q2img[w][lane + k * kWave] = q.q2[k];
+            ql.q0[k] = q.q0[k];
+            ql.q1[k] = q.q1[k];
+        }
+        ql.q2 = LdsOperand<V>{q2img[w], lane};
+        run(ql);
+    } else {
+        run(q);
+    }
+}
 
 template <int FN, bool CH, int V, int G, bool ST = false>
 __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
@@ -2458,6 +2503,8 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, false>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_STEP_FWD_XCD)
         hipLaunchKernelGGL((step_fwd_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_SCORE_SHARD_XCD)
+        hipLaunchKernelGGL((score_sharded_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_STEP_FWD_GRAD) {
         if constexpr (FN != KGE_PROTATE && G <= kFwdGradMaxG) {
             if (!p.adversarial)

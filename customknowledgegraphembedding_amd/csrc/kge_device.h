@@ -743,10 +743,11 @@ step_fwd_xcd_kernel(ScoreParams p) {
 }
 
 
-// Row-sharded scoring in the XCD-sliced order (kge_score_sharded, N >= 128): this shard's rows [c_base,
-// c_base + c_rows) are cut into 8 slices and scored as step_fwd_xcd_kernel scores the whole table; a
-// candidate outside the shard scores 0 (written by the slice-0 wave). At the north star's 8-way split of
-// YAGO3-10 a slice is 3.9 MB, so each XCD's L2 holds its whole slice while its waves sweep it.
+// Scoring in the XCD-sliced order (kge_score_indexed / kge_score_sharded, N >= 128): the table's rows
+// [c_base, c_base + c_rows) are cut into 8 slices and scored as step_fwd_xcd_kernel scores them, without the
+// positives. Sharded (skip_foreign): a candidate outside the shard scores 0 (written by the slice-0 wave);
+// at the north star's 8-way split of YAGO3-10 a slice is 3.9 MB, so each XCD's L2 holds its whole slice
+// while its waves sweep it. Unsharded: out-of-range ids go to slice 0 and score against a zero row.
 template <int FN, bool CH, int V, int G>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(G <= 4 ? 4 : 1))) void
 score_sharded_xcd_kernel(ScoreParams p) {
@@ -763,7 +764,8 @@ score_sharded_xcd_kernel(ScoreParams p) {
     bool qok, rok;
     build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
     auto run = [&](const auto& qq) {
-        for_slice_runs_sorted(p, b, e_lo, e_hi, false, x == 0, lane, [&](int id, int n, int cnt) {
+        const bool sh = p.skip_foreign != 0;
+        for_slice_runs_sorted(p, b, e_lo, e_hi, !sh && x == 0, sh && x == 0, lane, [&](int id, int n, int cnt) {
             float2 st;
             const float s = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, 1>(p, qq, (int64_t)id, cnt, lane, st);
             if (lane < cnt) p.out[b * p.out_ld + n] = s;

@@ -70,3 +70,23 @@ def test_c3_c4_positives_from_reference_splits():
         assert tri.shape == (n, 3)
         assert tri[:, 0].max() < w["nentity"] and tri[:, 2].max() < w["nentity"]
         assert tri[:, 1].max() < w["nrelation"]
+
+
+def test_pmc_traffic_is_tied_to_the_library_build(tmp_path, monkeypatch):
+    """roofline.traffic comes from the committed PMC summary only while the loaded libkge_hip.so is the build
+    the passes ran (sha256 recorded by scripts/pmc_summary.py); any other build reports it stale."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    rows = [{"kernel": "step_fwd_xcd_kernel<4, true, 4, 4>", "hbm_read_bytes_corrected": 800.0, "hbm_write_bytes": 2.0},
+            {"kernel": "step_fwd_xcd_kernel<4, false, 4, 4>", "hbm_read_bytes_corrected": 900.0, "hbm_write_bytes": 2.0},
+            {"kernel": "neg_rows_kernel", "hbm_read_bytes_corrected": 10.0, "hbm_write_bytes": 1.0}]
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "library_sha256", lambda: "abc")
+    (prof / "pmc_c2.json").write_text(json.dumps({"library_sha256": "abc", "kernels": rows}))
+    t, src = bench.pmc_traffic("c2", ["step_fwd_xcd_kernel", "neg_rows_kernel"])
+    assert t == (802.0 + 902.0) / 2 + 11.0 and src.endswith("pmc_c2.json")
+    (prof / "pmc_c2.json").write_text(json.dumps({"library_sha256": "other", "kernels": rows}))
+    t, src = bench.pmc_traffic("c2", ["step_fwd_xcd_kernel"])
+    assert t is None and src.startswith("stale")
+    t, src = bench.pmc_traffic("c9", ["step_fwd_xcd_kernel"])
+    assert t is None

@@ -1345,9 +1345,16 @@ int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld
     p.ev_count = w.count;
     rc = run_score(fn, mode, p, KIND_STEP_FWD_GRAD, stream);
     if (rc) return rc;
-    // 2. bucket offsets (one launch)
-    hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, nentity, w.off, w.cursor, 0,
-                       (int)(B * N + 3 * B));
+    // 2. bucket offsets (one launch): every 4096-entity tile scanned at once, the tiles' prefix added by the
+    //    epilogue; one block walking all tiles for tables of more than 4M entities
+    const int64_t ntiles = (nentity + kTile4k - 1) / kTile4k;
+    const bool tiled = nentity > 0 && ntiles <= kEvMaxTiles;
+    if (tiled)
+        hipLaunchKernelGGL(scan_tiles4k_kernel, dim3((unsigned)ntiles), dim3(kScanTile), 0, st, w.count, nentity, w.off,
+                           w.cursor, w.tiles);
+    else
+        hipLaunchKernelGGL(scan_block_kernel, dim3(1), dim3(kScanTile), 0, st, w.count, nentity, w.off, w.cursor, 0,
+                           (int)(B * N + 3 * B));
     rc = check_launch("kge_train_step scan");
     if (rc) return rc;
     // 3. one launch: event scatter, loss weights, score gradients, both slots' query chains, the loss
@@ -1368,6 +1375,11 @@ int kge_train_step(int fn, int mode, float* ent, int64_t nentity, int64_t ent_ld
     e.loss_sum = loss_sum;
     e.ev_cursor = w.cursor;
     e.ev_code_w = w.code;
+    if (tiled) {
+        e.ev_tile_sum = w.tiles;
+        e.ev_off_fix = w.off;
+        e.ev_ntiles = (int)ntiles;
+    }
     rc = run_score(fn, mode, e, KIND_STEP_EPILOGUE, stream);
     if (rc) return rc;
     // 4. phase 2 with Adam fused into the entity pass, relation gradient with Adam (supervisor.py:25-26)

@@ -2023,28 +2023,62 @@ __device__ __forceinline__ int64_t step_ev_key(const ScoreParams& p, int code) {
     return p.pos_base[(int64_t)b * 3];
 }
 
+// the tile-local bucket scan (scan_tiles4k_kernel): entities per tile, and the most tiles the epilogue takes
+constexpr int kEvTile = 4096, kEvMaxTiles = 1024;
+
 template <int FN, bool CH, int V, int G>
 __global__ __launch_bounds__(kBlock) void step_epilogue_kernel(ScoreParams p) {
     __shared__ float red[3][kBlock];
+    __shared__ int tpre[kEvMaxTiles + 1];  // exclusive prefix of the tile totals (tile-local scan), and the total
     const int64_t slot = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int64_t B = p.B;
     const int D = p.D, DV = D / V;
+    const int total = (int)(B * p.N + 3 * B);
+    const bool tiled = p.ev_tile_sum != nullptr;
+    if (tiled) {
+        if (threadIdx.x < kWave) {
+            int carry = 0;
+            for (int base = 0; base < p.ev_ntiles; base += kWave) {
+                const int i = base + lane;
+                const int v = i < p.ev_ntiles ? p.ev_tile_sum[i] : 0;
+                int incl = v;
+#pragma unroll
+                for (int o = 1; o < kWave; o <<= 1) {
+                    const int y = __shfl_up(incl, o, kWave);
+                    if (lane >= o) incl += y;
+                }
+                if (i < p.ev_ntiles) tpre[i] = carry + incl - v;
+                carry += __shfl(incl, kWave - 1, kWave);
+            }
+            if (lane == 0) tpre[p.ev_ntiles] = carry;
+        }
+        __syncthreads();
+    }
     {
         // scatter the gradient events into their entity buckets (offsets from the scan kernel)
         // four codes per thread per round, their key loads and cursor atomics all in flight together
         constexpr int U = 4;
-        const int total = (int)(B * p.N + 3 * B), nl = (int)gridDim.x * kBlock;
+        const int nl = (int)gridDim.x * kBlock;
         for (int c0 = (int)blockIdx.x * kBlock + (int)threadIdx.x; c0 < total; c0 += U * nl) {
             int64_t k[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) k[u] = c0 + u * nl < total ? step_ev_key<CH>(p, c0 + u * nl) : -1;
             int at[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) at[u] = (k[u] >= 0 && k[u] < p.c_rows) ? atomicAdd(p.ev_cursor + k[u], 1) : -1;
+            for (int u = 0; u < U; ++u) {
+                at[u] = (k[u] >= 0 && k[u] < p.c_rows) ? atomicAdd(p.ev_cursor + k[u], 1) : -1;
+                if (tiled && at[u] >= 0) at[u] += tpre[k[u] / kEvTile];
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (at[u] >= 0 && at[u] < total) p.ev_code_w[at[u]] = c0 + u * nl;
+        }
+        if (tiled) {
+            // phase 2's bucket offsets: tile-local -> global (clamped to the event count)
+            for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e <= p.c_rows; e += nl)
+                p.ev_off_fix[e] = e < p.c_rows ? min(p.ev_off_fix[e] + tpre[e / kEvTile], total)
+                                               : min(tpre[p.ev_ntiles], total);
         }
     }
     if (blockIdx.x == gridDim.x - 1) {

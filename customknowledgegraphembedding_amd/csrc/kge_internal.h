@@ -87,6 +87,9 @@ struct ScoreParams {
     int* ev_count;             // fused forward: per-entity event counts (atomics)
     int* ev_cursor;            // epilogue: bucket cursors (scatter)
     int* ev_code_w;            // epilogue: event codes grouped by entity
+    const int* ev_tile_sum;    // epilogue: per-4096-entity tile totals of the counts (tile-local cursors), or null
+    int* ev_off_fix;           // epilogue: the tile-local offsets it rewrites to global ones (phase 2 reads them)
+    int ev_ntiles;
     float* out_neg;      // [B] reduced negative branch
     float* out_pos_raw;  // [B] raw positive score (may be null)
     float* out_pos_ls;   // [B] logsigmoid(positive score)

@@ -152,5 +152,57 @@ __global__ __launch_bounds__(kScanTile) void scan_block_kernel(int* __restrict__
     if (t == 0) off[E] = min(carry_s, cap);
 }
 
+// Tile-local exclusive scan for the train step's entity buckets: block i (1024 threads, one int4 each)
+// scans the 4096 counts of tile i, writes the tile-LOCAL exclusive offsets to off and cursor and the tile's
+// total to tile_sum[i]. The consumer (step_epilogue_kernel) adds the tiles' prefix itself: the scatter adds
+// it to each cursor it draws, and it rewrites off to the global offsets for phase 2. All tiles run at once
+// (one launch, no cross-block wait), instead of one block walking every tile.
+constexpr int kTile4k = 4 * kScanTile;
+__global__ __launch_bounds__(kScanTile) void scan_tiles4k_kernel(const int* __restrict__ count, int64_t E,
+                                                                 int* __restrict__ off, int* __restrict__ cursor,
+                                                                 int* __restrict__ tile_sum) {
+    constexpr int NW = kScanTile / kWave;
+    __shared__ int wtot[NW];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t e0 = (int64_t)blockIdx.x * kTile4k + (int64_t)t * 4;
+    const uint32_t bytes = (uint32_t)(E * 4);
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(count), (short)0, (int)bytes, 0x00020000);
+    const scan_i4 x = e0 < E ? __builtin_bit_cast(scan_i4, __builtin_amdgcn_raw_buffer_load_b128(rc, (uint32_t)(e0 * 4), 0, 0))
+                             : scan_i4{0, 0, 0, 0};
+    const int v = x[0] + x[1] + x[2] + x[3];
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int y = __shfl_up(incl, o, kWave);
+        if (lane >= o) incl += y;
+    }
+    if (lane == kWave - 1) wtot[w] = incl;
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) {
+        const int s = wtot[ww];
+        before += ww < w ? s : 0;
+        all += s;
+    }
+    int run = before + incl - v;
+    scan_i4 o4;
+    o4[0] = run;
+    run += x[0];
+    o4[1] = run;
+    run += x[1];
+    o4[2] = run;
+    run += x[2];
+    o4[3] = run;
+    if (e0 < E) {
+        const auto ro = __builtin_amdgcn_make_buffer_rsrc(off, (short)0, (int)bytes, 0x00020000);
+        const auto ru = __builtin_amdgcn_make_buffer_rsrc(cursor, (short)0, (int)bytes, 0x00020000);
+        const scan_u4 u = __builtin_bit_cast(scan_u4, o4);
+        __builtin_amdgcn_raw_buffer_store_b128(u, ro, (uint32_t)(e0 * 4), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u, ru, (uint32_t)(e0 * 4), 0, 0);
+    }
+    if (t == 0) tile_sum[blockIdx.x] = all;
+}
+
 }  // namespace
 }  // namespace kge_impl

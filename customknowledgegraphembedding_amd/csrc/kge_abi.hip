@@ -254,12 +254,13 @@ struct RelAdam {
     int on;
 };
 
-__global__ __launch_bounds__(kBlock) void bwd_rel_kernel(const int64_t* __restrict__ pos, int64_t B, int64_t R,
+constexpr int kRelWaves = 16;  // waves per relation chunk: each scans 1/16 of the slots (fewer dependent rounds)
+__global__ __launch_bounds__(kRelWaves * kWave) void bwd_rel_kernel(const int64_t* __restrict__ pos, int64_t B, int64_t R,
                                                          const float* __restrict__ qg_rel, int64_t rel_w,
                                                          int64_t rel_off, float* __restrict__ d_rel, int64_t rel_ld,
                                                          int64_t rel_dim, const float* __restrict__ dmod_part,
                                                          float* __restrict__ d_mod, RelAdam ra) {
-    __shared__ float red[kWavesPerBlock][kWave];
+    __shared__ float red[kRelWaves][kWave];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (blockIdx.x == 0 && threadIdx.x == 0 && d_mod && dmod_part) {
         float m = 0.f;
@@ -272,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void bwd_rel_kernel(const int64_t* __restri
     const int64_t c = (blockIdx.x - rho * chunks) * kWave + lane;  // column of the full relation row
     const bool used = c >= rel_off && c < rel_off + rel_w;
     const int64_t cu = c - rel_off;
-    const int64_t S = 2 * B, per = (S + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t S = 2 * B, per = (S + kRelWaves - 1) / kRelWaves;
     const int64_t s_lo = w * per, s_hi = min(S, s_lo + per);
     float acc = 0.f;
     if (__ballot(used)) {
@@ -301,7 +302,9 @@ __global__ __launch_bounds__(kBlock) void bwd_rel_kernel(const int64_t* __restri
     red[w][lane] = acc;
     __syncthreads();
     if (w != 0 || c >= rel_dim) return;
-    float g = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    float g = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kRelWaves; ++ww) g += red[ww][lane];
     g = used ? g : 0.f;  // parts no score function reads get 0
     if (ra.on) {
         const int64_t e = rho * rel_ld + c;
@@ -1161,7 +1164,7 @@ static int step_backward_impl(int fn, int mode, const float* ent, int64_t nentit
             ra.a = *adam;
             ra.on = 1;
         }
-        hipLaunchKernelGGL(bwd_rel_kernel, dim3((unsigned)rb), dim3(kBlock), 0, st, pos, B, nrelation, w.qg_rel, rel_w,
+        hipLaunchKernelGGL(bwd_rel_kernel, dim3((unsigned)rb), dim3(kRelWaves * kWave), 0, st, pos, B, nrelation, w.qg_rel, rel_w,
                            rel_off, d_rel, rel_ld, rel_dim, w.dmod, d_modulus, ra);
     }
     return check_launch("kge_step_backward");

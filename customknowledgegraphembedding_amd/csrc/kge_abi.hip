@@ -469,7 +469,11 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         waves = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock * 8;  // 8 slice blocks per 4 rows
     } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS) {
         waves = p.B;  // one wave per slot
-    } else if (kind == KIND_STEP_EPILOGUE || kind == KIND_SHARD_EPILOGUE) {
+    } else if (kind == KIND_STEP_EPILOGUE) {
+        // one wave per slot (negative rows' chains, positives, negative rows' score gradients), then one
+        // block for the loss
+        waves = (3 * p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock + kWavesPerBlock;
+    } else if (kind == KIND_SHARD_EPILOGUE) {
         // one wave per slot (negative rows, then positives), then one block for the loss
         waves = (2 * p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock + kWavesPerBlock;
     } else if (kind == KIND_BWD_ENT) {

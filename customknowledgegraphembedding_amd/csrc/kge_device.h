@@ -2111,19 +2111,22 @@ __global__ __launch_bounds__(kBlock) void step_epilogue_kernel(ScoreParams p) {
         }
         return;
     }
-    if (slot >= 2 * B) return;
+    // waves [0, B): the negative slots' query chains; [B, 2B): the positive slots; [2B, 3B): the negative rows'
+    // score gradients (split from the chains: neither waits for the other's loads and stores)
+    if (slot >= 3 * B) return;
     {
-        const bool negslot = slot < B;
-        const int64_t b = negslot ? slot : slot - B;
+        const bool negslot = slot < B, rowgrad = slot >= 2 * B;
+        const int64_t b = negslot ? slot : (rowgrad ? slot - 2 * B : slot - B);
         // sum w in a fixed order: every wave gets the same value
         float sw = 0.f;
         for (int64_t i = lane; i < B; i += kWave) sw += p.weight[i];
         sw = wave_sum(sw);
         const float wb = p.weight[b];
         const float go = (-0.5f / sw) * wb;
-        if (negslot) {
+        if (rowgrad) {
             neg_row_bwd(p.neg_scores + b * p.ns_ld, p.N, p.temperature, p.adversarial, p.detach, go,
                         const_cast<float*>(p.d_ns) + b * p.N, lane);
+        } else if (negslot) {
             Query<FN, CH, V, G> q;
             int64_t qi, ri;
             bool qok, rok;

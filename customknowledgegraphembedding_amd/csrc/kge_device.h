@@ -72,6 +72,20 @@ constexpr int kAuxNT = 2, kAuxSC1 = 16;
 #ifndef KGE_ENT_ST_AUX
 #define KGE_ENT_ST_AUX kAuxNT
 #endif
+// bwd_ent_stream_kernel: a small bucket's codes requested ahead of the row, the row's norms taken
+// after the first events' loads are issued (0: the earlier order, for A/B builds)
+#ifndef KGE_ENT_EARLY
+#define KGE_ENT_EARLY 1
+#endif
+#ifndef KGE_ENT_UMAX
+#define KGE_ENT_UMAX 2
+#endif
+#ifndef KGE_ENT_WPE
+#define KGE_ENT_WPE 0
+#endif
+#ifndef KGE_ENT_LATE_MV
+#define KGE_ENT_LATE_MV 1
+#endif
 
 template <int V, int AUX = 0>
 __device__ __forceinline__ vecf<V> bload(rsrc_t r, uint32_t off) {
@@ -2252,11 +2266,17 @@ constexpr int kEntSortMax = 2048;
 // the relation row, is read from the relation table instead: it stays in L2)
 constexpr int ent_nq(int fn) { return (fn == KGE_COMPLEX || fn == KGE_ROTATE || fn == KGE_INTERHT) ? 2 : 1; }
 
+#if KGE_ENT_WPE > 0
+#define KGE_ENT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(KGE_ENT_WPE)))
+#else
+#define KGE_ENT_WPE_ATTR
+#endif
 template <int FN, bool CH, int V, int G>
-__global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
+__global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel(ScoreParams p) {
     static_assert(G % kWavesPerBlock == 0, "the streaming phase 2 needs a multiple of 4 groups per lane");
     constexpr int GW = G / kWavesPerBlock;
-    constexpr int U = GW == 1 ? 4 : (GW == 2 ? 2 : 1);  // events whose query slices are in flight
+    constexpr int U0 = GW == 1 ? 4 : (GW == 2 ? 2 : 1);  // events whose query slices are in flight
+    constexpr int U = U0 < KGE_ENT_UMAX ? U0 : KGE_ENT_UMAX;
     constexpr bool SPLIT = is_split(FN);
     constexpr int NH = SPLIT ? 2 : 1;
     constexpr int NQ = ent_nq(FN);
@@ -2283,6 +2303,12 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
     const int ntot = (int)(p.Bn * p.Nn + 3 * p.Bn);
     const int lo = min(max(p.ev_off[e], 0), ntot), hi = min(max(p.ev_off[e + 1], lo), ntot);
     const int n = hi - lo;
+#if KGE_ENT_EARLY
+    // a small bucket's codes are requested before the row and its moments: the vector-memory counter
+    // retires in order, so the code -> relation index -> event-slice chain then runs under the row's
+    // HBM latency instead of after it
+    int code0 = (n <= kWave && lane < n) ? p.ev_code[lo + lane] : INT32_MAX;
+#endif
     // the row slice, and the Adam moments requested up front so their latency overlaps the walk
     vecf<V> ca[GW], cb[GW], mm[NH][GW], vv[NH][GW];
     {
@@ -2295,37 +2321,48 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
             cb[gg] = SPLIT ? sload(sb, goffs[gg]) : vzero<V>();
         }
     }
-    if (p.adam.on) {
+    auto load_mv = [&]() {
+        if (p.adam.on) {
 #pragma unroll
-        for (int h = 0; h < NH; ++h) {
-            const rsrc_t sm = make_rsrc(p.adam.m + e * p.c_ld + h * D, nb);
-            const rsrc_t sv = make_rsrc(p.adam.v + e * p.c_ld + h * D, nb);
+            for (int h = 0; h < NH; ++h) {
+                const rsrc_t sm = make_rsrc(p.adam.m + e * p.c_ld + h * D, nb);
+                const rsrc_t sv = make_rsrc(p.adam.v + e * p.c_ld + h * D, nb);
 #pragma unroll
-            for (int gg = 0; gg < GW; ++gg) {
-                mm[h][gg] = sload(sm, goffs[gg]);
-                vv[h][gg] = sload(sv, goffs[gg]);
+                for (int gg = 0; gg < GW; ++gg) {
+                    mm[h][gg] = sload(sm, goffs[gg]);
+                    vv[h][gg] = sload(sv, goffs[gg]);
+                }
             }
         }
-    }
+    };
+#if !KGE_ENT_LATE_MV
+    load_mv();
+#endif
     vecf<V> sa[GW], sb[GW], ra[GW], rb[GW];  // candidate terms (normalised space), row events
 #pragma unroll
     for (int gg = 0; gg < GW; ++gg) sa[gg] = sb[gg] = ra[gg] = rb[gg] = vzero<V>();
     float ia = 0.f, ib = 0.f;
     bool any_cand = false;
     if (n > 0) {
-        if constexpr (FN == KGE_INTERHT) {
-            float s2a = 0.f, s2b = 0.f;
+        // InterHT's half-norms of the row (block-wide; every wave calls this at the same point)
+        auto norms = [&]() {
+            if constexpr (FN == KGE_INTERHT) {
+                float s2a = 0.f, s2b = 0.f;
 #pragma unroll
-            for (int gg = 0; gg < GW; ++gg)
+                for (int gg = 0; gg < GW; ++gg)
 #pragma unroll
-                for (int i = 0; i < V; ++i) {
-                    s2a += ca[gg].a[i] * ca[gg].a[i];
-                    s2b += cb[gg].a[i] * cb[gg].a[i];
-                }
-            const float2 s = block_sum2(s2a, s2b, red, lane, w);
-            ia = rsqrt_f(s.x);
-            ib = rsqrt_f(s.y);
-        }
+                    for (int i = 0; i < V; ++i) {
+                        s2a += ca[gg].a[i] * ca[gg].a[i];
+                        s2b += cb[gg].a[i] * cb[gg].a[i];
+                    }
+                const float2 s = block_sum2(s2a, s2b, red, lane, w);
+                ia = rsqrt_f(s.x);
+                ib = rsqrt_f(s.y);
+            }
+        };
+#if !KGE_ENT_EARLY
+        norms();
+#endif
         // one event: its slice of the slot's stored query (candidate event) or of the slot's
         // query-entity gradient (row event)
         auto load_ev = [&](int code, vecf<V>(&x0)[GW], vecf<V>(&x1)[GW], vecf<V>(&x2)[GW]) {
@@ -2381,7 +2418,11 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
             }
         };
         if (n <= kWave) {
+#if KGE_ENT_EARLY
+            int code = code0;
+#else
             int code = lane < n ? p.ev_code[lo + lane] : INT32_MAX;
+#endif
             if ((unsigned)code >= (unsigned)ntot) code = INT32_MAX;  // never index with a stray code
             const int nv = __popcll(__ballot(code != INT32_MAX));
             code = wave_sort_asc(code, lane);
@@ -2390,11 +2431,18 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (j + u < nv) load_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
+#if KGE_ENT_EARLY
+                // the norms after the first events' loads are issued (nv is block-uniform)
+                if (j == 0) norms();
+#endif
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (j + u < nv) apply_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
             }
         } else if (n <= kEntSortMax) {
+#if KGE_ENT_EARLY
+            norms();
+#endif
             // large bucket (a hub entity, or a small table): one block-wide bitonic sort of its codes in LDS,
             // then the same ordered walk, U events in flight (n is block-uniform: every barrier is reached)
             int np2 = 2 * kWave;
@@ -2432,6 +2480,9 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
                     if (j + u < nv) apply_ev(srt[j + u], x0[u], x1[u], x2[u]);
             }
         } else {
+#if KGE_ENT_EARLY
+            norms();
+#endif
             // larger still: extract codes in ascending order (O(n^2 / 64))
             int last = -1;
             for (int it = 0; it < n; ++it) {
@@ -2448,6 +2499,9 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
                 last = m;
             }
         }
+#if KGE_ENT_LATE_MV
+        load_mv();  // the moments' latency overlaps the row's closing dot
+#endif
         if constexpr (FN == KGE_INTERHT) {
             // any_cand is block-uniform (every wave walks the same events)
             if (any_cand) {
@@ -2477,6 +2531,9 @@ __global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
                 sb[gg].a[i] += rb[gg].a[i];
             }
     }
+#if KGE_ENT_LATE_MV
+    if (n <= 0) load_mv();
+#endif
     auto sstore = [&](rsrc_t r, uint32_t off, const vecf<V>& v) { bstore<V, KGE_ENT_ST_AUX>(r, off, v); };
     if (p.adam.on) {
 #pragma unroll

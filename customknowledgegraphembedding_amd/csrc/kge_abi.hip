@@ -470,9 +470,11 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS) {
         waves = p.B;  // one wave per slot
     } else if (kind == KIND_STEP_EPILOGUE) {
-        // one wave per slot (negative rows' chains, positives, negative rows' score gradients), then one
-        // block for the loss
-        waves = (3 * p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock + kWavesPerBlock;
+        // one wave per slot (negative rows' chains, positives, negative rows' score gradients), then the
+        // event-scatter blocks (about four codes per thread, at most 256 blocks), then one block for the loss
+        const int64_t ev = p.B * p.N + 3 * p.B;
+        const int64_t sb = std::min<int64_t>(std::max<int64_t>((ev + 4 * kBlock - 1) / (4 * kBlock), 1), 256);
+        waves = (3 * p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock + (sb + 1) * kWavesPerBlock;
     } else if (kind == KIND_SHARD_EPILOGUE) {
         // one wave per slot (negative rows, then positives), then one block for the loss
         waves = (2 * p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock + kWavesPerBlock;

@@ -2050,52 +2050,59 @@ __global__ __launch_bounds__(kBlock) void step_epilogue_kernel(ScoreParams p) {
     const int D = p.D, DV = D / V;
     const int total = (int)(B * p.N + 3 * B);
     const bool tiled = p.ev_tile_sum != nullptr;
-    if (tiled) {
-        if (threadIdx.x < kWave) {
-            int carry = 0;
-            for (int base = 0; base < p.ev_ntiles; base += kWave) {
-                const int i = base + lane;
-                const int v = i < p.ev_ntiles ? p.ev_tile_sum[i] : 0;
-                int incl = v;
-#pragma unroll
-                for (int o = 1; o < kWave; o <<= 1) {
-                    const int y = __shfl_up(incl, o, kWave);
-                    if (lane >= o) incl += y;
-                }
-                if (i < p.ev_ntiles) tpre[i] = carry + incl - v;
-                carry += __shfl(incl, kWave - 1, kWave);
-            }
-            if (lane == 0) tpre[p.ev_ntiles] = carry;
-        }
-        __syncthreads();
-    }
-    {
-        // scatter the gradient events into their entity buckets (offsets from the scan kernel)
-        // four codes per thread per round, their key loads and cursor atomics all in flight together
-        constexpr int U = 4;
-        const int nl = (int)gridDim.x * kBlock;
-        for (int c0 = (int)blockIdx.x * kBlock + (int)threadIdx.x; c0 < total; c0 += U * nl) {
-            int64_t k[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) k[u] = c0 + u * nl < total ? step_ev_key<CH>(p, c0 + u * nl) : -1;
-            int at[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                at[u] = (k[u] >= 0 && k[u] < p.c_rows) ? atomicAdd(p.ev_cursor + k[u], 1) : -1;
-                if (tiled && at[u] >= 0) at[u] += tpre[k[u] / kEvTile];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (at[u] >= 0 && at[u] < total) p.ev_code_w[at[u]] = c0 + u * nl;
-        }
+    // blocks [0, nsb): slots; [nsb, last): the event scatter; last: the loss. The scatter's chain (key
+    // load -> cursor atomic -> code store) runs beside the slots' chains instead of ahead of them.
+    const int nsb = (int)((3 * B + kWavesPerBlock - 1) / kWavesPerBlock), last = (int)gridDim.x - 1;
+    const int sblk = (int)blockIdx.x - nsb, nscat = last - nsb;
+    if (sblk >= 0 && sblk < nscat) {
         if (tiled) {
-            // phase 2's bucket offsets: tile-local -> global (clamped to the event count)
-            for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e <= p.c_rows; e += nl)
-                p.ev_off_fix[e] = e < p.c_rows ? min(p.ev_off_fix[e] + tpre[e / kEvTile], total)
-                                               : min(tpre[p.ev_ntiles], total);
+            if (threadIdx.x < kWave) {
+                int carry = 0;
+                for (int base = 0; base < p.ev_ntiles; base += kWave) {
+                    const int i = base + lane;
+                    const int v = i < p.ev_ntiles ? p.ev_tile_sum[i] : 0;
+                    int incl = v;
+#pragma unroll
+                    for (int o = 1; o < kWave; o <<= 1) {
+                        const int y = __shfl_up(incl, o, kWave);
+                        if (lane >= o) incl += y;
+                    }
+                    if (i < p.ev_ntiles) tpre[i] = carry + incl - v;
+                    carry += __shfl(incl, kWave - 1, kWave);
+                }
+                if (lane == 0) tpre[p.ev_ntiles] = carry;
+            }
+            __syncthreads();
         }
+        {
+            // scatter the gradient events into their entity buckets (offsets from the scan kernel)
+            // four codes per thread per round, their key loads and cursor atomics all in flight together
+            constexpr int U = 4;
+            const int nl = nscat * kBlock;
+            for (int c0 = sblk * kBlock + (int)threadIdx.x; c0 < total; c0 += U * nl) {
+                int64_t k[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) k[u] = c0 + u * nl < total ? step_ev_key<CH>(p, c0 + u * nl) : -1;
+                int at[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    at[u] = (k[u] >= 0 && k[u] < p.c_rows) ? atomicAdd(p.ev_cursor + k[u], 1) : -1;
+                    if (tiled && at[u] >= 0) at[u] += tpre[k[u] / kEvTile];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (at[u] >= 0 && at[u] < total) p.ev_code_w[at[u]] = c0 + u * nl;
+            }
+            if (tiled) {
+                // phase 2's bucket offsets: tile-local -> global (clamped to the event count)
+                for (int64_t e = (int64_t)sblk * kBlock + threadIdx.x; e <= p.c_rows; e += nl)
+                    p.ev_off_fix[e] = e < p.c_rows ? min(p.ev_off_fix[e] + tpre[e / kEvTile], total)
+                                                   : min(tpre[p.ev_ntiles], total);
+            }
+        }
+        return;
     }
-    if (blockIdx.x == gridDim.x - 1) {
+    if ((int)blockIdx.x == last) {
         // the last block: the loss of supervisor.py:19-23 (fixed reduction order) and the Sum metric
         const int t = threadIdx.x;
         float sw = 0.f, sp = 0.f, sn = 0.f;

@@ -231,6 +231,35 @@ def test_one_call_train_step_matches_split_path(name, d):
         assert float((x - y).abs().max()) <= 1e-4 * scale, name
 
 
+@pytest.mark.parametrize("name", ["InterHT", "DistMult"])
+def test_one_call_train_step_matches_split_path_many_events(name):
+    """B·N + 3B = 300 900 events: past one round of the epilogue's scatter blocks (at most 256 blocks × 256
+    threads × 4 codes = 262 144 per round), so the scatter loops and every bucket is still filled exactly once."""
+    de, tr = (True, True) if name == "InterHT" else (False, False)
+    E, R, B, N, d, lr = 4000, 5, 300, 1000, 24, 2e-3
+    g = np.random.RandomState(21)
+    data = []
+    for i in range(2):
+        pos = torch.from_numpy(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1))
+        neg = torch.from_numpy(g.randint(E, size=(B, N)))
+        w = torch.from_numpy(g.uniform(0.1, 1, size=(B, 1))).float()
+        data.append((pos, neg, w, torch.tensor([i % 2] * B)))
+
+    def run(fused):
+        m = kge.TFKGEModel(name, E, R, d, 9.0, de, False, tr, device=DEV, seed=5)
+        opt = Adam(m.parameters(), lr=lr)
+        tr_ = Trainer(Strategy(), data, m, opt, Sum(), fused=fused)
+        it = iter(data)
+        losses = [float(tr_.train_step(it)) for _ in range(2)]
+        return losses, [p.detach().clone() for p in m.parameters() if p.requires_grad]
+
+    la, pa = run(True)
+    lc, pc = run("split")
+    np.testing.assert_allclose(la, lc, rtol=2e-6, atol=1e-7)
+    for x, y in zip(pa, pc):
+        assert float((x - y).abs().max()) <= 2e-2 * lr, name
+
+
 @pytest.mark.parametrize("E,B,N", [(60, 6, 24), (12, 48, 200), (3, 40, 160)])
 def test_one_call_train_step_matches_oracle_tf_step(E, B, N):
     """kge_train_step against the oracle's fp64 TF-semantics step (loss graph + Keras Adam). E = 12 puts

@@ -86,6 +86,11 @@ constexpr int kAuxNT = 2, kAuxSC1 = 16;
 #ifndef KGE_ENT_LATE_MV
 #define KGE_ENT_LATE_MV 1
 #endif
+// step_fwd_grad_kernel: InterHT's per-element Jacobian signs kept from the score pass, under a 2-waves/SIMD
+// bound (256 VGPRs, 36 B/lane spilled; 191 -> 175 us at C2 same box). 0: recomputed, 229 VGPRs
+#ifndef KGE_FG_KEEPSGN
+#define KGE_FG_KEEPSGN 1
+#endif
 
 template <int V, int AUX = 0>
 __device__ __forceinline__ vecf<V> bload(rsrc_t r, uint32_t off) {
@@ -370,7 +375,7 @@ struct LdsQuery {
 
 template <int FN, bool CH, int V, int G, class Q>
 __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Q& q, const ScoreParams& p,
-                                            float2* stats = nullptr) {
+                                            float2* stats = nullptr, vecf<V>* nsg = nullptr) {
     float acc = 0.f;
     if constexpr (FN == KGE_INTERHT) {
         float sa = 0.f, sb = 0.f;
@@ -395,6 +400,7 @@ __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Q& q,
                 else
                     x = q.q0[k].a[i] * bh - ah * q.q1[k].a[i] + q.q2[k].a[i];
                 acc += fabsf(x);
+                if (nsg) nsg[k].a[i] = -sgnf(x);  // the Jacobian's sign (0 past D: x = 0 there)
             }
         // groups past D: candidate zero-loaded and query zero -> x = 0
     } else {
@@ -985,7 +991,7 @@ template <int FN, bool CH, int V, bool TWO>
 __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, const vecf<V>& q0, const vecf<V>& q1,
                                           const vecf<V>& q2, bool in, float ia, float ib, const ScoreParams& p,
                                           float wa, float wb, vecf<V>& a0, vecf<V>& a1, vecf<V>& a2, vecf<V>& b0,
-                                          vecf<V>& b1, vecf<V>& b2) {
+                                          vecf<V>& b1, vecf<V>& b2, const vecf<V>* nsg = nullptr) {
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         const float x = ca.a[i];
@@ -994,14 +1000,14 @@ __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, 
             const float ah = x * ia;
             const float bh = cb.a[i] * ib + 1.f;
             if (CH) {
-                const float xx = ah * q1.a[i] - q0.a[i] * bh + q2.a[i];
-                const float Gx = in ? -sgnf(xx) : 0.f;
+                const float xx = nsg ? 0.f : ah * q1.a[i] - q0.a[i] * bh + q2.a[i];
+                const float Gx = nsg ? nsg->a[i] : (in ? -sgnf(xx) : 0.f);
                 j1 = Gx * ah;
                 j0 = -Gx * bh;
                 j2 = Gx;
             } else {
-                const float xx = q0.a[i] * bh - ah * q1.a[i] + q2.a[i];
-                const float Gx = in ? -sgnf(xx) : 0.f;
+                const float xx = nsg ? 0.f : q0.a[i] * bh - ah * q1.a[i] + q2.a[i];
+                const float Gx = nsg ? nsg->a[i] : (in ? -sgnf(xx) : 0.f);
                 j0 = Gx * bh;
                 j1 = -Gx * ah;
                 j2 = Gx;
@@ -1031,8 +1037,13 @@ __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, 
     }
 }
 
+#if KGE_FG_KEEPSGN
+#define KGE_FG_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#else
+#define KGE_FG_ATTR
+#endif
 template <int FN, bool CH, int V, int G, int RED>
-__global__ __launch_bounds__(kBlock) void step_fwd_grad_kernel(ScoreParams p) {
+__global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(ScoreParams p) {
     static_assert(FN != KGE_PROTATE, "pRotatE's modulus gradient is not part of the fused query pass");
     constexpr bool TWO = RED == 2;
     constexpr int W = G * kWave;  // vecf<V> per operand per wave image
@@ -1070,7 +1081,8 @@ __global__ __launch_bounds__(kBlock) void step_fwd_grad_kernel(ScoreParams p) {
     {
 
         // one candidate's contribution (s is wave-uniform)
-        auto accumulate = [&](const Cand<FN, V, G>& c, const LdsQuery<V>& q, float s, float2 nst) {
+        auto accumulate = [&](const Cand<FN, V, G>& c, const LdsQuery<V>& q, float s, float2 nst,
+                              const vecf<V>* nsg) {
             float wa, wb = 0.f;
             if constexpr (RED == 0) {
                 wa = -sigmoidf(s);
@@ -1108,7 +1120,7 @@ __global__ __launch_bounds__(kBlock) void step_fwd_grad_kernel(ScoreParams p) {
 #pragma unroll
             for (int k = 0; k < G; ++k)
                 group_jac<FN, CH, V, TWO>(c.ca[k], c.cb[k], q.q0[k], q.q1[k], q.q2[k], (lane + k * kWave) < DV, nst.x,
-                                          nst.y, p, wa, wb, a0[k], a1[k], a2[k], b0[k], b1[k], b2[k]);
+                                          nst.y, p, wa, wb, a0[k], a1[k], a2[k], b0[k], b1[k], b2[k], nsg ? nsg + k : nullptr);
         };
         const int64_t per = (p.N + kWavesPerBlock - 1) / kWavesPerBlock;
         const int64_t lo = w * per, hi = min(p.N, lo + per);
@@ -1143,12 +1155,23 @@ __global__ __launch_bounds__(kBlock) void step_fwd_grad_kernel(ScoreParams p) {
                 asm volatile("" : "+v"(li));
                 const LdsQuery<V> q{{qimg[0], li}, {qimg[1], li}, {qimg[2], li}};
                 float2 nst = make_float2(0.f, 0.f);
+#if KGE_FG_KEEPSGN
+                // InterHT: the score pass leaves each element's -sgn for the Jacobian sums (16 VGPRs
+                // instead of recomputing the element's term)
+                vecf<V> nsg[G];
+                const float s = cand_score<FN, CH, V, G>(c, q, p, &nst, FN == KGE_INTERHT ? nsg : nullptr);
+#else
                 const float s = cand_score<FN, CH, V, G>(c, q, p, &nst);
+#endif
                 if (lane == jj) my_score = s;
                 // opaque copies of the half-norms: the gradient recomputes the candidate's terms
                 // instead of keeping the score's per-element values alive across the reductions
                 asm volatile("" : "+v"(nst.x), "+v"(nst.y));
-                accumulate(c, q, s, nst);
+#if KGE_FG_KEEPSGN
+                accumulate(c, q, s, nst, FN == KGE_INTERHT ? nsg : nullptr);
+#else
+                accumulate(c, q, s, nst, nullptr);
+#endif
             };
             // software pipeline (as score_run): row j + 1 is in flight while row j is reduced
             x0.load(cand_row(p, readlane64(my_id, 0), ok0), ok0, p.D, lane);

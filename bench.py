@@ -84,12 +84,18 @@ def library_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
+def loaded_source_hash():
+    """kge_source_hash() of the loaded libkge_hip.so (the sources it was built from)."""
+    from customknowledgegraphembedding_amd import _lib
+    return _lib.load().kge_source_hash().decode()
+
+
 def pmc_traffic(workload, kernel_prefixes):
-    """HBM bytes per step of the kernels `kernel_prefixes` (each: the mean over its head/tail
-    instantiations, summed over the prefixes) from the committed rocprofv3 --pmc summary of this
-    workload (profiles/pmc_<workload>.json, scripts/pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x 2
-    + WRITE_SIZE, the gfx950 corrections). (None, reason) when no summary was committed, or when it
-    was measured on another build of libkge_hip.so than the one loaded now (stale)."""
+    """Fabric (L2 <-> memory) bytes per step of the kernels `kernel_prefixes` (each: the mean over its
+    head/tail instantiations, summed over the prefixes) from the committed rocprofv3 --pmc summary of
+    this workload (profiles/pmc_<workload>.json, scripts/pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x 2
+    + WRITE_SIZE, the gfx950 corrections). (None, reason) when no summary was committed, or when it was
+    measured on a library built from other sources than the one loaded now (kge_source_hash: stale)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     try:
         with open(path) as f:
@@ -97,8 +103,10 @@ def pmc_traffic(workload, kernel_prefixes):
         rows = summ["kernels"]
     except (OSError, ValueError, KeyError):
         return None, "no PMC summary committed"
-    if summ.get("library_sha256") != library_sha256():
-        return None, f"stale: {os.path.relpath(path, ROOT)} was measured on another libkge_hip.so build"
+    have = loaded_source_hash()
+    if summ.get("source_hash") != have:
+        return None, (f"stale: {os.path.relpath(path, ROOT)} was measured on sources {summ.get('source_hash')}, "
+                      f"the loaded library is built from {have}")
     total = 0.0
     for pre in kernel_prefixes:
         got = [r["hbm_read_bytes_corrected"] + r.get("hbm_write_bytes", 0.0) for r in rows
@@ -108,6 +116,26 @@ def pmc_traffic(workload, kernel_prefixes):
             return None, f"{os.path.relpath(path, ROOT)} has no {pre}"
         total += sum(got) / len(got)
     return total, os.path.relpath(path, ROOT)
+
+
+def roofline_hbm(step_bytes, traffic, traffic_src, kern_avg_s, **extra):
+    """The HBM roofline object of a gather-bound step. `frac` is on the COUNTER bytes (the PMC passes'
+    FETCH_SIZE x 2 + WRITE_SIZE of the same kernels, per launch) whenever a summary of this build
+    exists: the algorithmic-bytes fraction can pass 1 when repeat gathers hit L2 / the Infinity Cache,
+    the counter fraction cannot. The algorithmic figure (SURVEY §8d bytes) is reported beside it."""
+    alg = step_bytes / kern_avg_s / 1e9
+    r = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic, "traffic_unit": "bytes/step",
+         "traffic_source": traffic_src, "achieved_algorithmic": alg, "frac_algorithmic": alg / HBM_PEAK_GBS,
+         "algorithmic_bytes_per_launch": step_bytes, "kernel_avg_us": kern_avg_s * 1e6}
+    if traffic:
+        ach = traffic / kern_avg_s / 1e9
+        r.update({"achieved": ach, "frac": ach / HBM_PEAK_GBS, "frac_basis": "counter bytes (PMC)",
+                  "frac_counter": ach / HBM_PEAK_GBS})
+    else:
+        r.update({"achieved": alg, "frac": alg / HBM_PEAK_GBS, "frac_basis": "algorithmic bytes (no PMC summary "
+                  "of this build)", "frac_counter": None})
+    r.update(extra)
+    return r
 
 
 def dims(w):
@@ -165,19 +193,32 @@ def positives(w, rank, n_batches, world=1):
     return out, f"reference triples tests/golden/{w['dataset']}_ids.npz (RandomState(0) permutation)"
 
 
+def rank_batches(w, rank, n_batches=8, world=1):
+    """Host ids of rank `rank`'s batches: ([(pos [B,3], neg [B,N])], positives source). Ranks read
+    disjoint positives (batch i of rank r is sequential batch i * world + r); negatives
+    RandomState(2 + 1000 rank + i).randint(E, (B, N))."""
+    E, B, N = w["nentity"], w["B"], w["N"]
+    pos_l, src = positives(w, rank, n_batches, world)
+    return [(pos_l[i], np.random.RandomState(2 + 1000 * rank + i).randint(E, size=(B, N)))
+            for i in range(n_batches)], src
+
+
 def make_inputs(w, rank, device, n_batches=8, world=1):
     from customknowledgegraphembedding_amd.model import TFKGEModel
     m = TFKGEModel(w["fn"], w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"],
                    double_entity_embedding=w["de"], double_relation_embedding=w["dr"],
                    triple_relation_embedding=w["tr"], device=device, seed=0)
-    E, B, N = w["nentity"], w["B"], w["N"]
-    pos_l, src = positives(w, rank, n_batches, world)
-    batches = []
-    for i in range(n_batches):
-        neg = np.random.RandomState(2 + 1000 * rank + i).randint(E, size=(B, N))
-        batches.append((torch.from_numpy(pos_l[i]).to(device), torch.from_numpy(neg).to(device)))
+    host, src = rank_batches(w, rank, n_batches, world)
+    batches = [(torch.from_numpy(p).to(device), torch.from_numpy(n).to(device)) for p, n in host]
     m.positives_source = src
     return m, batches
+
+
+def cpu_baseline_inputs(w, rows):
+    """The CPU baseline's sample: the first `rows` rows of rank 0's batch 0, the GPU line's own inputs."""
+    (pos, neg), = rank_batches(w, 0, 1)[0][:1]
+    src = rank_batches(w, 0, 1)[1]
+    return torch.from_numpy(pos[:rows]), torch.from_numpy(neg[:rows]), src
 
 
 def run_step(m, pos, neg, mode, fn, ev=None):
@@ -224,11 +265,20 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
 
         def step(b, i):
             return sk.train_step(b[0], b[1], b[2], i % 2)
+    elif w.get("scheme") == "gather":
+        def step(b, i):
+            return sk.step_forward_gather(b[0], b[1], i % 2)
     else:
-        fwd = sk.step_forward_gather if w.get("scheme") == "gather" else sk.step_forward
+        # the exchange plan of step i + 1 (kge_shard_plan: ownership counts and ranks from the ids, its
+        # split sizes copied to the host asynchronously) is issued before step i's work, so the host
+        # never waits for it; it is device work inside the timed region like the rest of the step
+        plans = {}
 
         def step(b, i):
-            return fwd(b[0], b[1], i % 2)
+            nb = batches[(i + 1) % 4]
+            plan = plans.pop(i, None) or sk.plan(b[0], b[1], i % 2)
+            plans[i + 1] = sk.plan(nb[0], nb[1], (i + 1) % 2)
+            return sk.step_forward(b[0], b[1], i % 2, plan=plan)
     for i in range(a.warmup):
         step(batches[i % 4], i)
     torch.cuda.synchronize()
@@ -237,7 +287,7 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
+    for i in range(a.warmup, a.warmup + a.steps):
         step(batches[i % 4], i)
     torch.cuda.synchronize()
     if dist_on:
@@ -245,77 +295,130 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
     return time.perf_counter() - t0
 
 
-def shard_sim_bench(device, world=8, reps=10):
+def shard_sim_bench(device, world=8, reps=10, v1=None):
     """Single-GPU evidence for the row-sharded scaling at the full C4 size (YAGO3-10
-    DistMult d=500, E=123182, N=1024): ONE rank's kernels of a simulated `world`-way split, on the
-    global batch of world x 512 rows, timed with events on the launch stream, against the unsharded
-    kernel on the same global batch (what one GPU holding the whole table would run)."""
-    from customknowledgegraphembedding_amd.distributed import HipShardKernels, ShardedKGE
+    DistMult d=500, E=123182, N=1024, global batch of world x 512 rows):
+      * the WHOLE `world`-rank forward step on this GPU: every rank a thread (ThreadComm: the
+        all-gather / all-to-all are device copies here), every rank's kernels serialised on one device;
+      * rank 0's own kernels of one step (plan, per-chunk query gather and compact scoring, finish),
+        timed alone with events on the launch stream: the per-GPU compute of an N-GPU step;
+      * the payload rank 0's collectives carry per step, and the RCCL bandwidth a step needs to reach
+        6x the 1-GPU row-sharded throughput `v1` (triples/s) when the collectives do not overlap;
+      * the sharded train step's kernels of rank 0 (forward, combine, backward)."""
+    from customknowledgegraphembedding_amd.distributed import HipShardKernels, ShardedKGE, ThreadComm, run_threads
     from customknowledgegraphembedding_amd.model import TFKGEModel
     w = WORKLOADS["c4s"]
     E, d, N = w["nentity"], w["hidden_dim"], w["N"]
     pos, neg, wt = _global_batches(w, world, 1, device)[0]
     Bg = pos.shape[0]
+    B = Bg // world
     full = TFKGEModel("DistMult", E, w["nrelation"], d, w["gamma"], device=device, seed=0)
     ent, rel = full.entity_embedding.detach(), full.relation_embedding.detach()
-    sk = ShardedKGE("DistMult", E, w["nrelation"], d, w["gamma"], device=device, seed=0, world=world, rank=0)
+    tables = (ent, rel, full._gamma_f, full._range_f, 0.0)
     fn = FN_IDS["DistMult"]
-    qent = ent[pos[:, 2]].contiguous()  # head-batch query rows (assembled by the all-reduce on N GPUs)
-    qpos = ent[pos[:, 0]].contiguous()
-    out = torch.empty((Bg, N), dtype=torch.float32, device=device)
 
-    def timed(f):
+    def timed(f, n=reps):
         f()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(reps):
+        for _ in range(n):
             f()
         e1.record()
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / reps * 1e3  # us
+        return e0.elapsed_time(e1) / n * 1e3  # us
 
     unsharded_us = timed(lambda: ops.score_indexed_raw(fn, 0, ent, rel, 0, pos, neg, d, full._gamma_f, full._range_f))
-    shard_us = timed(lambda: HipShardKernels.score_sharded(fn, 0, qent, rel, 0, sk.shard, sk.lo, pos, neg, d,
-                                                           full._gamma_f, full._range_f, 0.0, out))
-    sk.configure_optimizer()
-    bufs = HipShardKernels.train_alloc(sk, Bg, N)
-    train_fwd_us = timed(lambda: HipShardKernels.train_forward(sk, bufs, 0, qent, qpos, pos, neg, wt))
-    # the whole sharded train step of a simulated world: `world` ranks as threads on this GPU (ThreadComm),
-    # then rank 0's three calls timed on their own (kernels only; the collectives are priced from their sizes)
-    from customknowledgegraphembedding_amd.distributed import ThreadComm, run_threads
     comm = ThreadComm(world)
-    ranks = [ShardedKGE("DistMult", E, w["nrelation"], d, w["gamma"], device=device, seed=0, world=world, rank=r,
-                        comm=comm).configure_optimizer(lr=5e-5) for r in range(world)]
-    for i in range(2):
-        run_threads([lambda sk=x: sk.train_step(pos, neg, wt, i % 2) for x in ranks])
-    torch.cuda.synchronize()
-    r0 = ranks[0]
-    b0 = r0._bufs[(Bg, N)]
+    ranks = [ShardedKGE("DistMult", E, w["nrelation"], d, w["gamma"], device=device, world=world, rank=r, comm=comm,
+                        full_tables=tables) for r in range(world)]
+    t0 = time.perf_counter()
+    sim_dev_us = timed(lambda: run_threads([lambda sk=sk: sk.step_forward(pos, neg, 0) for sk in ranks]), 3)
+    sim_wall_us = (time.perf_counter() - t0) / 4 * 1e6
+    # rank 0 alone: the kernels of one step, with the other ranks' contributions prepared untimed
     HK = HipShardKernels
-    qa, qb = qent, qpos
-    stats_all = torch.stack([x._bufs[(Bg, N)]["stats"] for x in ranks])
-    t_fwd = timed(lambda: HK.train_forward(r0, b0, 0, qa, qb, pos, neg, wt))
-    t_comb = timed(lambda: HK.train_combine(r0, b0, 0, qa, qb, pos, neg, wt, stats_all))
-    t_bwd = timed(lambda: HK.train_backward(r0, b0, 0, qa, qb, pos, neg, wt, 3, None))
-    del ranks, comm
-    coll_bytes = {"query_rows_allreduce": 2 * Bg * d * 4, "stats_allgather": world * Bg * 16,
-                  "query_grad_allreduce": 2 * Bg * d * 4}
-    owned = (((neg >= sk.lo) & (neg < sk.hi)).sum().item())
-    per_cand = 4 * d + 12
-    return {"workload": f"C4 YAGO3-10 DistMult d=500 N=1024, global batch {world} x 512, one rank of a simulated "
-                        f"{world}-way row split (rows [{sk.lo}, {sk.hi}))",
-            "unsharded_global_kernel_us": unsharded_us, "rank_score_kernel_us": shard_us,
-            "rank_over_unsharded": shard_us / unsharded_us,
-            "rank_train_forward_kernels_us": train_fwd_us,
-            "rank_train_step_kernels_us": {"forward": t_fwd, "combine": t_comb, "backward": t_bwd,
-                                           "total": t_fwd + t_comb + t_bwd},
-            "rank_train_triples_per_s_kernels_only": world * 512 * (N + 1) / ((t_fwd + t_comb + t_bwd) * 1e-6),
-            "collective_bytes_per_step": coll_bytes,
-            "owned_candidates": owned, "owned_fraction": owned / (Bg * N),
-            "rank_score_kernel_gbs": owned * per_cand / (shard_us * 1e-6) / 1e9,
-            "what": "kge_score_sharded (owned candidates compacted per wave) vs kge_score_indexed over the whole "
-                    "global batch; kge_shard_train_forward = the sharded train step's gather pass"}
+    r0 = ranks[0]
+    plan = r0.plan(pos, neg, 0)
+    tot, qtot = plan.summary()
+    K, nc = plan.chunks, plan.ncol
+    Rk, hpc = Bg // K, world // K
+    caps = [max(1, int(qtot[k].max())) for k in range(K)]
+    blocks, qidxs, sends = [], [], []
+    for k in range(K):
+        blk = torch.empty((world, nc, caps[k], r0.entity_dim), dtype=torch.float32, device=device)
+        qidx = torch.empty((nc, Rk), dtype=torch.int64, device=device)
+        for sk in ranks:  # every owner's compacted rows: the all-gather's result
+            HK.gather_queries(sk, plan, pos, k * Rk, Rk, caps[k], blk[sk.rank], qidx)
+        blocks.append(blk.view(-1, r0.entity_dim))
+        qidxs.append(qidx)
+        sends.append(torch.empty(int(sum(tot[h, 0] for h in range(k * hpc, (k + 1) * hpc))), dtype=torch.float32,
+                                 device=device))
+    # home 0's all-to-all output: every owner's block of home 0's rows, in rank order
+    recv = []
+    for sk in ranks:
+        snd = torch.empty(int(sum(tot[h, sk.rank] for h in range(hpc))), dtype=torch.float32, device=device)
+        HK.score_compact(sk, 0, blocks[0], qidxs[0][0], pos, neg, plan, 0, Rk, snd)
+        HK.score_compact(sk, 3, blocks[0], qidxs[0][-1], pos, neg, plan, 0, Rk, snd)
+        recv.append(snd[:int(tot[0, sk.rank])])
+    recv = torch.cat(recv)
+    q_send = torch.empty((nc, max(caps), r0.entity_dim), dtype=torch.float32, device=device)
+
+    def rank0_gather():
+        for k in range(K):
+            HK.gather_queries(r0, plan, pos, k * Rk, Rk, caps[k], q_send, qidxs[k])
+
+    def rank0_score():
+        for k in range(K):
+            HK.score_compact(r0, 0, blocks[k], qidxs[k][0], pos, neg, plan, k * Rk, Rk, sends[k])
+            HK.score_compact(r0, 3, blocks[k], qidxs[k][-1], pos, neg, plan, k * Rk, Rk, sends[k])
+
+    t_plan = timed(lambda: HK.plan(r0, pos, neg, 0, K))
+    t_gather = timed(rank0_gather)
+    t_score = timed(rank0_score)
+    t_finish = timed(lambda: HK.shard_finish(r0, plan, recv, pos, neg, 1.0, True))
+    rank_us = t_plan + t_gather + t_score + t_finish
+    cb = r0.collective_bytes(plan)
+    coll = cb["query_rows_allgather"] + cb["scores_alltoall"]
+    out = {"workload": f"C4 YAGO3-10 DistMult d=500 N=1024, global batch {world} x 512 (YAGO3-10 positives), "
+                       f"entity table split over {world} simulated ranks",
+           "step_us_all_ranks_one_gpu": sim_dev_us,
+           "step_wall_us_all_ranks_one_gpu": sim_wall_us,
+           "rank_step_kernels_us": {"plan": t_plan, "query_gather": t_gather, "compact_scoring": t_score,
+                                    "finish": t_finish, "total": rank_us},
+           "unsharded_global_kernel_us": unsharded_us,
+           "rank_scoring_over_unsharded": t_score / unsharded_us,
+           "collective_bytes_per_rank_step": cb,
+           "zero_padded_round2_bytes_per_rank_step": {"query_rows_allreduce": 2 * (world - 1) * Bg * d * 4 * nc // world,
+                                                       "scores_reduce_scatter": (world - 1) * B * (N + 1) * 4},
+           "chunks": K,
+           "what": "step_us_all_ranks_one_gpu: the whole 8-rank ShardedKGE.step_forward run by 8 threads on this "
+                   "GPU (every rank's kernels serialised, ThreadComm device copies for RCCL); rank_step_kernels_us: "
+                   "rank 0's kernels of one step alone (its per-GPU compute in an 8-GPU step)"}
+    if v1:
+        t6 = world * B * (N + 1) / (6.0 * v1) * 1e6  # us per step at 6x the 1-GPU throughput
+        out["six_x_target"] = {"one_gpu_triples_per_s": v1, "step_budget_us": t6,
+                               "collective_budget_us_without_overlap": t6 - rank_us,
+                               "rccl_gbps_needed_without_overlap": (coll / ((t6 - rank_us) * 1e-6) / 1e9
+                                                                    if t6 > rank_us else None)}
+    # the sharded train step's kernels of rank 0 (forward, combine, backward), collectives priced by size
+    sk = ShardedKGE("DistMult", E, w["nrelation"], d, w["gamma"], device=device, world=world, rank=0,
+                    full_tables=tables).configure_optimizer(lr=5e-5)
+    qent = ent[pos[:, 2]].contiguous()  # head-batch query rows (the all-gather's result)
+    qpos = ent[pos[:, 0]].contiguous()
+    bufs = HK.train_alloc(sk, Bg, N)
+    HK.train_forward(sk, bufs, 0, qent, qpos, pos, neg, wt)
+    stats_all = bufs["stats"].unsqueeze(0).expand(world, -1, -1).contiguous()
+    t_fwd = timed(lambda: HK.train_forward(sk, bufs, 0, qent, qpos, pos, neg, wt))
+    t_comb = timed(lambda: HK.train_combine(sk, bufs, 0, qent, qpos, pos, neg, wt, stats_all))
+    t_bwd = timed(lambda: HK.train_backward(sk, bufs, 0, qent, qpos, pos, neg, wt, 3, None))
+    out["rank_train_step_kernels_us"] = {"forward": t_fwd, "combine": t_comb, "backward": t_bwd,
+                                         "total": t_fwd + t_comb + t_bwd}
+    tplan = sk.plan(pos, pos[:, :0], 0, chunks=1)  # the train step's query plan (one chunk)
+    cap1 = max(1, int(tplan.summary()[1][0].max()))
+    out["train_collective_bytes_per_rank_step"] = {
+        "query_rows_allgather": (world - 1) * nc * cap1 * d * 4,
+        "stats_allgather": (world - 1) * Bg * 16, "query_grad_allreduce_ring": 2 * (world - 1) * 2 * Bg * d * 4 // world}
+    return out
 
 
 def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
@@ -591,10 +694,9 @@ def cpu_baseline(w, budget_s=15.0, rows=64):
     ent_dim, rel_dim, D, _ = dims(w)
     ent, rel, rng = O.make_tables(w["nentity"], w["nrelation"], ent_dim, rel_dim, w["gamma"],
                                   w["hidden_dim"], seed=0, dtype=torch.float32)
-    g = np.random.RandomState(1)
-    E, R, N = w["nentity"], w["nrelation"], w["N"]
-    pos = torch.from_numpy(np.stack([g.randint(E, size=rows), g.randint(R, size=rows), g.randint(E, size=rows)], 1))
-    neg = torch.from_numpy(np.random.RandomState(2).randint(E, size=(rows, N)))
+    # the same inputs as the timed GPU steps: the first `rows` rows of rank 0's batch 0 (make_inputs)
+    N = w["N"]
+    pos, neg, src = cpu_baseline_inputs(w, rows)
     mod = 0.5 * rng
 
     def faithful(mode):
@@ -629,9 +731,9 @@ def cpu_baseline(w, budget_s=15.0, rows=64):
         "unit": "triples/s",
         "cores": cores,
         "kind": "port",
-        "sample": (f"{rows} batch rows x {N} negatives of {w['name']}: oracle torch-CPU fp32 restatement of "
-                   f"the reference TF graph (2 calls/step, all 3 branches each, Q2), median of "
-                   f"{res['faithful'][1]} steps"),
+        "sample": (f"the first {rows} batch rows x {N} negatives of the GPU line's batch 0 ({w['name']}; positives: "
+                   f"{src}, negatives RandomState(2).randint(E)): oracle torch-CPU fp32 restatement of the reference "
+                   f"TF graph (2 calls/step, all 3 branches each, Q2), median of {res['faithful'][1]} steps"),
         "useful_only_value": triples / res["useful"][0],
         "cpu_model": cpu_model,
     }
@@ -760,13 +862,15 @@ def main(argv=None):
                 "roofline": {"bound": "hbm", "achieved": owned_bytes / (elapsed / a.steps) / 1e9,
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": owned_bytes / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                             "kernel": "whole sharded step (gather, all-reduce, score, reduce-scatter, finish)"}}
+                             "kernel": "whole sharded step (plan, query all-gather, compact scoring, score "
+                                       "all-to-all, finish)"},
+                "build": kge.build_id()}
         if rank == 0:
             print(json.dumps(line), flush=True)
         if dist:
             tdist.destroy_process_group()
         return
-    m, batches = make_inputs(w, rank, device)
+    m, batches = make_inputs(w, rank, device, world=world)
 
     def barrier():
         if dist:
@@ -829,7 +933,6 @@ def main(argv=None):
     ent_dim_, _, _, _ = dims(w)
     pos0, neg0 = batches[0]
     uniq = torch.unique(torch.cat([neg0.reshape(-1), pos0[:, 0], pos0[:, 2]])).numel()
-    achieved = step_bytes / kern_avg_s / 1e9
     triples = (B * N + B) * a.steps * world
     value = triples / elapsed
     line = {
@@ -848,18 +951,14 @@ def main(argv=None):
                 "; negatives RandomState(2).randint(E); 8 distinct batches resident in HBM, mode alternating head/tail",
         "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N, "hidden_dim": w["hidden_dim"],
                    "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/step",
-                     "traffic_source": traffic_src,
-                     "kernel": ("step_fwd_xcd_kernel + neg_rows_kernel (the step's two launches: negatives and "
-                                "positives gathered in XCD-sliced ascending-id order, then the row reductions)" if xcd
-                                else "step_fwd_kernel (negatives + positives + row reductions, one launch)"),
-                     "kernel_avg_us": kern_avg_s * 1e6,
-                     "kernel_avg_us_head_batch": head_ms[0] * 1e3,
-                     "kernel_avg_us_tail_batch": tail_ms[0] * 1e3,
-                     "algorithmic_bytes_per_launch": step_bytes,
-                     "unique_row_bytes_per_step": uniq * ent_dim_ * 4,
-                     "row_reuse": (B * N + 2 * B) / max(1, uniq)},
+        "roofline": roofline_hbm(
+            step_bytes, traffic, traffic_src, kern_avg_s,
+            kernel=("step_fwd_xcd_kernel + neg_rows_kernel (the step's two launches: negatives and positives "
+                    "gathered in XCD-sliced ascending-id order, then the row reductions)" if xcd
+                    else "step_fwd_kernel (negatives + positives + row reductions, one launch)"),
+            kernel_avg_us_head_batch=head_ms[0] * 1e3, kernel_avg_us_tail_batch=tail_ms[0] * 1e3,
+            unique_row_bytes_per_step=uniq * ent_dim_ * 4, row_reuse=(B * N + 2 * B) / max(1, uniq)),
+        "build": kge.build_id(),
     }
     if a.train_steps > 0:
         line["train_step"] = train_step_bench(m, batches, a.train_steps, 5)
@@ -894,7 +993,7 @@ def main(argv=None):
                     "per candidate row, RCCL all-reduce of query rows, all-gather of [Bg,4] row stats, all-reduce "
                     "of query gradients; Adam on the shard"}
         if world == 1:
-            line["yago3_10_shard_sim8"] = shard_sim_bench(device)
+            line["yago3_10_shard_sim8"] = shard_sim_bench(device, v1=line["yago3_10_rowshard"]["triples_per_s"])
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w, a.cpu_budget)
     if rank == 0:

@@ -5,9 +5,9 @@ supervisor.py's negative-sample scoring step, and the upstream KGEModel lookup/s
 Scoring runs in hand-written gfx950 HIP kernels inside libkge_hip.so (C-ABI: include/kge_hip.h),
 called through ctypes on torch's current stream. There is no CPU / eager fallback.
 """
-from ._lib import FN_IDS, HEAD_BATCH, SINGLE, TAIL_BATCH, KGEHipError, load  # noqa: F401
+from ._lib import FN_IDS, HEAD_BATCH, SINGLE, TAIL_BATCH, KGEHipError, build_id, load  # noqa: F401
 from .model import KGEModel, TFKGEModel  # noqa: F401
 from . import ops  # noqa: F401
 
-__all__ = ["TFKGEModel", "KGEModel", "ops", "load", "KGEHipError", "FN_IDS",
+__all__ = ["TFKGEModel", "KGEModel", "ops", "load", "build_id", "KGEHipError", "FN_IDS",
            "HEAD_BATCH", "TAIL_BATCH", "SINGLE"]

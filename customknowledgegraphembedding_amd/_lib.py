@@ -58,6 +58,22 @@ SIGNATURES = {
     ),
     "kge_gather_rows": (
         _c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
+    "kge_build_id": (ctypes.c_char_p, []),
+    "kge_source_hash": (ctypes.c_char_p, []),
+    "kge_shard_plan": (
+        _c_i, [_c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "kge_shard_gather_queries": (
+        _c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p,
+               _c_i64, _c_p, _c_p, _c_p]),
+    "kge_score_sharded_compact": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64,
+         _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i64,
+         _c_i64, _c_p, _c_p],
+    ),
+    "kge_shard_finish": (
+        _c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_i64,
+               _c_p, _c_p, _c_p, _c_p]),
     "kge_eval_query": (
         _c_i, [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
     "kge_gemm_nt": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p]),
@@ -167,6 +183,33 @@ def load(path: str | None = None):
         if path is None:
             _lib = lib
         return lib
+
+
+def source_hash(root: str | None = None) -> str:
+    """The sha256 (16 hex digits) of the sources libkge_hip.so is built from, by the Makefile's recipe
+    (make's byte-order sort of: include/kge_hip.h by absolute path, Makefile, csrc/*.{hip,cpp,h}). It
+    equals the loaded library's kge_source_hash() exactly when the library was built from this tree."""
+    import glob
+    import hashlib
+
+    pkg = root or _HERE
+    top = os.path.dirname(os.path.abspath(pkg))
+    rel = ["Makefile"] + [os.path.relpath(p, pkg) for ext in ("hip", "cpp", "h")
+                          for p in glob.glob(os.path.join(pkg, "csrc", "*." + ext))]
+    files = [os.path.join(top, "include", "kge_hip.h")] + [os.path.join(pkg, r) for r in sorted(rel)]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> dict:
+    """Provenance of the loaded library: its build id string and source hash, and whether that hash
+    matches the sources in this tree."""
+    lib = load()
+    sh = lib.kge_source_hash().decode()
+    return {"build_id": lib.kge_build_id().decode(), "source_hash": sh, "source_hash_matches_tree": sh == source_hash()}
 
 
 def check(rc: int, what: str) -> None:

@@ -486,6 +486,7 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         // sharded scoring compacts each wave's owned candidates: long runs (up to 512 ids, ~64 owned
         // at 8 shards) keep the per-wave query build amortised; >= 8192 waves still fill the chip
         p.cpw = p.skip_foreign ? pick_cpw_sharded(p.B, p.N) : pick_cpw(p.B, p.N);
+        if (p.cmp_pre) p.cpw = (int)std::max<int64_t>(p.N, 1);  // compact ranks: one wave walks the whole row
         p.wpr = (int)((p.N + p.cpw - 1) / p.cpw);
         waves = p.B * p.wpr;
     }
@@ -720,6 +721,48 @@ int kge_score_sharded(int fn, int mode, const float* qent, int64_t q_ld, const f
     if (mode != KGE_SINGLE && shard_lo >= 0 && shard_lo + shard_rows < ((int64_t)1 << 31) &&
         use_xcd_order(shard_rows, N))
         return run_score(fn, mode, p, KIND_SCORE_SHARD_XCD, stream);  // XCD-sliced order over the shard
+    return run_score(fn, mode, p, KIND_FWD, stream);
+}
+
+int kge_score_sharded_compact(int fn, int mode, const float* qent, int64_t q_rows, int64_t q_ld, const int64_t* q_idx,
+                              const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off, const float* shard,
+                              int64_t shard_rows, int64_t shard_ld, int64_t shard_lo, const int64_t* pos,
+                              const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma,
+                              float emb_range, float modulus, const int* pre, const int* cnt, const int* tot,
+                              int world, int rank, int64_t home_B, int64_t home0, float* send, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (B < 0 || N < 0 || D <= 0 || shard_rows < 0 || q_rows < 0) return fail(KGE_EINVAL, "bad shape");
+    if (world < 1 || rank < 0 || rank >= world || home_B <= 0 || B % home_B || home0 < 0 ||
+        home0 + B / home_B > world)
+        return fail(KGE_EINVAL, "kge_score_sharded_compact: rows must be whole homes of home_B rows");
+    if (empty(B, mode == KGE_SINGLE ? 1 : N)) return ok();
+    if (!pos || (mode != KGE_SINGLE && !neg) || !send || !qent || !q_idx || !shard || !pre || !cnt || !tot)
+        return fail(KGE_EINVAL, "null pointer");
+    ScoreParams p;
+    fill_indexed(p, fn, mode, shard, shard_rows, shard_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
+                 D, gamma, emb_range, modulus);
+    // query entity rows: row q_idx[b] of the all-gathered query block
+    p.qent = qent;
+    p.q_idx = q_idx;
+    p.q_stride = 1;
+    p.q_ld = q_ld;
+    p.q_rows = q_rows;
+    p.c_base = shard_lo;
+    p.skip_foreign = 1;
+    p.cmp_pre = pre;
+    p.cmp_cnt = cnt;
+    p.cmp_tot = tot;
+    p.cmp_home0 = home0;
+    p.cmp_last = mode == KGE_SINGLE;
+    p.home_B = home_B;
+    p.world = world;
+    p.rank = rank;
+    p.out = send;
+    p.out_ld = 0;
+    if (mode != KGE_SINGLE && shard_lo >= 0 && shard_lo + shard_rows < ((int64_t)1 << 31) &&
+        use_xcd_order(shard_rows, N))
+        return run_score(fn, mode, p, KIND_SCORE_SHARD_XCD, stream);
     return run_score(fn, mode, p, KIND_FWD, stream);
 }
 

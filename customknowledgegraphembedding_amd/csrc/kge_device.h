@@ -581,14 +581,29 @@ __device__ __forceinline__ int kth_set_bit(uint64_t m, int k) {
 // value of `v` in lane `src` (every lane must execute this)
 __device__ __forceinline__ int lane_pull(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
 
+// number of set bits of m in the lanes below this one
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Start of batch row b's run in the compact send block (ScoreParams::cmp_pre): the row's home-local
+// prefix plus this rank's owned counts of the launch's earlier homes.
+__device__ __forceinline__ int64_t cmp_row_off(const ScoreParams& p, int64_t b) {
+    const int64_t h = b / p.home_B;
+    int64_t off = p.cmp_pre[b];
+    for (int64_t k = 0; k < h; ++k) off += p.cmp_tot[(p.cmp_home0 + k) * p.world + p.rank];
+    return off;
+}
+
 // Walks candidates [lo, hi) of batch row b and calls body(row, n, cnt) with the owned ones compacted
 // into lanes 0..cnt-1 (row: local shard row, n: candidate column), in candidate order; every call but
 // the last has cnt = 64. With zero_out, a foreign candidate's score slot p.out[b, n] is written 0 (the
-// partial score block a SUM over shards assembles).
+// partial score block a SUM over shards assembles). In compact mode (p.cmp_pre) n is instead the
+// candidate's rank among the row's owned ones (the walk then covers the whole row: lo = 0).
 template <class Body>
 __device__ __forceinline__ void for_owned_runs(const ScoreParams& p, int64_t b, int64_t lo, int64_t hi, int lane,
                                                bool zero_out, Body&& body) {
-    int buf_row = 0, buf_n = 0, fill = 0;
+    int buf_row = 0, buf_n = 0, fill = 0, run = 0;
     for (int64_t c0 = lo; c0 < hi; c0 += kWave) {
         const int64_t n = c0 + lane;
         int64_t row = -1;
@@ -597,8 +612,13 @@ __device__ __forceinline__ void for_owned_runs(const ScoreParams& p, int64_t b, 
         if (zero_out && n < hi && !own) p.out[b * p.out_ld + n] = 0.f;
         const uint64_t m = __ballot(own);
         const int cnt = __popcll(m);
+        int n32 = (int)n;
+        if (p.cmp_pre) {
+            n32 = run + lanes_below(m);
+            run += cnt;
+        }
         if (cnt == 0) continue;  // wave-uniform
-        const int row32 = (int)row, n32 = (int)n;
+        const int row32 = (int)row;
         // lanes [fill, min(fill + cnt, 64)) take the first owned candidates of this chunk
         const int d = lane - fill;
         const bool take = d >= 0 && d < cnt;
@@ -627,11 +647,14 @@ __device__ __forceinline__ void for_owned_runs(const ScoreParams& p, int64_t b, 
 template <int FN, bool CH, int V, int G>
 __device__ __forceinline__ void score_owned(const ScoreParams& p, const Query<FN, CH, V, G>& q, int64_t b, int64_t lo,
                                             int64_t hi, int lane) {
-    for_owned_runs(p, b, lo, hi, lane, true, [&](int row, int n, int cnt) {
+    const bool cmp = p.cmp_pre != nullptr;
+    const int64_t off = cmp ? cmp_row_off(p, b) : 0;
+    for_owned_runs(p, b, lo, hi, lane, !cmp, [&](int row, int n, int cnt) {
         const int64_t my_id = (int64_t)row + p.c_base;
         float2 st;
         const float s = score_lanes<FN, CH, V, G, false>(p, q, my_id, cnt, lane, st);
-        if (lane < cnt) p.out[b * p.out_ld + n] = s;
+        if (lane < cnt)
+            p.out[cmp ? (p.cmp_last ? off + p.cmp_cnt[b] - 1 : off + n) : b * p.out_ld + n] = s;
     });
 }
 
@@ -655,7 +678,7 @@ __device__ __forceinline__ void score_owned(const ScoreParams& p, const Query<FN
 template <class Body>
 __device__ __forceinline__ void for_slice_runs_sorted(const ScoreParams& p, int64_t b, int64_t e_lo, int64_t e_hi,
                                                       bool take_invalid, bool zero_foreign, int lane, Body&& body) {
-    int buf_key = INT32_MAX, buf_id = -1, buf_n = 0, fill = 0;
+    int buf_key = INT32_MAX, buf_id = -1, buf_n = 0, fill = 0, run = 0;
     auto flush = [&](int cnt) {
         // sort key: (id - e_lo) << 6 | source lane (invalid ids first, as id - e_lo = 0)
         const int key = wave_sort_asc(lane < cnt ? buf_key : INT32_MAX, lane);
@@ -670,10 +693,16 @@ __device__ __forceinline__ void for_slice_runs_sorted(const ScoreParams& p, int6
         const bool valid = id >= p.c_base && id < p.c_base + p.c_rows;
         const bool own = n < p.N && (valid ? (id >= e_lo && id < e_hi) : take_invalid);
         if (zero_foreign && n < p.N && !valid) p.out[b * p.out_ld + n] = 0.f;
+        int n32 = (int)n;
+        if (p.cmp_pre) {  // compact mode: n becomes the rank among the row's candidates in the table
+            const uint64_t mv = __ballot(n < p.N && valid);
+            n32 = run + lanes_below(mv);
+            run += __popcll(mv);
+        }
         const uint64_t m = __ballot(own);
         const int cnt = __popcll(m);
         if (cnt == 0) continue;  // wave-uniform
-        const int id32 = valid ? (int)id : -1, n32 = (int)n, rl = valid ? (int)(id - e_lo) : 0;
+        const int id32 = valid ? (int)id : -1, rl = valid ? (int)(id - e_lo) : 0;
         const int d = lane - fill;
         const bool take = d >= 0 && d < cnt;
         const int src = kth_set_bit(m, take ? d : 0);
@@ -783,12 +812,14 @@ score_sharded_xcd_kernel(ScoreParams p) {
     int64_t qi, ri;
     bool qok, rok;
     build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+    const bool cmp = p.cmp_pre != nullptr;
+    const int64_t off = cmp ? cmp_row_off(p, b) : 0;
     auto run = [&](const auto& qq) {
         const bool sh = p.skip_foreign != 0;
-        for_slice_runs_sorted(p, b, e_lo, e_hi, !sh && x == 0, sh && x == 0, lane, [&](int id, int n, int cnt) {
+        for_slice_runs_sorted(p, b, e_lo, e_hi, !sh && x == 0, sh && !cmp && x == 0, lane, [&](int id, int n, int cnt) {
             float2 st;
             const float s = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, 1>(p, qq, (int64_t)id, cnt, lane, st);
-            if (lane < cnt) p.out[b * p.out_ld + n] = s;
+            if (lane < cnt) p.out[cmp ? off + n : b * p.out_ld + n] = s;
         });
     };
     if constexpr (FN == KGE_INTERHT) {
@@ -848,14 +879,9 @@ __device__ __forceinline__ float row_reduce(const float* row, int64_t N, float T
 // The row reduction of kge_step_forward's XCD-sliced form: out_neg[b] = sum softmax(T s) logsigmoid(-s)
 // or mean logsigmoid(-s) over row b's scores (model.py:168-171), one wave per row. The row is loaded
 // into registers in one round (N <= 64 NR) and reduced in row_reduce's exact order (bitwise its result).
+// row_reduce_vals: the same reduction on values already in registers (v[k] = row[lane + 64 k]).
 template <int NR>
-__device__ __forceinline__ float row_reduce_regs(const float* row, int64_t N, float T, int adversarial, int lane) {
-    float v[NR];
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-        const int64_t n = lane + (int64_t)k * kWave;
-        v[k] = n < N ? row[n] : 0.f;
-    }
+__device__ __forceinline__ float row_reduce_vals(const float (&v)[NR], int64_t N, float T, int adversarial, int lane) {
     if (adversarial) {
         float m = -INFINITY;
 #pragma unroll
@@ -877,6 +903,17 @@ __device__ __forceinline__ float row_reduce_regs(const float* row, int64_t N, fl
     for (int k = 0; k < NR; ++k)
         if (lane + (int64_t)k * kWave < N) wsum += log_sigmoid(-v[k]);
     return wave_sum(wsum) / (float)N;
+}
+
+template <int NR>
+__device__ __forceinline__ float row_reduce_regs(const float* row, int64_t N, float T, int adversarial, int lane) {
+    float v[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const int64_t n = lane + (int64_t)k * kWave;
+        v[k] = n < N ? row[n] : 0.f;
+    }
+    return row_reduce_vals<NR>(v, N, T, adversarial, lane);
 }
 
 // row_reduce with the row loaded in one round for N <= 1024 (bitwise row_reduce's result)

@@ -56,6 +56,15 @@ struct ScoreParams {
     int64_t c_ld, c_stride, c_rows, c_dense;
     int64_t c_base;    // candidate ids are global: row = id - c_base (row-sharded tables)
     int skip_foreign;  // sharded scoring: a candidate outside [c_base, c_base + c_rows) scores 0, no work
+    // compact output of the row-sharded score exchange (kge_score_sharded_compact): only this rank's owned
+    // scores are written, row b's at out[cmp_off(b) + k], k = the candidate's rank among the row's owned
+    // ones in column order (the positive, scored by a second launch, last). cmp_off(b) = cmp_pre[b] + the
+    // owned counts of the launch's earlier homes: the send block of an all-to-all, home-major.
+    const int* cmp_pre;   // [B] home-local exclusive prefix of this rank's owned counts (null: dense out)
+    const int* cmp_cnt;   // [B] this rank's owned candidates of each row (negatives + the positive)
+    const int* cmp_tot;   // [W * W] tot[h * W + o]: candidates of home h's rows owned by rank o
+    int64_t cmp_home0;    // home of the launch's row 0 (its rows are whole homes of home_B rows)
+    int cmp_last;         // the positives' launch: a row's score takes the last slot of its run
     float* out;
     int64_t out_ld;
     int64_t B, N;

@@ -5,23 +5,25 @@ Two layouts:
 * Replicas (C2 WN18RR, C3 FB15k-237; any table that fits one GPU's 288 GB): every rank holds the
   whole table and scores its own batch rows; the data path has no collective (bench.py --gpus N).
 * Row-sharded owner-computes (`ShardedKGE`; C4 YAGO3-10 as the north star names it, and any table
-  larger than one GPU): rank r owns entity rows [lo_r, hi_r). The global batch (W*B rows) is known
-  to every rank (the sampler seed is replicated, so no ids move). One step:
-    1. query-entity rows: each rank gathers the rows it owns (zeros elsewhere)      kge_gather_rows
-       -> SUM all-reduce [W*B, ent_dim]                                              RCCL
-    2. every rank scores the candidates it owns (others exactly 0, no traffic) and
-       the positives whose tail it owns                                              kge_score_sharded
-    3. SUM reduce-scatter of the [W*B, N+1] partial scores -> each rank's home rows  RCCL
-    4. home rank: self-adversarial reduction + logsigmoid of its B rows               kge_neg_reduce/...
-  Each (row, candidate) has exactly one owner, so the SUMs add exact zeros: the sharded scores
-  equal the unsharded ones bitwise. (An out-of-range candidate id has no owner and scores 0 here;
-  the unsharded kernels and the gather scheme score it against a zero row, as TF-GPU gather does.) Table rows never cross xGMI; per step a rank moves
-  W*B*ent_dim*4 bytes of query rows and W*B*(N+1)*4 bytes of scores.
-  Pipelining: the global batch is cut into K chunks (each chunk = B/K rows of every home rank, so
-  the reduce-scatter of a chunk still lands on the home ranks). All chunks' query all-reduces are
-  issued up front; chunk k is scored as soon as its all-reduce completes while chunk k+1's
-  all-reduce and chunk k-1's reduce-scatter run on RCCL's stream, so the collectives hide behind
-  the scoring kernels.
+  larger than one GPU): rank r owns entity rows [lo_r, hi_r). The global batch (W*B rows, home rank h
+  owning rows [h B, (h+1) B)) is known to every rank (the sampler seed is replicated, so no ids move),
+  so every rank can work out from the ids alone who owns which row and in which order it will send it:
+  the collectives carry payload only. One step (`step_forward`):
+    0. plan: ownership counts and ranks of the batch's candidates and query rows      kge_shard_plan
+    1. query rows: each owner gathers the query-entity rows it owns, compacted;
+       one ALL-GATHER of [ncol, cap] rows per rank                                     RCCL
+    2. every rank scores only the candidates it owns, writing the scores compacted
+       per row (column order, the row's positive last) into one block per home rank    kge_score_sharded_compact
+    3. one ALL-TO-ALL: home h receives exactly the scores of its rows, no indices       RCCL
+    4. home rank: scatter by the same ranks, self-adversarial reduction, logsigmoid     kge_shard_finish
+  Each (row, candidate) has exactly one owner and is moved once: the sharded scores equal the
+  unsharded ones bitwise. (An out-of-range id has no owner and scores 0 here; the unsharded kernels
+  score it against a zero row, as TF-GPU gather does.) Per step and rank the collectives move
+  ~7/8 of (W B ncol ent_dim) query floats in and ~7/8 of (B (N+1)) scores in, against twice those
+  queries and W times those scores for the zero-padded SUM all-reduce / reduce-scatter of round 2.
+  Pipelining: the global batch is cut into K chunks of W/K whole homes; every chunk's all-gather
+  is issued up front, chunk k is scored as soon as its rows arrived, and its all-to-all runs on
+  RCCL's stream while chunk k+1 is scored.
 
 * Row-sharded gather (`ShardedKGE.step_forward_gather`, the north star's literal scheme, kept beside
   owner-computes as SURVEY §8e asks so the two can be measured against each other): every rank
@@ -31,11 +33,16 @@ Two layouts:
   ent_dim x 4 bytes per rank (C4 at 8 ranks: ~45k rows, ~89 MB) instead of owner-computes' queries
   + scores, which is why owner-computes is the default.
 
-The GPU kernels are reached through a small backend object (`HipShardKernels`); tests on CPU swap
+Every collective goes through a communicator object (`TorchComm`: one torch.distributed call per
+method; `ThreadComm`: the same methods between W threads of one process, so a W-rank step runs on
+one GPU). The GPU kernels are reached through a backend object (`HipShardKernels`); tests on CPU swap
 in an oracle-backed backend to check the orchestration with gloo (tests/test_distributed_cpu.py).
 """
 from __future__ import annotations
 
+import warnings
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -43,6 +50,11 @@ from . import ops
 from ._lib import FN_IDS, HEAD_BATCH, SINGLE, TAIL_BATCH, check
 from . import _lib
 from .model import _dims_for
+
+
+# widest per-half dimension the row-sharded train kernels take (kge_shard_train_*: kFwdGradMaxG float4
+# groups per lane, six accumulators per element in registers); wider models train on the dense path
+SHARD_MAX_D = 1024
 
 
 def shard_bounds(nentity: int, world: int, rank: int):
@@ -53,14 +65,212 @@ def shard_bounds(nentity: int, world: int, rank: int):
     return lo, hi
 
 
+def default_chunks(world: int, chunks=None) -> int:
+    """Chunks of the pipelined sharded forward: a divisor of W (each chunk is W/K whole homes),
+    the largest <= the request (default 4)."""
+    want = max(1, min(int(chunks if chunks is not None else 4), world))
+    while world % want:
+        want -= 1
+    return want
+
+
+def query_cols(mode: int):
+    """Columns of pos holding each batch row's query entity: the negative call's (head-batch: the
+    tail, else the head) and, in head-batch mode, the positive call's (the head)."""
+    return [2, 0] if mode == HEAD_BATCH else [0]
+
+
+# ------------------------------------------------------------------------------------------------
+# communicators
+# ------------------------------------------------------------------------------------------------
+class _Done:
+    """Handle of a collective that already completed."""
+
+    def wait(self):
+        return None
+
+
+class TorchComm:
+    """Every collective of the row-sharded steps, one torch.distributed call each (RCCL on ROCm
+    device tensors, gloo on CPU tensors). async_op=True returns the work handle."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    @property
+    def world(self):
+        return dist.get_world_size(self.group)
+
+    @property
+    def rank(self):
+        return dist.get_rank(self.group)
+
+    @staticmethod
+    def _h(h):
+        return _Done() if h is None else h
+
+    def all_gather_into(self, out, inp, async_op=False):
+        """out [W * inp.numel()] (any shape, contiguous) <- every rank's inp, rank-major."""
+        return self._h(dist.all_gather_into_tensor(out.view(-1), inp.contiguous().view(-1), group=self.group,
+                                                   async_op=async_op))
+
+    def all_to_all(self, out, inp, out_splits, in_splits, async_op=False):
+        """inp [sum(in_splits)] -> rank d gets inp's d-th piece; out [sum(out_splits)] holds the pieces
+        sent to this rank, source-rank-major (torch.distributed.all_to_all_single)."""
+        return self._h(dist.all_to_all_single(out, inp, [int(x) for x in out_splits], [int(x) for x in in_splits],
+                                              group=self.group, async_op=async_op))
+
+    def all_reduce_sum_(self, t, async_op=False):
+        h = self._h(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op))
+        return h if async_op else t
+
+    def broadcast_(self, t, src):
+        dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def all_gather_cat(self, t):
+        """[W, *t.shape], rank-major."""
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self.all_gather_into(out, t)
+        return out
+
+
+class ThreadComm:
+    """The same collectives between W threads of ONE process (one Python thread per simulated rank,
+    all on one device and stream): used to run the W-rank sharded steps on a single GPU. Sums are
+    taken in rank order, as RCCL's result is the same on every rank. `view(rank)` is the per-rank
+    communicator (TorchComm's methods); ShardedKGE takes the ThreadComm itself and makes the view."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self._barrier = threading.Barrier(world, timeout=120)  # a failed rank breaks it instead of hanging
+        self._slots = [None] * world
+
+    def view(self, rank):
+        return _ThreadCommRank(self, rank)
+
+    def _exchange(self, rank, t):
+        self._slots[rank] = t
+        self._barrier.wait()
+        got = list(self._slots)
+        self._barrier.wait()
+        return got
+
+    # rank-explicit forms (kept for callers holding the shared object)
+    def all_gather_cat(self, t, rank):
+        return self.view(rank).all_gather_cat(t)
+
+    def all_reduce_sum_(self, t, rank):
+        return self.view(rank).all_reduce_sum_(t)
+
+
+class _ThreadCommRank:
+    def __init__(self, shared, rank):
+        self.shared, self.rank, self.world = shared, rank, shared.world
+
+    def all_gather_into(self, out, inp, async_op=False):
+        parts = self.shared._exchange(self.rank, inp.contiguous())
+        flat = out.view(-1)
+        n = parts[0].numel()
+        for r, x in enumerate(parts):
+            flat[r * n:(r + 1) * n].copy_(x.view(-1))
+        return _Done()
+
+    def all_to_all(self, out, inp, out_splits, in_splits, async_op=False):
+        got = self.shared._exchange(self.rank, (inp, [int(x) for x in in_splits]))
+        at = 0
+        for src, (x, splits) in enumerate(got):
+            n = splits[self.rank]
+            if n != int(out_splits[src]):
+                raise RuntimeError(f"all_to_all: rank {src} sends {n} to rank {self.rank}, which expects "
+                                   f"{int(out_splits[src])}")
+            off = sum(splits[:self.rank])
+            if n:
+                out[at:at + n].copy_(x[off:off + n])
+            at += n
+        return _Done()
+
+    def all_reduce_sum_(self, t, async_op=False):
+        parts = self.shared._exchange(self.rank, t.clone())
+        acc = parts[0].clone()
+        for x in parts[1:]:
+            acc += x
+        t.copy_(acc)
+        return _Done() if async_op else t
+
+    def broadcast_(self, t, src):
+        parts = self.shared._exchange(self.rank, t)
+        if src != self.rank:
+            t.copy_(parts[src])
+        return t
+
+    def all_gather_cat(self, t):
+        return torch.stack(self.shared._exchange(self.rank, t.contiguous()))
+
+
+def run_threads(fns):
+    """Runs fns[r]() on one thread per simulated rank; returns their results (re-raises the first error)."""
+    import threading
+    res, err = [None] * len(fns), []
+
+    def go(r):
+        try:
+            res[r] = fns[r]()
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+
+    th = [threading.Thread(target=go, args=(r,)) for r in range(len(fns))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if err:
+        raise err[0]
+    return res
+
+
+# ------------------------------------------------------------------------------------------------
+# the exchange plan of one global batch
+# ------------------------------------------------------------------------------------------------
+class ShardPlan:
+    """Ownership counts and ranks of one global batch (kge_shard_plan; identical on every rank).
+    Device arrays: cnt, hpre [W, Bg], qown, qslot [ncol, Bg]; `summary()` -> (tot [W, W], qtot [K,
+    ncol, W]) on the host: tot[h, o] = scores of home h's rows owned by rank o (the all-to-all split
+    sizes), qtot[k, c, o] = chunk k's column-c query rows owned by o (the all-gather caps). The host copy
+    is issued asynchronously when the plan is made: a plan made one step ahead costs no host wait."""
+
+    def __init__(self, world, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summary_dev, summary_host, event):
+        self.world, self.chunks, self.mode, self.Bg, self.N = world, chunks, mode, Bg, N
+        self.ncol = len(query_cols(mode))
+        self.cnt, self.hpre, self.qown, self.qslot = cnt, hpre, qown, qslot
+        self._dev, self._host, self._event = summary_dev, summary_host, event
+        self._parsed = None
+
+    def summary(self):
+        if self._parsed is None:
+            if self._event is not None:
+                self._event.synchronize()
+            s = self._host.numpy().astype(np.int64)
+            W, K, nc = self.world, self.chunks, self.ncol
+            self._parsed = (s[:W * W].reshape(W, W), s[W * W:W * W + K * nc * W].reshape(K, nc, W))
+        return self._parsed
+
+
+# ------------------------------------------------------------------------------------------------
+# kernels
+# ------------------------------------------------------------------------------------------------
+def _st(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
 class HipShardKernels:
     """libkge_hip.so entry points used by ShardedKGE (device tensors, torch's current stream)."""
 
     @staticmethod
     def gather_rows(table, lo, ids, id_stride, n, out):
         rc = _lib.load().kge_gather_rows(table.data_ptr(), table.shape[0], table.stride(0), lo, ids.data_ptr(),
-                                         id_stride, n, out.shape[1], out.data_ptr(), out.stride(0),
-                                         torch.cuda.current_stream(table.device).cuda_stream)
+                                         id_stride, n, out.shape[1], out.data_ptr(), out.stride(0), _st(table))
         check(rc, "kge_gather_rows")
 
     @staticmethod
@@ -71,13 +281,69 @@ class HipShardKernels:
             fn, mode, qent.data_ptr(), qent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), rel_off,
             shard.data_ptr(), shard.shape[0], shard.stride(0), lo, pos.data_ptr(),
             None if mode == SINGLE else neg.data_ptr(), 0 if mode == SINGLE else neg.stride(0), B, N, D,
-            float(gamma), float(emb_range), float(modulus), out.data_ptr(), out.stride(0),
-            torch.cuda.current_stream(shard.device).cuda_stream)
+            float(gamma), float(emb_range), float(modulus), out.data_ptr(), out.stride(0), _st(shard))
         check(rc, "kge_score_sharded")
 
+    # ---- the O(information) exchange of the sharded forward (kge_shard_*; include/kge_hip.h) ----
     @staticmethod
-    def neg_reduce(scores, temperature, adversarial):
-        return ops.neg_reduce_raw(scores, temperature, adversarial)
+    def plan(sk, pos_g, neg_g, mode, chunks):
+        Bg, N = neg_g.shape
+        W = sk.world
+        nc = len(query_cols(mode))
+        i32 = dict(dtype=torch.int32, device=neg_g.device)
+        cnt, hpre = torch.empty((W, Bg), **i32), torch.empty((W, Bg), **i32)
+        qown, qslot = torch.empty((nc, Bg), **i32), torch.empty((nc, Bg), **i32)
+        summ = torch.empty(W * W + chunks * nc * W, **i32)
+        rc = _lib.load().kge_shard_plan(pos_g.data_ptr(), neg_g.data_ptr(), neg_g.stride(0), Bg, N, sk.nentity, W,
+                                        chunks, mode, cnt.data_ptr(), hpre.data_ptr(), qown.data_ptr(),
+                                        qslot.data_ptr(), summ.data_ptr(), _st(neg_g))
+        check(rc, "kge_shard_plan")
+        host = torch.empty(summ.shape, dtype=torch.int32, pin_memory=True)
+        host.copy_(summ, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ShardPlan(W, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summ, host, ev)
+
+    @staticmethod
+    def gather_queries(sk, plan, pos_g, row0, rows, cap, send, qidx):
+        rc = _lib.load().kge_shard_gather_queries(
+            sk.shard.data_ptr(), sk.shard.shape[0], sk.shard.stride(0), sk.lo, pos_g.data_ptr(), plan.Bg, row0, rows,
+            sk.entity_dim, sk.world, sk.rank, plan.mode, plan.qown.data_ptr(), plan.qslot.data_ptr(), cap,
+            send.data_ptr(), qidx.data_ptr(), _st(sk.shard))
+        check(rc, "kge_shard_gather_queries")
+
+    @staticmethod
+    def score_compact(sk, mode, qblock, qidx, pos_g, neg_g, plan, row0, rows, send):
+        """Owned scores of rows [row0, row0 + rows) (whole homes) -> send, compacted."""
+        N = 1 if mode == SINGLE else plan.N
+        Bg = plan.Bg
+        hB = Bg // sk.world
+        rel = sk.relation_embedding
+        pos = pos_g[row0:row0 + rows]
+        neg = None if mode == SINGLE else neg_g[row0:row0 + rows]
+        rc = _lib.load().kge_score_sharded_compact(
+            sk.fn, mode, qblock.data_ptr(), qblock.shape[0], qblock.stride(0), qidx.data_ptr(), rel.data_ptr(),
+            rel.shape[0], rel.stride(0), sk.rel_off, sk.shard.data_ptr(), sk.shard.shape[0], sk.shard.stride(0),
+            sk.lo, pos.data_ptr(), None if neg is None else neg.data_ptr(), 0 if neg is None else neg.stride(0),
+            rows, N, sk.D, float(sk.gamma), float(sk.emb_range), float(sk.modulus),
+            plan.hpre[sk.rank, row0:].data_ptr(), plan.cnt[sk.rank, row0:].data_ptr(), plan._dev.data_ptr(),
+            sk.world, sk.rank, hB, row0 // hB, send.data_ptr(), _st(sk.shard))
+        check(rc, "kge_score_sharded_compact")
+
+    @staticmethod
+    def shard_finish(sk, plan, recv, pos_g, neg_g, temperature, adversarial):
+        W, r = sk.world, sk.rank
+        B, N = plan.Bg // W, plan.N
+        f32 = dict(dtype=torch.float32, device=neg_g.device)
+        scores, out_neg = torch.empty((B, N), **f32), torch.empty(B, **f32)
+        pos_raw, out_pos = torch.empty(B, **f32), torch.empty(B, **f32)
+        rc = _lib.load().kge_shard_finish(
+            recv.data_ptr() if recv.numel() else None, plan._dev.data_ptr(), plan.hpre.data_ptr(), pos_g.data_ptr(),
+            neg_g.data_ptr(), neg_g.stride(0), plan.Bg, N, sk.nentity, W, r, float(temperature), int(adversarial),
+            scores.data_ptr(), scores.stride(0), out_neg.data_ptr(), pos_raw.data_ptr(), out_pos.data_ptr(),
+            _st(neg_g))
+        check(rc, "kge_shard_finish")
+        return out_neg, out_pos, scores
 
     @staticmethod
     def step_forward(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus, temperature, adversarial):
@@ -117,129 +383,39 @@ class HipShardKernels:
 
     @classmethod
     def train_forward(cls, sk, bufs, mode, qent, qent_pos, pos, neg, w):
-        st = torch.cuda.current_stream(sk.device).cuda_stream
         rc = _lib.load().kge_shard_train_forward(*cls._prefix(sk, bufs, mode, qent, qent_pos, pos, neg, w),
                                                  bufs["stats"].data_ptr(), bufs["dq"].data_ptr(), bufs["ws"].data_ptr(),
-                                                 bufs["ws"].numel(), st)
+                                                 bufs["ws"].numel(), _st(sk.shard))
         check(rc, "kge_shard_train_forward")
 
     @classmethod
     def train_combine(cls, sk, bufs, mode, qent, qent_pos, pos, neg, w, stats_all):
-        st = torch.cuda.current_stream(sk.device).cuda_stream
         rc = _lib.load().kge_shard_train_combine(*cls._prefix(sk, bufs, mode, qent, qent_pos, pos, neg, w),
                                                  stats_all.data_ptr(), bufs["dq"].data_ptr(),
                                                  bufs["out_neg"].data_ptr(), bufs["out_pos_raw"].data_ptr(),
                                                  bufs["out_pos"].data_ptr(), bufs["ws"].data_ptr(), bufs["ws"].numel(),
-                                                 st)
+                                                 _st(sk.shard))
         check(rc, "kge_shard_train_combine")
 
     @classmethod
     def train_backward(cls, sk, bufs, mode, qent, qent_pos, pos, neg, w, step, loss_sum):
-        st = torch.cuda.current_stream(sk.device).cuda_stream
         a = sk.adam
         rc = _lib.load().kge_shard_train_backward(
             *cls._prefix(sk, bufs, mode, qent, qent_pos, pos, neg, w), bufs["dq"].data_ptr(),
             bufs["loss"].data_ptr(), None if loss_sum is None else loss_sum.data_ptr(), a["m_ent"].data_ptr(),
             a["v_ent"].data_ptr(), a["m_rel"].data_ptr(), a["v_rel"].data_ptr(), float(a["lr"]), float(a["b1"]),
-            float(a["b2"]), float(a["eps"]), int(step), int(a["keras"]), bufs["ws"].data_ptr(), bufs["ws"].numel(), st)
+            float(a["b2"]), float(a["eps"]), int(step), int(a["keras"]), bufs["ws"].data_ptr(), bufs["ws"].numel(),
+            _st(sk.shard))
         check(rc, "kge_shard_train_backward")
         return bufs["loss"]
 
 
-class TorchComm:
-    """Collectives of the sharded step over torch.distributed (RCCL on ROCm, gloo on CPU)."""
-
-    def __init__(self, group=None):
-        self.group = group
-
-    def all_gather_cat(self, t):
-        """[W, *t.shape], rank-major."""
-        W = dist.get_world_size(self.group)
-        parts = [torch.empty_like(t) for _ in range(W)]
-        dist.all_gather(parts, t.contiguous(), group=self.group)  # any backend (RCCL, gloo), any device
-        return torch.stack(parts)
-
-    def all_reduce_sum_(self, t):
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-        return t
-
-
-class ThreadComm:
-    """The same collectives between W threads of ONE process (one Python thread per simulated rank,
-    all on one device and stream): used to run the W-rank sharded step on a single GPU. Sums are
-    taken in rank order, as RCCL's result is the same on every rank."""
-
-    def __init__(self, world):
-        import threading
-        self.world = world
-        self._barrier = threading.Barrier(world, timeout=120)  # a failed rank breaks it instead of hanging
-        self._slots = [None] * world
-
-    def _exchange(self, rank, t):
-        self._slots[rank] = t
-        self._barrier.wait()
-        got = list(self._slots)
-        self._barrier.wait()
-        return got
-
-    def all_gather_cat(self, t, rank):
-        return torch.stack(self._exchange(rank, t.contiguous()))
-
-    def all_reduce_sum_(self, t, rank):
-        parts = self._exchange(rank, t.clone())
-        acc = parts[0].clone()
-        for x in parts[1:]:
-            acc += x
-        t.copy_(acc)
-        return t
-
-
-def run_threads(fns):
-    """Runs fns[r]() on one thread per simulated rank; returns their results (re-raises the first error)."""
-    import threading
-    res, err = [None] * len(fns), []
-
-    def go(r):
-        try:
-            res[r] = fns[r]()
-        except BaseException as e:  # noqa: BLE001
-            err.append(e)
-
-    th = [threading.Thread(target=go, args=(r,)) for r in range(len(fns))]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    if err:
-        raise err[0]
-    return res
-
-
-def _reduce_scatter_rows(full, world, rank, group):
-    """SUM over ranks of `full` [W*B, C], returning this rank's [B, C] block. RCCL has a native
-    reduce-scatter; gloo (CPU tests) falls back to all-reduce + slice."""
-    B = full.shape[0] // world
-    if full.is_cuda:
-        out = torch.empty((B,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
-        dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=group)
-        return out
-    dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
-    return full[rank * B:(rank + 1) * B].contiguous()
-
-
-def _reduce_scatter_rows_into(out, full, world, rank, group):
-    """Async SUM reduce-scatter of `full` [W*b, C] into this rank's `out` [b, C] (a contiguous row
-    block). Returns the work handle (None when it completed synchronously: gloo fallback)."""
-    b = full.shape[0] // world
-    if full.is_cuda:
-        return dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=group, async_op=True)
-    dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
-    out.copy_(full[rank * b:(rank + 1) * b])
-    return None
-
-
+# ------------------------------------------------------------------------------------------------
+# the row-sharded model
+# ------------------------------------------------------------------------------------------------
 class ShardedKGE:
-    """Row-sharded owner-computes forward of supervisor.py:17-18 (both model calls).
+    """Row-sharded owner-computes forward of supervisor.py:17-18 (both model calls) and train step
+    (supervisor.py:15-26 across replicas).
 
     The shard is the slice [lo, hi) of exactly the table TFKGEModel(seed) would build, so sharded
     results can be compared with the unsharded model row for row.
@@ -258,6 +434,8 @@ class ShardedKGE:
             self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         else:
             self.world, self.rank = int(world), int(rank)
+        if isinstance(comm, ThreadComm):
+            comm = comm.view(self.rank)
         self.comm = comm if comm is not None else (TorchComm(group) if self.world > 1 else None)
         self.kernels = kernels or HipShardKernels()
         self.model_name = model_name
@@ -283,7 +461,7 @@ class ShardedKGE:
         self.temperature, self.adversarial, self.detach = 1.0, True, False
         self.adam = None
         self.step = 0
-        self.loss_sum = None
+        self.loss_sum = None  # optional 0-dim fp32 device tensor: the step adds W * sum(replica losses)
         self._bufs = {}
 
     @classmethod
@@ -291,9 +469,13 @@ class ShardedKGE:
         """A sharded view of an existing TFKGEModel / KGEModel: this rank's shard IS rows [lo, hi) of the
         model's entity table (a view: updates land in the model's own storage) and the relation table
         is the model's (updated identically on every rank). Rows outside the shard go stale during
-        training until `sync_entity_table` re-broadcasts every rank's block."""
+        training until `sync_entity_table` re-broadcasts every rank's block. With a ThreadComm (W
+        simulated ranks of one process) each rank gets its own copy of the relation table: W in-place
+        relation updates of one shared tensor would compound."""
         ent = model.entity_embedding.data
         rel = model.relation_embedding.data
+        if isinstance(comm, (ThreadComm, _ThreadCommRank)):
+            rel = rel.clone()
         modulus = float(model.modulus.reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0
         return cls(model.model_name, model.nentity, model.nrelation, model.hidden_dim, model._gamma_f,
                    device=ent.device, group=group, kernels=kernels, world=world, rank=rank, comm=comm,
@@ -308,12 +490,14 @@ class ShardedKGE:
             blk = table[lo:hi]
             if r == self.rank and blk.data_ptr() != self.shard.data_ptr():
                 blk.copy_(self.shard)
-            dist.broadcast(blk, src=r, group=self.group)
+            self.comm.broadcast_(blk, r)
         return table
 
     def configure_optimizer(self, lr=5e-5, betas=(0.9, 0.999), eps=None, semantics="keras"):
         """Adam over this rank's shard and the replicated relation table (supervisor.py:26; run.py:111
-        Keras Adam by default). Every rank applies the same relation update, so the replicas stay equal."""
+        Keras Adam by default). Every rank applies the same relation update, so the replicas stay equal.
+        The entity moments exist only for this rank's rows (Trainer keeps them as views of the
+        optimizer's full-table state, whose rows outside the shard are never advanced by this rank)."""
         if eps is None:
             eps = 1e-7 if semantics == "keras" else 1e-8
         self.adam = {"m_ent": torch.zeros_like(self.shard), "v_ent": torch.zeros_like(self.shard),
@@ -323,22 +507,95 @@ class ShardedKGE:
         self.step = 0
         return self
 
-    def _coll(self, name, t):
-        if self.world == 1:
-            return t.unsqueeze(0) if name == "gather" else t
-        if isinstance(self.comm, ThreadComm):
-            return self.comm.all_gather_cat(t, self.rank) if name == "gather" else self.comm.all_reduce_sum_(t, self.rank)
-        return self.comm.all_gather_cat(t) if name == "gather" else self.comm.all_reduce_sum_(t)
+    # ---- the exchange (§ module docstring) ----
+    def plan(self, pos_g, neg_g, mode, chunks=None):
+        """The exchange plan of a global batch (kge_shard_plan, two launches on the current stream, the
+        split sizes copied to the host asynchronously). Make it one step ahead and pass it to
+        step_forward(plan=...) so the host never waits for it."""
+        mode = ops.mode_id(mode)
+        if mode not in (HEAD_BATCH, TAIL_BATCH):
+            raise ValueError("the sharded step needs a negative mode (0 or 1)")
+        WB = neg_g.shape[0]
+        if WB % self.world:
+            raise ValueError("global batch must split evenly over ranks")
+        return self.kernels.plan(self, pos_g, neg_g, mode, default_chunks(self.world, chunks))
 
-    def assemble_queries(self, pos_g, mode):
+    def _gather_queries(self, plan, pos_g, k):
+        """Chunk k's query rows: each owner's compacted rows, all-gathered (async). Returns (block [W *
+        ncol * cap, ent_dim] viewed as rows, qidx [ncol, rows] into it, handle)."""
+        W, K, nc = self.world, plan.chunks, plan.ncol
+        _, qtot = plan.summary()
+        Rk = plan.Bg // K
+        cap = max(1, int(qtot[k].max()))
+        f32 = dict(dtype=torch.float32, device=self.device)
+        send = torch.empty((nc, cap, self.entity_dim), **f32)
+        qidx = torch.empty((nc, Rk), dtype=torch.int64, device=self.device)
+        self.kernels.gather_queries(self, plan, pos_g, k * Rk, Rk, cap, send, qidx)
+        if W == 1:
+            return send.view(-1, self.entity_dim), qidx, _Done(), send
+        block = torch.empty((W * nc * cap, self.entity_dim), **f32)
+        h = self.comm.all_gather_into(block, send, async_op=True)
+        return block, qidx, h, send
+
+    def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None, plan=None):
+        """pos_g [W*B, 3], neg_g [W*B, N] (the global batch, identical on every rank) ->
+        (out_neg [B], out_pos [B], scores [B, N]) for this rank's home rows [rank*B, (rank+1)*B).
+        Collectives: one all-gather of compacted query rows and one all-to-all of compacted owned
+        scores per chunk, every one through self.comm."""
+        if plan is None:
+            plan = self.plan(pos_g, neg_g, mode, chunks)
+        mode = plan.mode
+        W, me, K = self.world, self.rank, plan.chunks
+        Bg = plan.Bg
+        Rk, hpc = Bg // K, W // K
+        tot, _ = plan.summary()
+        k_home = me // hpc
+        # 1. every chunk's query all-gather in flight before any scoring
+        qx = [self._gather_queries(plan, pos_g, k) for k in range(K)]
+        # 2. owner-computes scores per chunk, compacted per home; 3. all-to-all to the home ranks
+        pending, recv = [], None
+        for k in range(K):
+            block, qidx, h, _ = qx[k]
+            h.wait()
+            homes = range(k * hpc, (k + 1) * hpc)
+            in_splits = [int(tot[hh, me]) if hh in homes else 0 for hh in range(W)]
+            send = torch.empty(sum(in_splits), dtype=torch.float32, device=self.device)
+            self.kernels.score_compact(self, mode, block, qidx[0], pos_g, neg_g, plan, k * Rk, Rk, send)
+            self.kernels.score_compact(self, SINGLE, block, qidx[-1], pos_g, neg_g, plan, k * Rk, Rk, send)
+            if W == 1:
+                recv = send
+                continue
+            out_splits = [int(tot[me, o]) for o in range(W)] if k == k_home else [0] * W
+            out = torch.empty(sum(out_splits), dtype=torch.float32, device=self.device)
+            if k == k_home:
+                recv = out
+            pending.append((self.comm.all_to_all(out, send, out_splits, in_splits, async_op=True), send, out))
+        for h, _, _ in pending:
+            h.wait()
+        # 4. scatter to the home rows, reductions
+        return self.kernels.shard_finish(self, plan, recv, pos_g, neg_g, temperature, adversarial)
+
+    def collective_bytes(self, plan):
+        """Bytes this rank receives per step through the forward's collectives (payload only)."""
+        tot, qtot = plan.summary()
+        W, me = self.world, self.rank
+        caps = [max(1, int(qtot[k].max())) for k in range(plan.chunks)]
+        q = sum((W - 1) * plan.ncol * c * self.entity_dim * 4 for c in caps)
+        s = sum(int(tot[me, o]) for o in range(W) if o != me) * 4
+        return {"query_rows_allgather": q, "scores_alltoall": s}
+
+    def assemble_queries(self, pos_g, mode, plan=None):
         """The query-entity rows of every global batch row: (qent [Bg, ent_dim] = E[pos[:, 2 if head
-        else 0]], qent_pos [Bg, ent_dim] = E[pos[:, 0]]): owners gather their rows, one SUM all-reduce."""
+        else 0]], qent_pos [Bg, ent_dim] = E[pos[:, 0]]): owners' compacted rows, one all-gather, then a
+        local gather into batch-row order."""
+        if plan is None:
+            plan = self.plan(pos_g, pos_g[:, :0], mode, chunks=1)
+        block, qidx, h, _ = self._gather_queries(plan, pos_g, 0)
+        h.wait()
         Bg = pos_g.shape[0]
-        cols = [2, 0] if mode == HEAD_BATCH else [0]
-        rows = torch.empty((len(cols), Bg, self.entity_dim), dtype=torch.float32, device=self.device)
-        for i, c in enumerate(cols):
-            self.kernels.gather_rows(self.shard, self.lo, pos_g[:, c:], 3, Bg, rows[i])
-        rows = self._coll("sum", rows)
+        rows = torch.empty((plan.ncol, Bg, self.entity_dim), dtype=torch.float32, device=self.device)
+        for c in range(plan.ncol):
+            self.kernels.gather_rows(block, 0, qidx[c], 1, Bg, rows[c])
         return rows[0], rows[-1]
 
     def train_step(self, pos_g, neg_g, weight_g, mode):
@@ -346,7 +603,7 @@ class ShardedKGE:
         aggregation): pos_g [Bg, 3], neg_g [Bg, N], weight_g [Bg] — the global batch (home rank h's
         replica batch is rows [h Bg/W, (h+1) Bg/W)), identical on every rank. Updates this rank's
         shard and the relation table in place; returns this rank's replica loss (0-dim tensor).
-        Collectives per step: one SUM all-reduce of the query rows, one all-gather of [Bg, 4] row
+        Collectives per step: one all-gather of the compacted query rows, one all-gather of [Bg, 4] row
         statistics, one SUM all-reduce of the [2 Bg, nq D] query gradients."""
         if self.adam is None:
             self.configure_optimizer()
@@ -362,83 +619,19 @@ class ShardedKGE:
         if key not in self._bufs:
             self._bufs = {key: k.train_alloc(self, Bg, N)}
         bufs = self._bufs[key]
-        if self.loss_sum is None:
-            self.loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
         qent, qent_pos = self.assemble_queries(pos_g, mode)
         k.train_forward(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w)
-        stats_all = self._coll("gather", bufs["stats"])
+        stats_all = self._gather_cat(bufs["stats"])
         k.train_combine(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w, stats_all)
-        self._coll("sum", bufs["dq"])
+        if self.world > 1:
+            self.comm.all_reduce_sum_(bufs["dq"])
         loss = k.train_backward(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w, self.step + 1, self.loss_sum)
         self.step += 1
         self.last_losses = loss  # every replica's loss [W] (identical on every rank)
         return loss[self.rank]
 
-    def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None):
-        """pos_g [W*B, 3], neg_g [W*B, N] (the global batch, identical on every rank) ->
-        (out_neg [B], out_pos [B], scores [B, N]) for this rank's home rows [rank*B, (rank+1)*B)."""
-        mode = ops.mode_id(mode)
-        if mode not in (HEAD_BATCH, TAIL_BATCH):
-            raise ValueError("step_forward needs a negative mode (0 or 1)")
-        WB, N = neg_g.shape
-        W = self.world
-        if WB % W:
-            raise ValueError("global batch must split evenly over ranks")
-        B = WB // W
-        K = max(1, min(int(chunks if chunks is not None else (4 if W > 1 else 1)), B))
-        while B % K:
-            K -= 1
-        Bk = B // K
-        k = self.kernels
-        dev = self.device
-        qcols = [2, 0] if mode == HEAD_BATCH else [0]
-        dist_on = W > 1
-
-        # chunk k = rows h*B + k*Bk + [0, Bk) of every home rank h, in h-major order
-        def chunk_rows(kk):
-            if K == 1:
-                return pos_g, neg_g
-            base = torch.arange(W, device=pos_g.device, dtype=torch.int64) * B + kk * Bk
-            idx = (base[:, None] + torch.arange(Bk, device=pos_g.device, dtype=torch.int64)[None, :]).reshape(-1)
-            return pos_g.index_select(0, idx), neg_g.index_select(0, idx)
-
-        # 1. query-entity rows (t for head-batch, h otherwise; plus the positives' h rows in head-batch):
-        #    owner-gathered, SUM all-reduce; every chunk's all-reduce is in flight before any scoring
-        batches, rows_k, ar = [], [], []
-        for kk in range(K):
-            pk, nk = chunk_rows(kk)
-            rows = torch.empty((len(qcols), W * Bk, self.entity_dim), dtype=torch.float32, device=dev)
-            for i, c in enumerate(qcols):
-                k.gather_rows(self.shard, self.lo, pk[:, c:], 3, W * Bk, rows[i])
-            ar.append(dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-                      if dist_on else None)
-            batches.append((pk, nk))
-            rows_k.append(rows)
-        # 2. owner-computes scores per chunk, 3. SUM reduce-scatter of the chunk to the home ranks
-        home = torch.empty((B, N + 1), dtype=torch.float32, device=dev)
-        pending = []
-        for kk in range(K):
-            if ar[kk] is not None:
-                ar[kk].wait()
-            pk, nk = batches[kk]
-            rows = rows_k[kk]
-            qe, ph = rows[0], rows[-1]
-            part = home if not dist_on else torch.empty((W * Bk, N + 1), dtype=torch.float32, device=dev)
-            k.score_sharded(self.fn, mode, qe, self.relation_embedding, self.rel_off, self.shard, self.lo, pk, nk,
-                            self.D, self.gamma, self.emb_range, self.modulus, part)
-            k.score_sharded(self.fn, SINGLE, ph, self.relation_embedding, self.rel_off, self.shard, self.lo, pk,
-                            None, self.D, self.gamma, self.emb_range, self.modulus, part[:, N:])
-            if dist_on:
-                pending.append((_reduce_scatter_rows_into(home[kk * Bk:(kk + 1) * Bk], part, W, self.rank,
-                                                          self.group), part))
-        for h, _ in pending:
-            if h is not None:
-                h.wait()
-        scores = home[:, :N].contiguous()
-        # 4. per-row reductions on the home rank
-        out_neg = k.neg_reduce(scores, temperature, adversarial)
-        out_pos = k.log_sigmoid(home[:, N].contiguous())
-        return out_neg, out_pos, scores
+    def _gather_cat(self, t):
+        return t.unsqueeze(0) if self.world == 1 else self.comm.all_gather_cat(t)
 
     def step_forward_gather(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True):
         """Same contract and results as step_forward (bitwise: the same rows reach the same kernel
@@ -461,17 +654,12 @@ class ShardedKGE:
                               dtype=torch.int64, device=U.device)
         edges = torch.searchsorted(U, bounds)
         need = (edges[1:] - edges[:-1]).to(torch.int64)  # rows this rank needs from each owner
-        if W > 1:
-            allneed = [torch.empty_like(need) for _ in range(W)]
-            dist.all_gather(allneed, need, group=self.group)
-            C = torch.stack(allneed).cpu()  # C[q, o]: rows requester q needs from owner o
-        else:
-            C = need.cpu().view(1, 1)
+        C = self._gather_cat(need).cpu()  # C[q, o]: rows requester q needs from owner o
         send_ids = C[r].tolist()                   # my requests, grouped by owner (U is owner-ordered)
         recv_ids = C[:, r].tolist()                # requests addressed to me, per requester
         if W > 1:
             req = torch.empty(sum(recv_ids), dtype=torch.int64, device=U.device)
-            dist.all_to_all_single(req, U, recv_ids, send_ids, group=self.group)
+            self.comm.all_to_all(req, U, recv_ids, send_ids)
         else:
             req = U
         rows_out = torch.empty((req.numel(), self.entity_dim), dtype=torch.float32, device=dev)
@@ -479,8 +667,8 @@ class ShardedKGE:
             self.kernels.gather_rows(self.shard, self.lo, req.to(dev), 1, req.numel(), rows_out)
         cache = torch.zeros((U.numel() + 1, self.entity_dim), dtype=torch.float32, device=dev)  # + zero row
         if W > 1:
-            dist.all_to_all_single(cache[:U.numel()], rows_out, [c * 1 for c in send_ids], recv_ids,
-                                   group=self.group)
+            self.comm.all_to_all(cache[:U.numel()].view(-1), rows_out.view(-1),
+                                 [c * self.entity_dim for c in send_ids], [c * self.entity_dim for c in recv_ids])
         else:
             cache[:U.numel()] = rows_out
         # home ids -> cache rows (out-of-range ids -> the zero row, TF-GPU gather semantics)
@@ -494,3 +682,12 @@ class ShardedKGE:
             self.fn, mode, cache, self.relation_embedding, self.rel_off, pos_l.to(dev), neg_l.to(dev), self.D,
             self.gamma, self.emb_range, self.modulus, temperature, adversarial)
         return out_neg, out_pos, scores
+
+
+def warn_dense_fallback(model, world, reason):
+    """One-time warning: a multi-replica Trainer that cannot use the row-sharded fused step all-reduces
+    the dense table gradients every step (supervisor.py:26 under tf.distribute)."""
+    nbytes = sum(p.numel() * p.element_size() for p in model.parameters() if p.requires_grad)
+    warnings.warn(f"Trainer at {world} replicas falls back to the dense-gradient path ({reason}): every step "
+                  f"all-reduces {nbytes / 1e6:.1f} MB of table gradients (the row-sharded fused step moves "
+                  f"O(batch) bytes instead)", RuntimeWarning, stacklevel=3)

@@ -37,6 +37,14 @@ class Strategy:
     def run(self, fn, args=()):
         return fn(*args)
 
+    def sum_over_replicas(self, t):
+        """The SUM of a (small) tensor over the replicas."""
+        if self._dist is None or self.num_replicas_in_sync == 1:
+            return t
+        t = t.clone()
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM)
+        return t
+
     def all_reduce_grads(self, params):
         if self._dist is None or self.num_replicas_in_sync == 1:
             return
@@ -102,11 +110,20 @@ class Trainer:
         self.one_call = fused != "split"
         self.fused = bool(fused)
         self.sharded = None
-        if self.fused and replicas > 1:
-            if fused == "split":
+        if replicas > 1:
+            from .distributed import SHARD_MAX_D, ShardedKGE, warn_dense_fallback
+            if self.fused and fused == "split":
                 raise ValueError("fused='split' is single-replica only")
-            from .distributed import ShardedKGE
-            self.sharded = ShardedKGE.from_model(model, kernels=shard_kernels)
+            D = int(getattr(model, "_D", 0))
+            if self.fused and D > SHARD_MAX_D:
+                # the row-sharded kernels keep six accumulators per element in registers (D <= 1024
+                # per half); the dense all-reduce path below has no such limit
+                self.fused = False
+                warn_dense_fallback(model, replicas, f"per-half width {D} > {SHARD_MAX_D}")
+            elif self.fused:
+                self.sharded = ShardedKGE.from_model(model, kernels=shard_kernels)
+            else:
+                warn_dense_fallback(model, replicas, "no fused step for this model / optimizer")
 
     def loss(self, positive_sample, negative_sample, subsampling_weight, mode):
         """supervisor.py:17-23 — both calls fused, then the weighted loss (one HIP launch each)."""
@@ -140,7 +157,11 @@ class Trainer:
             loss.backward()                                                    # :25
             self.strategy.all_reduce_grads(self.model.parameters())
             self.optimizer.step()                                              # :26
-            self.metrics.update_state(loss * self.strategy.num_replicas_in_sync)  # :28
+            # :28 under tf.distribute: every replica adds loss * num_replicas_in_sync to a Sum metric
+            # whose read is the cross-replica SUM, so the metric is W * (sum of the replicas' losses),
+            # as the row-sharded path records it
+            self.metrics.update_state(self.strategy.sum_over_replicas(loss.detach())
+                                      * self.strategy.num_replicas_in_sync)
             return loss
 
         return self.strategy.run(train_step_fn, next(data_iter))
@@ -180,11 +201,15 @@ class Trainer:
         st_e["step"] += 1
         st_r["step"] += 1
         # supervisor.py:28: every replica adds loss * num_replicas_in_sync to the (cross-replica SUM) metric
+        # (ShardedKGE.loss_sum stays None on this path: the metric is updated here, not inside the step)
         self.metrics.update_state(sk.last_losses.sum() * self.strategy.num_replicas_in_sync)
         return loss
 
     def sync_model(self):
-        """After sharded training: every rank's block of entity rows back into the model's table."""
+        """After sharded training: every rank's block of entity rows back into the model's table. The
+        Adam moments are NOT re-broadcast: each rank advances only its own rows of the optimizer's
+        exp_avg / exp_avg_sq (views of the shard), so a state_dict taken mid-training is current on the
+        rank's own rows only."""
         if self.sharded is not None:
             self.sharded.sync_entity_table(self.model.entity_embedding.data)
 

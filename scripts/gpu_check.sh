@@ -17,7 +17,12 @@ step() {
 }
 [[ $STEPS == *smoke* ]] && step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *test* ]] && step pytest_gpu 900 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+[[ $STEPS == *two* ]] && step shard_two_proc 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29511 scripts/shard_two_proc.py
 [[ $STEPS == *bench* ]] && step bench 600 python3 bench.py
+for wl in ${WORKLOADS:-}; do
+  step "bench_$wl" 600 python3 bench.py --workload "$wl" ${BENCH_ARGS:-}
+done
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- \

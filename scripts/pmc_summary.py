@@ -42,5 +42,12 @@ if json_out:
     with open(json_out, "w") as f:
         import hashlib
         sha = hashlib.sha256(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
-        json.dump({"source": root, "library_sha256": sha, "correction": "FETCH_SIZE kB x 1024 x 2 (gfx950, MI355X_MICROARCH.md HBM); "
+        # the sources the library was built from (bench.py pairs these counters only with that build)
+        import ctypes
+        so = ctypes.CDLL(os.path.abspath(lib))
+        for fn in (so.kge_source_hash, so.kge_build_id):
+            fn.restype = ctypes.c_char_p
+        json.dump({"source": root, "library_sha256": sha, "source_hash": so.kge_source_hash().decode(),
+                   "build_id": so.kge_build_id().decode(),
+                   "correction": "FETCH_SIZE kB x 1024 x 2 (gfx950, MI355X_MICROARCH.md HBM); "
                    "WRITE_SIZE kB x 1024", "kernels": out}, f, indent=1)

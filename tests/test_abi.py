@@ -106,3 +106,27 @@ def test_mode_codes_q1():
     assert ops.mode_id(torch.tensor(0)) == kge.HEAD_BATCH
     with pytest.raises(ValueError):
         ops.mode_id("sideways")
+
+
+def test_library_is_built_from_this_tree():
+    """Provenance: kge_source_hash() compiled into the library equals the sha256 of this tree's sources
+    (Makefile recipe restated by _lib.source_hash), so the binary the GPU runs is these sources."""
+    info = kge.build_id()
+    assert info["source_hash"] == _lib.source_hash(), "libkge_hip.so is stale: rebuild with make"
+    assert info["build_id"].endswith("src:" + info["source_hash"])
+
+
+def test_sharded_exchange_rejects_bad_arguments():
+    lib = kge.load()
+    d = ctypes.c_void_p(16)
+    # chunks must divide the world; world limit; modes
+    assert lib.kge_shard_plan(d, d, 4, 8, 4, 100, 4, 3, 0, d, d, d, d, d, None) == -22
+    assert lib.kge_shard_plan(d, d, 4, 130, 4, 1000, 65, 1, 0, d, d, d, d, d, None) == -95
+    assert lib.kge_shard_plan(d, d, 4, 8, 4, 100, 2, 1, 3, d, d, d, d, d, None) == -22
+    assert lib.kge_shard_plan(d, d, 4, 9, 4, 100, 2, 1, 1, d, d, d, d, d, None) == -22  # Bg % W
+    assert lib.kge_shard_plan(d, d, 4, 0, 4, 100, 2, 1, 1, d, d, d, d, d, None) == 0    # empty
+    # compact scoring: rows must be whole homes
+    rc = lib.kge_score_sharded_compact(1, 1, d, 8, 4, d, d, 2, 4, 0, d, 10, 4, 0, d, d, 4, 3, 4, 4, 1.0, 1.0, 0.0,
+                                       d, d, d, 2, 0, 2, 0, d, None)
+    assert rc == -22 and b"whole homes" in lib.kge_last_error()
+    assert lib.kge_shard_finish(d, d, d, d, d, 4, 8, 4, 100, 2, 2, 1.0, 1, d, 4, d, d, d, None) == -22

@@ -73,20 +73,48 @@ def test_c3_c4_positives_from_reference_splits():
 
 
 def test_pmc_traffic_is_tied_to_the_library_build(tmp_path, monkeypatch):
-    """roofline.traffic comes from the committed PMC summary only while the loaded libkge_hip.so is the build
-    the passes ran (sha256 recorded by scripts/pmc_summary.py); any other build reports it stale."""
+    """roofline.traffic comes from the committed PMC summary only while the loaded libkge_hip.so is built from
+    the sources the passes ran (kge_source_hash, recorded by scripts/pmc_summary.py); any other build reports it
+    stale."""
     prof = tmp_path / "profiles"
     prof.mkdir()
     rows = [{"kernel": "step_fwd_xcd_kernel<4, true, 4, 4>", "hbm_read_bytes_corrected": 800.0, "hbm_write_bytes": 2.0},
             {"kernel": "step_fwd_xcd_kernel<4, false, 4, 4>", "hbm_read_bytes_corrected": 900.0, "hbm_write_bytes": 2.0},
             {"kernel": "neg_rows_kernel", "hbm_read_bytes_corrected": 10.0, "hbm_write_bytes": 1.0}]
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
-    monkeypatch.setattr(bench, "library_sha256", lambda: "abc")
-    (prof / "pmc_c2.json").write_text(json.dumps({"library_sha256": "abc", "kernels": rows}))
+    monkeypatch.setattr(bench, "loaded_source_hash", lambda: "abc")
+    (prof / "pmc_c2.json").write_text(json.dumps({"source_hash": "abc", "kernels": rows}))
     t, src = bench.pmc_traffic("c2", ["step_fwd_xcd_kernel", "neg_rows_kernel"])
     assert t == (802.0 + 902.0) / 2 + 11.0 and src.endswith("pmc_c2.json")
-    (prof / "pmc_c2.json").write_text(json.dumps({"library_sha256": "other", "kernels": rows}))
+    (prof / "pmc_c2.json").write_text(json.dumps({"source_hash": "other", "kernels": rows}))
     t, src = bench.pmc_traffic("c2", ["step_fwd_xcd_kernel"])
     assert t is None and src.startswith("stale")
     t, src = bench.pmc_traffic("c9", ["step_fwd_xcd_kernel"])
     assert t is None
+
+
+def test_main_gives_ranks_disjoint_positives():
+    """main() builds each rank's batches with its world size (make_inputs(..., world=world)), so at world 2
+    the two ranks' first batches hold disjoint slices of the permuted WN18RR train triples."""
+    import inspect
+    src = inspect.getsource(bench.main)
+    assert "make_inputs(w, rank, device, world=world)" in src
+    w = bench.WORKLOADS["c2"]
+    (a0, _), = bench.rank_batches(w, 0, 1, world=2)[0]
+    (b0, _), = bench.rank_batches(w, 1, 1, world=2)[0]
+    tri = bench.load_triples(w)
+    perm = np.random.RandomState(0).permutation(len(tri))
+    assert np.array_equal(a0, tri[perm[0:512]]) and np.array_equal(b0, tri[perm[512:1024]])
+    ia = set(perm[0:512].tolist())
+    assert not ia & set(perm[512:1024].tolist())
+
+
+def test_cpu_baseline_runs_on_the_gpu_lines_inputs():
+    """The CPU baseline's sample is the first rows of the timed batch 0 (rank 0): WN18RR train triples and
+    the RandomState(2) negatives, not separate random ids."""
+    w = bench.WORKLOADS["c2"]
+    pos, neg, src = bench.cpu_baseline_inputs(w, 64)
+    (p0, n0), = bench.rank_batches(w, 0, 1)[0]
+    assert np.array_equal(pos.numpy(), p0[:64]) and np.array_equal(neg.numpy(), n0[:64])
+    assert "wn18rr_ids.npz" in src
+    assert np.array_equal(n0, np.random.RandomState(2).randint(w["nentity"], size=(512, 256)))

@@ -243,3 +243,15 @@ def test_trainer_multi_replica_row_sharded_gloo():
     for r in range(2):
         eerr, rerr, merr = results[r]
         assert eerr < 1e-3 and rerr < 1e-3 and merr < 1e-5, (r, results[r])
+
+
+@pytest.mark.parametrize("world,chunks", [(4, 2), (3, 3), (4, 1)])
+def test_sharded_owner_computes_more_ranks_gloo(world, chunks):
+    """World 3 and 4 over gloo: chunks of several whole homes (world 4, 2 chunks), one home per chunk, and
+    one chunk for all; the all-gather / all-to-all splits come from the plan, with no padding of scores."""
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), "TransE", results, chunks, 2), nprocs=world, join=True)
+    assert len(results) == world
+    for r in range(world):
+        assert results[r] < 1e-5, (r, results[r])

@@ -317,10 +317,14 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
     tables = (ent, rel, full._gamma_f, full._range_f, 0.0)
     fn = FN_IDS["DistMult"]
 
-    def timed(f, n=reps):
+    def timed(f, n=reps, queue=True):
+        """Device time of f() per call: the launches are queued behind a sleep kernel, so the events bracket
+        back-to-back GPU work and not the host's launch rate (ctypes launches cost ~10 us each here)."""
         f()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if queue:
+            torch.cuda._sleep(50_000_000)
         e0.record()
         for _ in range(n):
             f()
@@ -329,48 +333,53 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
         return e0.elapsed_time(e1) / n * 1e3  # us
 
     unsharded_us = timed(lambda: ops.score_indexed_raw(fn, 0, ent, rel, 0, pos, neg, d, full._gamma_f, full._range_f))
+    step_us = timed(lambda: ops.step_forward_raw(fn, 0, ent, rel, 0, pos, neg, d, full._gamma_f, full._range_f))
     comm = ThreadComm(world)
     ranks = [ShardedKGE("DistMult", E, w["nrelation"], d, w["gamma"], device=device, world=world, rank=r, comm=comm,
                         full_tables=tables) for r in range(world)]
     t0 = time.perf_counter()
-    sim_dev_us = timed(lambda: run_threads([lambda sk=sk: sk.step_forward(pos, neg, 0) for sk in ranks]), 3)
+    sim_dev_us = timed(lambda: run_threads([lambda sk=sk: sk.step_forward(pos, neg, 0) for sk in ranks]), 3, False)
     sim_wall_us = (time.perf_counter() - t0) / 4 * 1e6
     # rank 0 alone: the kernels of one step, with the other ranks' contributions prepared untimed
     HK = HipShardKernels
     r0 = ranks[0]
     plan = r0.plan(pos, neg, 0)
     tot, qtot = plan.summary()
-    K, nc = plan.chunks, plan.ncol
+    K = plan.chunks
     Rk, hpc = Bg // K, world // K
-    caps = [max(1, int(qtot[k].max())) for k in range(K)]
     blocks, qidxs, sends = [], [], []
     for k in range(K):
-        blk = torch.empty((world, nc, caps[k], r0.entity_dim), dtype=torch.float32, device=device)
-        qidx = torch.empty((nc, Rk), dtype=torch.int64, device=device)
-        for sk in ranks:  # every owner's compacted rows: the all-gather's result
-            HK.gather_queries(sk, plan, pos, k * Rk, Rk, caps[k], blk[sk.rank], qidx)
-        blocks.append(blk.view(-1, r0.entity_dim))
+        per = [int(qtot[k, :, o].sum()) for o in range(world)]
+        parts = []
+        for sk in ranks:  # every owner's compacted rows: the query all-to-all's output
+            snd = torch.empty((world, per[sk.rank], r0.entity_dim), dtype=torch.float32, device=device)
+            qidx = torch.empty((plan.ncol, Rk), dtype=torch.int64, device=device)
+            HK.gather_queries(sk, plan, pos, k, snd, qidx)
+            parts.append(snd[0])
+        blocks.append(torch.cat(parts))
         qidxs.append(qidx)
         sends.append(torch.empty(int(sum(tot[h, 0] for h in range(k * hpc, (k + 1) * hpc))), dtype=torch.float32,
                                  device=device))
-    # home 0's all-to-all output: every owner's block of home 0's rows, in rank order
+    # home 0's score all-to-all output: every owner's block of home 0's rows, in rank order
     recv = []
     for sk in ranks:
         snd = torch.empty(int(sum(tot[h, sk.rank] for h in range(hpc))), dtype=torch.float32, device=device)
         HK.score_compact(sk, 0, blocks[0], qidxs[0][0], pos, neg, plan, 0, Rk, snd)
-        HK.score_compact(sk, 3, blocks[0], qidxs[0][-1], pos, neg, plan, 0, Rk, snd)
+        HK.score_compact(sk, 1, blocks[0], qidxs[0][-1], pos, neg, plan, 0, Rk, snd)
         recv.append(snd[:int(tot[0, sk.rank])])
     recv = torch.cat(recv)
-    q_send = torch.empty((nc, max(caps), r0.entity_dim), dtype=torch.float32, device=device)
+    q_sends = [torch.empty((world, int(qtot[k, :, 0].sum()), r0.entity_dim), dtype=torch.float32, device=device)
+               for k in range(K)]
+    q_idx_scratch = torch.empty_like(qidxs[0])
 
     def rank0_gather():
         for k in range(K):
-            HK.gather_queries(r0, plan, pos, k * Rk, Rk, caps[k], q_send, qidxs[k])
+            HK.gather_queries(r0, plan, pos, k, q_sends[k], q_idx_scratch)
 
     def rank0_score():
         for k in range(K):
             HK.score_compact(r0, 0, blocks[k], qidxs[k][0], pos, neg, plan, k * Rk, Rk, sends[k])
-            HK.score_compact(r0, 3, blocks[k], qidxs[k][-1], pos, neg, plan, k * Rk, Rk, sends[k])
+            HK.score_compact(r0, 1, blocks[k], qidxs[k][-1], pos, neg, plan, k * Rk, Rk, sends[k])
 
     t_plan = timed(lambda: HK.plan(r0, pos, neg, 0, K))
     t_gather = timed(rank0_gather)
@@ -378,7 +387,8 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
     t_finish = timed(lambda: HK.shard_finish(r0, plan, recv, pos, neg, 1.0, True))
     rank_us = t_plan + t_gather + t_score + t_finish
     cb = r0.collective_bytes(plan)
-    coll = cb["query_rows_allgather"] + cb["scores_alltoall"]
+    coll = cb["query_rows"] + cb["scores"]
+    B_ = Bg // world
     out = {"workload": f"C4 YAGO3-10 DistMult d=500 N=1024, global batch {world} x 512 (YAGO3-10 positives), "
                        f"entity table split over {world} simulated ranks",
            "step_us_all_ranks_one_gpu": sim_dev_us,
@@ -386,16 +396,18 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
            "rank_step_kernels_us": {"plan": t_plan, "query_gather": t_gather, "compact_scoring": t_score,
                                     "finish": t_finish, "total": rank_us},
            "unsharded_global_kernel_us": unsharded_us,
+           "unsharded_global_step_us": step_us,
            "rank_scoring_over_unsharded": t_score / unsharded_us,
            "collective_bytes_per_rank_step": cb,
-           "zero_padded_round2_bytes_per_rank_step": {"query_rows_allreduce": 2 * (world - 1) * Bg * d * 4 * nc // world,
-                                                       "scores_reduce_scatter": (world - 1) * B * (N + 1) * 4},
+           "zero_padded_round2_bytes_per_rank_step": {"query_rows_allreduce_ring": 2 * (world - 1) * Bg * d * 4 * 2 // world,
+                                                       "scores_reduce_scatter": (world - 1) * B_ * (N + 1) * 4},
            "chunks": K,
-           "what": "step_us_all_ranks_one_gpu: the whole 8-rank ShardedKGE.step_forward run by 8 threads on this "
-                   "GPU (every rank's kernels serialised, ThreadComm device copies for RCCL); rank_step_kernels_us: "
-                   "rank 0's kernels of one step alone (its per-GPU compute in an 8-GPU step)"}
+           "what": "rank_step_kernels_us: rank 0's kernels of one 8-rank step, device time (queued behind a sleep "
+                   "kernel): its per-GPU compute in an 8-GPU step; step_us_all_ranks_one_gpu: the whole 8-rank "
+                   "ShardedKGE.step_forward by 8 threads on this GPU (every rank's kernels serialised, ThreadComm "
+                   "device copies standing in for RCCL, host-bound)"}
     if v1:
-        t6 = world * B * (N + 1) / (6.0 * v1) * 1e6  # us per step at 6x the 1-GPU throughput
+        t6 = world * B_ * (N + 1) / (6.0 * v1) * 1e6  # us per step at 6x the 1-GPU throughput
         out["six_x_target"] = {"one_gpu_triples_per_s": v1, "step_budget_us": t6,
                                "collective_budget_us_without_overlap": t6 - rank_us,
                                "rccl_gbps_needed_without_overlap": (coll / ((t6 - rank_us) * 1e-6) / 1e9
@@ -413,10 +425,8 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
     t_bwd = timed(lambda: HK.train_backward(sk, bufs, 0, qent, qpos, pos, neg, wt, 3, None))
     out["rank_train_step_kernels_us"] = {"forward": t_fwd, "combine": t_comb, "backward": t_bwd,
                                          "total": t_fwd + t_comb + t_bwd}
-    tplan = sk.plan(pos, pos[:, :0], 0, chunks=1)  # the train step's query plan (one chunk)
-    cap1 = max(1, int(tplan.summary()[1][0].max()))
     out["train_collective_bytes_per_rank_step"] = {
-        "query_rows_allgather": (world - 1) * nc * cap1 * d * 4,
+        "query_rows_alltoall": (world - 1) * 2 * Bg // world * d * 4,
         "stats_allgather": (world - 1) * Bg * 16, "query_grad_allreduce_ring": 2 * (world - 1) * 2 * Bg * d * 4 // world}
     return out
 
@@ -977,8 +987,8 @@ def main(argv=None):
             "triples_per_s": (ws["B"] * ws["N"] + ws["B"]) * world * sa.steps / el,
             "ms_per_step": el / sa.steps * 1e3, "steps": sa.steps,
             "what": "distributed.ShardedKGE.step_forward: entity table row-sharded over the ranks, owner-computes "
-                    "scoring (owned candidates compacted), chunk-pipelined RCCL all-reduce (queries) + "
-                    "reduce-scatter (scores)"}
+                    "scoring; per chunk one RCCL all-to-all of the owners' compacted query rows and one of the "
+                    "owned scores (exchange plan made a step ahead); at 1 rank the unsharded fused forward"}
         el = sharded_bench(ws, sa, world, rank, device, dist, train=True)
         if dist:
             t = torch.tensor([el], device=device, dtype=torch.float64)
@@ -990,8 +1000,8 @@ def main(argv=None):
             "ms_per_step": el / sa.steps * 1e3, "steps": sa.steps,
             "what": "distributed.ShardedKGE.train_step: supervisor.py:15-26 over the replicas' batches (SUM "
                     "gradients, Keras Adam) with the entity table row-sharded: owned candidates only, one gather "
-                    "per candidate row, RCCL all-reduce of query rows, all-gather of [Bg,4] row stats, all-reduce "
-                    "of query gradients; Adam on the shard"}
+                    "per candidate row, RCCL all-to-all of the owners' query rows, all-gather of [Bg,4] row stats, "
+                    "all-reduce of query gradients; Adam on the shard"}
         if world == 1:
             line["yago3_10_shard_sim8"] = shard_sim_bench(device, v1=line["yago3_10_rowshard"]["triples_per_s"])
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -61,19 +61,19 @@ SIGNATURES = {
     "kge_build_id": (ctypes.c_char_p, []),
     "kge_source_hash": (ctypes.c_char_p, []),
     "kge_shard_plan": (
-        _c_i, [_c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+        _c_i, [_c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "kge_shard_gather_queries": (
-        _c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_p,
-               _c_i64, _c_p, _c_p, _c_p]),
+        _c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i, _c_i, _c_i64, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p,
+               _c_p, _c_p, _c_p, _c_p]),
     "kge_score_sharded_compact": (
         _c_i,
-        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64,
+        [_c_i, _c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64,
          _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i64,
          _c_i64, _c_p, _c_p],
     ),
     "kge_shard_finish": (
-        _c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_f, _c_i, _c_p, _c_i64,
-               _c_p, _c_p, _c_p, _c_p]),
+        _c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_f, _c_i, _c_p,
+               _c_i64, _c_p, _c_p, _c_p, _c_p]),
     "kge_eval_query": (
         _c_i, [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
     "kge_gemm_nt": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p]),

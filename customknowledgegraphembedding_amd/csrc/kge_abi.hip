@@ -467,7 +467,7 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
     } else if (kind == KIND_STEP_FWD_XCD || kind == KIND_SCORE_SHARD_XCD) {
         waves = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock * 8;  // 8 slice blocks per 4 rows
-    } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS) {
+    } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS || kind == KIND_SHARD_POS_HEAD) {
         waves = p.B;  // one wave per slot
     } else if (kind == KIND_STEP_EPILOGUE) {
         // one wave per slot (negative rows' chains, positives, negative rows' score gradients), then the
@@ -724,25 +724,29 @@ int kge_score_sharded(int fn, int mode, const float* qent, int64_t q_ld, const f
     return run_score(fn, mode, p, KIND_FWD, stream);
 }
 
-int kge_score_sharded_compact(int fn, int mode, const float* qent, int64_t q_rows, int64_t q_ld, const int64_t* q_idx,
-                              const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off, const float* shard,
-                              int64_t shard_rows, int64_t shard_ld, int64_t shard_lo, const int64_t* pos,
-                              const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma,
-                              float emb_range, float modulus, const int* pre, const int* cnt, const int* tot,
-                              int world, int rank, int64_t home_B, int64_t home0, float* send, void* stream) {
-    int rc = check_fn_mode(fn, mode);
+int kge_score_sharded_compact(int fn, int mode, int positives, const float* qent, int64_t q_rows, int64_t q_ld,
+                              const int64_t* q_idx, const float* rel, int64_t nrelation, int64_t rel_ld,
+                              int64_t rel_off, const float* shard, int64_t shard_rows, int64_t shard_ld,
+                              int64_t shard_lo, const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t B,
+                              int64_t N, int64_t D, float gamma, float emb_range, float modulus, const int* pre,
+                              const int* cnt, const int* tot, int world, int rank, int64_t home_B, int64_t home0,
+                              float* send, void* stream) {
+    if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH)
+        return fail(KGE_EINVAL, "kge_score_sharded_compact: mode must be 0 (head-batch) or 1 (tail-batch)");
+    const int smode = positives ? KGE_SINGLE : mode;
+    int rc = check_fn_mode(fn, smode);
     if (rc) return rc;
     if (B < 0 || N < 0 || D <= 0 || shard_rows < 0 || q_rows < 0) return fail(KGE_EINVAL, "bad shape");
     if (world < 1 || rank < 0 || rank >= world || home_B <= 0 || B % home_B || home0 < 0 ||
         home0 + B / home_B > world)
         return fail(KGE_EINVAL, "kge_score_sharded_compact: rows must be whole homes of home_B rows");
-    if (empty(B, mode == KGE_SINGLE ? 1 : N)) return ok();
-    if (!pos || (mode != KGE_SINGLE && !neg) || !send || !qent || !q_idx || !shard || !pre || !cnt || !tot)
+    if (empty(B, positives ? 1 : N)) return ok();
+    if (!pos || (!positives && !neg) || !send || !qent || !q_idx || !shard || !pre || !cnt || !tot)
         return fail(KGE_EINVAL, "null pointer");
     ScoreParams p;
-    fill_indexed(p, fn, mode, shard, shard_rows, shard_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
+    fill_indexed(p, fn, smode, shard, shard_rows, shard_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
                  D, gamma, emb_range, modulus);
-    // query entity rows: row q_idx[b] of the all-gathered query block
+    // query entity rows: row q_idx[b] of the exchanged query block
     p.qent = qent;
     p.q_idx = q_idx;
     p.q_stride = 1;
@@ -750,20 +754,22 @@ int kge_score_sharded_compact(int fn, int mode, const float* qent, int64_t q_row
     p.q_rows = q_rows;
     p.c_base = shard_lo;
     p.skip_foreign = 1;
+    p.pos_base = pos;
     p.cmp_pre = pre;
     p.cmp_cnt = cnt;
     p.cmp_tot = tot;
     p.cmp_home0 = home0;
-    p.cmp_last = mode == KGE_SINGLE;
+    p.cmp_last = positives != 0;
     p.home_B = home_B;
     p.world = world;
     p.rank = rank;
     p.out = send;
     p.out_ld = 0;
-    if (mode != KGE_SINGLE && shard_lo >= 0 && shard_lo + shard_rows < ((int64_t)1 << 31) &&
-        use_xcd_order(shard_rows, N))
+    if (positives && mode == KGE_HEAD_BATCH)  // the head's owner: query from its shard, the tail from the block
+        return run_score(fn, KGE_SINGLE, p, KIND_SHARD_POS_HEAD, stream);
+    if (!positives && shard_lo >= 0 && shard_lo + shard_rows < ((int64_t)1 << 31) && use_xcd_order(shard_rows, N))
         return run_score(fn, mode, p, KIND_SCORE_SHARD_XCD, stream);
-    return run_score(fn, mode, p, KIND_FWD, stream);
+    return run_score(fn, smode, p, KIND_FWD, stream);
 }
 
 int kge_gather_rows(const float* table, int64_t rows, int64_t ld, int64_t lo, const int64_t* ids, int64_t id_stride,

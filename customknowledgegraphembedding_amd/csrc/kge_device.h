@@ -837,6 +837,29 @@ score_sharded_xcd_kernel(ScoreParams p) {
     }
 }
 
+// The row-sharded forward's positives in head-batch mode (kge_score_sharded_compact, positives = 1): the
+// exchanged query block holds the negatives' query entity, the TAIL, so the owner of the HEAD scores the
+// positive: query (h, r) built from its shard row, candidate t read from the block (q_idx[b]), the
+// single-mode (tail) formula as every positive (bitwise step_fwd_xcd_kernel's). One wave per batch row; the
+// score takes the last slot of the row's compact run.
+template <int FN, int V, int G>
+__global__ __launch_bounds__(kBlock) void shard_pos_head_kernel(ScoreParams p) {
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t h = p.pos_base[b * 3] - p.c_base, rj = p.pos_base[b * 3 + 1];
+    if (h < 0 || h >= p.c_rows) return;  // another rank's head (wave-uniform)
+    const bool rok = rj >= 0 && rj < p.r_rows;
+    Query<FN, false, V, G> q;
+    q.build(p.cent + h * p.c_ld, true, p.rel + (rok ? rj : 0) * p.r_ld + p.r_off, rok, p.D, lane, p);
+    const int64_t ti = p.q_idx[b];
+    const bool tok = ti >= 0 && ti < p.q_rows;
+    Cand<FN, V, G> c;
+    c.load(p.qent + (tok ? ti : 0) * p.q_ld, tok, p.D, lane);
+    const float s = cand_score<FN, false, V, G>(c, q, p);
+    if (lane == 0) p.out[cmp_row_off(p, b) + p.cmp_cnt[b] - 1] = s;
+}
+
 template <int FN, bool CH, int V, int G, bool ST = false>
 __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
     WaveTask t;
@@ -2668,6 +2691,9 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         hipLaunchKernelGGL((step_fwd_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_SCORE_SHARD_XCD)
         hipLaunchKernelGGL((score_sharded_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_SHARD_POS_HEAD) {
+        if constexpr (!CH) hipLaunchKernelGGL((shard_pos_head_kernel<FN, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    }
     else if (kind == KIND_STEP_FWD_GRAD) {
         if constexpr (FN != KGE_PROTATE && G <= kFwdGradMaxG) {
             if (!p.adversarial)

@@ -5,15 +5,15 @@
 // on every rank, so every rank can compute, from the ids alone, who owns which query row and which
 // candidate, and in which order each owner will send them. Nothing but payload crosses xGMI:
 //   * query rows: owner o gathers the chunk's query-entity rows it owns, compacted in row order
-//     (kge_shard_gather_queries), one all-gather of [ncol, cap] rows per rank; a row's place in the
-//     gathered block is implicit (owner, rank among that owner's rows of the chunk);
+//     (kge_shard_gather_queries), and every rank receives every owner's rows (an all-to-all whose pieces
+//     are the same block, sized exactly: no padding); a row's place in the received block is implicit
+//     (owner, rank among that owner's rows of the chunk);
 //   * scores: owner o writes only the scores of the candidates it owns, compacted per row in column
 //     order with the row's positive last (kge_score_sharded_compact), and sends home h exactly the
 //     scores of h's rows (all-to-all, no indices); home h scatters them back with the same ranks
 //     (kge_shard_finish) and reduces its rows.
 // kge_shard_plan computes the ownership counts and ranks once per global batch (two launches, O(Bg N)
-// integer work on device); its small summary (the all-to-all split sizes and the query caps) is the
-// only thing the host reads.
+// integer work on device); its small summary (the all-to-all split sizes) is the only thing the host reads.
 #include <string>
 
 #include "kge_device.h"
@@ -49,11 +49,12 @@ Owners make_owners(int64_t E, int W) {
     return o;
 }
 
-// candidate n of global row g (n < N: negative, n == N: the positive's tail), -1 past the row
+// candidate n of global row g (n < N: negative, n == N: the positive, owned by the owner of pos[g, pcol]),
+// -1 past the row
 __device__ __forceinline__ int64_t cand_id(const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t N,
-                                           int64_t g, int64_t n) {
+                                           int64_t g, int64_t n, int pcol) {
     if (n < N) return neg[g * neg_ld + n];
-    if (n == N) return pos[g * 3 + 2];
+    if (n == N) return pos[g * 3 + pcol];
     return -1;
 }
 
@@ -68,17 +69,18 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 }
 
 // Plan pass 1, one wave per global row g: cnt[o * Bg + g] = candidates of row g (N negatives + the
-// positive tail) owned by rank o; qown[c * Bg + g] = owner of the row's query entity of column c.
+// positive) owned by rank o; qown[c * Bg + g] = owner of the row's query entity of column c.
 __global__ __launch_bounds__(kBlock) void plan_count_kernel(const int64_t* __restrict__ pos,
                                                             const int64_t* __restrict__ neg, int64_t neg_ld,
                                                             int64_t Bg, int64_t N, Owners own, int ncol, int qc0,
-                                                            int qc1, int* __restrict__ cnt, int* __restrict__ qown) {
+                                                            int qc1, int pcol, int* __restrict__ cnt,
+                                                            int* __restrict__ qown) {
     const int64_t g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (g >= Bg) return;
     const int lane = threadIdx.x & 63;
     int acc = 0;  // lane o: candidates owned by rank o
     for (int64_t c0 = 0; c0 <= N; c0 += kWave) {
-        const int o = own.of(cand_id(pos, neg, neg_ld, N, g, c0 + lane));
+        const int o = own.of(cand_id(pos, neg, neg_ld, N, g, c0 + lane, pcol));
         for (int k = 0; k < own.W; ++k) {
             const int c = __popcll(__ballot(o == k));
             if (lane == k) acc += c;
@@ -171,14 +173,18 @@ __global__ __launch_bounds__(kBlock) void plan_scan_kernel(const int* __restrict
     }
 }
 
-// Sender side of the query all-gather, one wave per (column c, chunk row i): qidx[c * rows + i] = row
-// of the gathered block [W, ncol, cap] that will hold the row's query entity ((owner * ncol + c) * cap +
-// slot, -1 without an owner); the owner copies its shard row into send[c, slot].
+// Sender side of the query exchange, one wave per (column c, chunk row i). Owner o's rows of chunk k go
+// to every rank (an all-to-all whose W pieces are the same block: NCCL has no all-gather of unequal
+// sizes): piece = [column 0 rows | column 1 rows] in slot order, per = sum_c qtot[k, c, me] rows, written W
+// times into send [W, per, width]. The all-to-all output holds the owners' pieces in rank order, so the row
+// holding (owner o, column c, slot) is roff[o] + (c ? qtot[k, 0, o] : 0) + slot, roff[o] = sum over o' < o
+// of the pieces: qidx[c * rows + i] (-1 without an owner).
 __global__ __launch_bounds__(kBlock) void gather_queries_kernel(const float* __restrict__ shard, int64_t shard_rows,
                                                                 int64_t ld, int64_t lo, const int64_t* __restrict__ pos,
                                                                 int64_t Bg, int64_t row0, int64_t rows, int ncol,
                                                                 int qc0, int qc1, const int* __restrict__ qown,
-                                                                const int* __restrict__ qslot, int rank, int64_t cap,
+                                                                const int* __restrict__ qslot,
+                                                                const int* __restrict__ qtot, int W, int rank,
                                                                 int64_t width, float* __restrict__ send,
                                                                 int64_t* __restrict__ qidx, int vec4) {
     const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
@@ -188,18 +194,35 @@ __global__ __launch_bounds__(kBlock) void gather_queries_kernel(const float* __r
     const int64_t i = t - (int64_t)c * rows, g = row0 + i;
     const int o = qown[(int64_t)c * Bg + g];
     const int64_t s = qslot[(int64_t)c * Bg + g];
-    if (lane == 0) qidx[t] = o >= 0 ? ((int64_t)o * ncol + c) * cap + s : -1;
+    // lane l < W: rank l's piece size; exclusive prefix = where its piece starts
+    int piece = 0, col0 = 0;
+    if (lane < W) {
+        col0 = qtot[lane];
+        piece = col0 + (ncol > 1 ? qtot[W + lane] : 0);
+    }
+    const int roff = wave_incl_scan(piece, lane) - piece;
+    if (o < 0) {
+        if (lane == 0) qidx[t] = -1;
+        return;
+    }
+    const int64_t inner = (c ? __builtin_amdgcn_readlane(col0, o) : 0) + s;
+    if (lane == 0) qidx[t] = __builtin_amdgcn_readlane(roff, o) + inner;
     if (o != rank) return;
+    const int64_t per = __builtin_amdgcn_readlane(piece, rank);
     const int64_t r = pos[g * 3 + (c == 0 ? qc0 : qc1)] - lo;
     const bool ok = r >= 0 && r < shard_rows;  // o == rank implies it
     const float* src = shard + (ok ? r : 0) * ld;
-    float* dst = send + ((int64_t)c * cap + s) * width;
     if (vec4) {
         const rsrc_t rs = make_rsrc(src, ok ? (uint32_t)(width * 4) : 0u);
-        for (int64_t e = (int64_t)lane * 4; e < width; e += 4 * kWave)
-            *reinterpret_cast<vecf<4>*>(dst + e) = bload<4>(rs, (uint32_t)(e * 4));
+        for (int64_t e = (int64_t)lane * 4; e < width; e += 4 * kWave) {
+            const vecf<4> v = bload<4>(rs, (uint32_t)(e * 4));
+            for (int d = 0; d < W; ++d) *reinterpret_cast<vecf<4>*>(send + (d * per + inner) * width + e) = v;
+        }
     } else {
-        for (int64_t e = lane; e < width; e += kWave) dst[e] = ok ? src[e] : 0.f;
+        for (int64_t e = lane; e < width; e += kWave) {
+            const float v = ok ? src[e] : 0.f;
+            for (int d = 0; d < W; ++d) send[(d * per + inner) * width + e] = v;
+        }
     }
 }
 
@@ -214,7 +237,8 @@ __global__ __launch_bounds__(kBlock) void shard_finish_kernel(const float* __res
                                                               const int64_t* __restrict__ pos,
                                                               const int64_t* __restrict__ neg, int64_t neg_ld,
                                                               int64_t Bg, int64_t B, int64_t N, Owners own, int h,
-                                                              float T, int adversarial, float* __restrict__ scores,
+                                                              int pcol, float T, int adversarial,
+                                                              float* __restrict__ scores,
                                                               int64_t ns_ld, float* __restrict__ out_neg,
                                                               float* __restrict__ pos_raw, float* __restrict__ pos_ls) {
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
@@ -229,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void shard_finish_kernel(const float* __res
     int k = 0;
     for (int64_t c0 = 0; c0 <= N; c0 += kWave, ++k) {
         const int64_t n = c0 + lane;
-        const int o = own.of(cand_id(pos, neg, neg_ld, N, g, n));
+        const int o = own.of(cand_id(pos, neg, neg_ld, N, g, n, pcol));
         int idx = -1;
         for (int q = 0; q < W; ++q) {
             const uint64_t m = __ballot(o == q);
@@ -281,14 +305,17 @@ int check_world(int64_t Bg, int world, int64_t nentity) {
     return 0;
 }
 
-int query_cols(int mode, int& qc0, int& qc1) {
-    if (mode == KGE_HEAD_BATCH) {  // negatives' query: the tail; the positive's: the head
-        qc0 = 2;
-        qc1 = 0;
-        return 2;
-    }
-    qc0 = qc1 = 0;
-    return 1;
+// The exchanged query columns and the column whose owner scores the positive. The forward (flags 0)
+// exchanges only the negative call's query entity (head-batch: the tail, else the head); its positive is
+// scored by the owner of the head in head-batch mode (query (h, r) from its shard, the tail row from the
+// exchanged block), by the owner of the tail otherwise. KGE_SHARD_TWO_COLUMNS (the sharded train step)
+// also exchanges the positive's query entity (the head) and leaves the positive with the tail's owner.
+int query_cols(int mode, int flags, int& qc0, int& qc1, int& pcol) {
+    const bool head = mode == KGE_HEAD_BATCH;
+    qc0 = head ? 2 : 0;
+    qc1 = 0;
+    pcol = (head && !(flags & KGE_SHARD_TWO_COLUMNS)) ? 0 : 2;
+    return (head && (flags & KGE_SHARD_TWO_COLUMNS)) ? 2 : 1;
 }
 
 }  // namespace
@@ -299,8 +326,8 @@ using namespace kge_impl;
 extern "C" {
 
 int kge_shard_plan(const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t Bg, int64_t N, int64_t nentity,
-                   int world, int chunks, int mode, int* cnt, int* hpre, int* qown, int* qslot, int* summary,
-                   void* stream) {
+                   int world, int chunks, int mode, int flags, int* cnt, int* hpre, int* qown, int* qslot,
+                   int* summary, void* stream) {
     int rc = check_world(Bg, world, nentity);
     if (rc) return rc;
     if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH)
@@ -309,12 +336,12 @@ int kge_shard_plan(const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64
     if (Bg == 0) return set_error(0, "");
     if (!pos || (N > 0 && !neg) || !cnt || !hpre || !qown || !qslot || !summary)
         return set_error(KGE_EINVAL, "kge_shard_plan: null pointer");
-    int qc0, qc1;
-    const int ncol = query_cols(mode, qc0, qc1);
+    int qc0, qc1, pcol;
+    const int ncol = query_cols(mode, flags, qc0, qc1, pcol);
     const Owners own = make_owners(nentity, world);
     const hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)((Bg + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
-                       st, pos, neg, neg_ld, Bg, N, own, ncol, qc0, qc1, cnt, qown);
+                       st, pos, neg, neg_ld, Bg, N, own, ncol, qc0, qc1, pcol, cnt, qown);
     rc = launched("kge_shard_plan counts");
     if (rc) return rc;
     const int64_t home_B = Bg / world, chunk_rows = Bg / chunks;
@@ -324,53 +351,59 @@ int kge_shard_plan(const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64
 }
 
 int kge_shard_gather_queries(const float* shard, int64_t shard_rows, int64_t ld, int64_t shard_lo,
-                             const int64_t* pos, int64_t Bg, int64_t row0, int64_t rows, int64_t width, int world,
-                             int rank, int mode, const int* qown, const int* qslot, int64_t cap, float* send,
-                             int64_t* qidx, void* stream) {
+                             const int64_t* pos, int64_t Bg, int chunks, int chunk, int64_t width, int world,
+                             int rank, int mode, int flags, const int* qown, const int* qslot, const int* summary,
+                             float* send, int64_t* qidx, void* stream) {
     if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world)
         return set_error(KGE_EINVAL, "kge_shard_gather_queries: bad world/rank");
     if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH)
         return set_error(KGE_EINVAL, "kge_shard_gather_queries: mode must be 0 or 1");
-    if (rows < 0 || row0 < 0 || row0 + rows > Bg || cap < 0 || width <= 0 || shard_rows < 0)
+    if (Bg < 0 || chunks < 1 || Bg % chunks || chunk < 0 || chunk >= chunks || width <= 0 || shard_rows < 0)
         return set_error(KGE_EINVAL, "kge_shard_gather_queries: bad shape");
-    if (rows == 0) return set_error(0, "");
-    if (!shard || !pos || !qown || !qslot || !qidx || (cap > 0 && !send))
+    if (Bg == 0) return set_error(0, "");
+    if (!shard || !pos || !qown || !qslot || !summary || !qidx)
         return set_error(KGE_EINVAL, "kge_shard_gather_queries: null pointer");
-    int qc0, qc1;
-    const int ncol = query_cols(mode, qc0, qc1);
+    int qc0, qc1, pcol;
+    const int ncol = query_cols(mode, flags, qc0, qc1, pcol);
+    const int64_t rows = Bg / chunks;
+    const int* qtot = summary + (int64_t)world * world + (int64_t)chunk * ncol * world;
     const int vec4 = (width % 4 == 0 && ld % 4 == 0 && ((uintptr_t)shard % 16) == 0 && ((uintptr_t)send % 16) == 0);
     const int64_t waves = ncol * rows;
     hipLaunchKernelGGL(gather_queries_kernel, dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)),
-                       dim3(kBlock), 0, (hipStream_t)stream, shard, shard_rows, ld, shard_lo, pos, Bg, row0, rows,
-                       ncol, qc0, qc1, qown, qslot, rank, cap, width, send, qidx, vec4);
+                       dim3(kBlock), 0, (hipStream_t)stream, shard, shard_rows, ld, shard_lo, pos, Bg, chunk * rows,
+                       rows, ncol, qc0, qc1, qown, qslot, qtot, world, rank, width, send, qidx, vec4);
     return launched("kge_shard_gather_queries");
 }
 
 int kge_shard_finish(const float* recv, const int* tot, const int* hpre, const int64_t* pos, const int64_t* neg,
-                     int64_t neg_ld, int64_t Bg, int64_t N, int64_t nentity, int world, int home,
+                     int64_t neg_ld, int64_t Bg, int64_t N, int64_t nentity, int world, int home, int mode,
                      float temperature, int adversarial, float* scores, int64_t ns_ld, float* out_neg,
                      float* pos_scores, float* out_pos, void* stream) {
     int rc = check_world(Bg, world, nentity);
     if (rc) return rc;
     if (home < 0 || home >= world || N < 0) return set_error(KGE_EINVAL, "kge_shard_finish: bad home or N");
+    if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH)
+        return set_error(KGE_EINVAL, "kge_shard_finish: mode must be 0 or 1");
     const int64_t B = Bg / world;
     if (B == 0) return set_error(0, "");
     if (!tot || !hpre || !pos || (N > 0 && (!neg || !scores)) || !out_neg || !pos_scores || !out_pos)
         return set_error(KGE_EINVAL, "kge_shard_finish: null pointer");
     // recv may be NULL only when nothing was received (no candidate of these rows has an owner)
+    int qc0, qc1, pcol;
+    query_cols(mode, 0, qc0, qc1, pcol);
     const Owners own = make_owners(nentity, world);
     const hipStream_t st = (hipStream_t)stream;
     const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock));
     // the row's positive is column N: N + 1 columns cover ceil((N + 1) / 64) register slots
     if (N + 1 <= 4 * kWave)
         hipLaunchKernelGGL(shard_finish_kernel<4>, grid, dim3(kBlock), 0, st, recv, tot, hpre, pos, neg, neg_ld, Bg, B,
-                           N, own, home, temperature, adversarial, scores, ns_ld, out_neg, pos_scores, out_pos);
+                           N, own, home, pcol, temperature, adversarial, scores, ns_ld, out_neg, pos_scores, out_pos);
     else if (N + 1 <= 17 * kWave && N <= 16 * kWave)
         hipLaunchKernelGGL(shard_finish_kernel<17>, grid, dim3(kBlock), 0, st, recv, tot, hpre, pos, neg, neg_ld, Bg,
-                           B, N, own, home, temperature, adversarial, scores, ns_ld, out_neg, pos_scores, out_pos);
+                           B, N, own, home, pcol, temperature, adversarial, scores, ns_ld, out_neg, pos_scores, out_pos);
     else {
         hipLaunchKernelGGL(shard_finish_kernel<0>, grid, dim3(kBlock), 0, st, recv, tot, hpre, pos, neg, neg_ld, Bg, B,
-                           N, own, home, temperature, adversarial, scores, ns_ld, out_neg, pos_scores, out_pos);
+                           N, own, home, pcol, temperature, adversarial, scores, ns_ld, out_neg, pos_scores, out_pos);
         rc = launched("kge_shard_finish scatter");
         if (rc) return rc;
         hipLaunchKernelGGL(shard_rows_reduce_kernel, grid, dim3(kBlock), 0, st, scores, ns_ld, B, N, temperature,

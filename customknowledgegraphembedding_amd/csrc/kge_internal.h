@@ -33,6 +33,7 @@ enum Kind {
     KIND_SHARD_EPILOGUE = 15,  // row-sharded train step: owned score gradients, every slot's chain, loss
     KIND_STEP_FWD_XCD = 16,    // kge_step_forward's negatives, XCD-sliced entity table, ascending ids per wave
     KIND_SCORE_SHARD_XCD = 17, // kge_score_indexed / kge_score_sharded in the same order (no positives)
+    KIND_SHARD_POS_HEAD = 18,  // row-sharded forward, head-batch positives on the head's owner (compact out)
 };
 // query operands a score function's gradient has (q0 always; q1 for the complex / split forms; q2 InterHT)
 constexpr int shard_nq(int fn) {

@@ -10,20 +10,22 @@ Two layouts:
   so every rank can work out from the ids alone who owns which row and in which order it will send it:
   the collectives carry payload only. One step (`step_forward`):
     0. plan: ownership counts and ranks of the batch's candidates and query rows      kge_shard_plan
-    1. query rows: each owner gathers the query-entity rows it owns, compacted;
-       one ALL-GATHER of [ncol, cap] rows per rank                                     RCCL
+    1. query rows (the negative call's query entity only): each owner gathers the
+       rows it owns, compacted; one ALL-TO-ALL sends that block to every rank           RCCL
     2. every rank scores only the candidates it owns, writing the scores compacted
        per row (column order, the row's positive last) into one block per home rank    kge_score_sharded_compact
+       (head-batch positives: the owner of the head, with the tail from step 1)
     3. one ALL-TO-ALL: home h receives exactly the scores of its rows, no indices       RCCL
     4. home rank: scatter by the same ranks, self-adversarial reduction, logsigmoid     kge_shard_finish
   Each (row, candidate) has exactly one owner and is moved once: the sharded scores equal the
-  unsharded ones bitwise. (An out-of-range id has no owner and scores 0 here; the unsharded kernels
-  score it against a zero row, as TF-GPU gather does.) Per step and rank the collectives move
-  ~7/8 of (W B ncol ent_dim) query floats in and ~7/8 of (B (N+1)) scores in, against twice those
-  queries and W times those scores for the zero-padded SUM all-reduce / reduce-scatter of round 2.
-  Pipelining: the global batch is cut into K chunks of W/K whole homes; every chunk's all-gather
-  is issued up front, chunk k is scored as soon as its rows arrived, and its all-to-all runs on
-  RCCL's stream while chunk k+1 is scored.
+  unsharded ones bitwise. (An id without an owner — out of range — scores 0 here; the unsharded
+  kernels score it against a zero row, as TF-GPU gather does.) Per step and rank the collectives
+  move ~7/8 of (W B ent_dim) query floats in and ~7/8 of (B (N+1)) scores in, against 2 x ncol times
+  those queries and W times those scores for the zero-padded SUM all-reduce / reduce-scatter of
+  round 2. Pipelining: the global batch is cut into K chunks of W/K whole homes; every chunk's query
+  exchange is issued up front, chunk k is scored as soon as its rows arrived, and its score
+  all-to-all runs on RCCL's stream while chunk k+1 is scored. At W = 1 the step is the unsharded
+  fused forward.
 
 * Row-sharded gather (`ShardedKGE.step_forward_gather`, the north star's literal scheme, kept beside
   owner-computes as SURVEY §8e asks so the two can be measured against each other): every rank
@@ -74,10 +76,19 @@ def default_chunks(world: int, chunks=None) -> int:
     return want
 
 
-def query_cols(mode: int):
-    """Columns of pos holding each batch row's query entity: the negative call's (head-batch: the
-    tail, else the head) and, in head-batch mode, the positive call's (the head)."""
-    return [2, 0] if mode == HEAD_BATCH else [0]
+KGE_SHARD_TWO_COLUMNS = 1  # include/kge_hip.h
+
+
+def query_cols(mode: int, flags: int = 0):
+    """Columns of pos whose entity rows the exchange moves: the negative call's query entity (head-batch:
+    the tail, else the head) and, with KGE_SHARD_TWO_COLUMNS in head-batch mode, the positive call's (the
+    head). Without it the head-batch positive is scored by the owner of its head."""
+    return [2, 0] if (mode == HEAD_BATCH and flags & KGE_SHARD_TWO_COLUMNS) else ([2] if mode == HEAD_BATCH else [0])
+
+
+def positive_col(mode: int, flags: int = 0):
+    """Column of pos whose owner scores the positive (kge_shard_plan's candidate N)."""
+    return 0 if (mode == HEAD_BATCH and not flags & KGE_SHARD_TWO_COLUMNS) else 2
 
 
 # ------------------------------------------------------------------------------------------------
@@ -236,13 +247,15 @@ def run_threads(fns):
 class ShardPlan:
     """Ownership counts and ranks of one global batch (kge_shard_plan; identical on every rank).
     Device arrays: cnt, hpre [W, Bg], qown, qslot [ncol, Bg]; `summary()` -> (tot [W, W], qtot [K,
-    ncol, W]) on the host: tot[h, o] = scores of home h's rows owned by rank o (the all-to-all split
-    sizes), qtot[k, c, o] = chunk k's column-c query rows owned by o (the all-gather caps). The host copy
-    is issued asynchronously when the plan is made: a plan made one step ahead costs no host wait."""
+    ncol, W]) on the host: tot[h, o] = scores of home h's rows owned by rank o (the score all-to-all's
+    split sizes), qtot[k, c, o] = chunk k's column-c query rows owned by o (the query all-to-all's). The
+    host copy is issued asynchronously when the plan is made: a plan made one step ahead costs no host
+    wait."""
 
-    def __init__(self, world, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summary_dev, summary_host, event):
-        self.world, self.chunks, self.mode, self.Bg, self.N = world, chunks, mode, Bg, N
-        self.ncol = len(query_cols(mode))
+    def __init__(self, world, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summary_dev, summary_host, event,
+                 flags=0):
+        self.world, self.chunks, self.mode, self.Bg, self.N, self.flags = world, chunks, mode, Bg, N, flags
+        self.ncol = len(query_cols(mode, flags))
         self.cnt, self.hpre, self.qown, self.qslot = cnt, hpre, qown, qslot
         self._dev, self._host, self._event = summary_dev, summary_host, event
         self._parsed = None
@@ -286,48 +299,49 @@ class HipShardKernels:
 
     # ---- the O(information) exchange of the sharded forward (kge_shard_*; include/kge_hip.h) ----
     @staticmethod
-    def plan(sk, pos_g, neg_g, mode, chunks):
+    def plan(sk, pos_g, neg_g, mode, chunks, flags=0):
         Bg, N = neg_g.shape
         W = sk.world
-        nc = len(query_cols(mode))
+        nc = len(query_cols(mode, flags))
         i32 = dict(dtype=torch.int32, device=neg_g.device)
         cnt, hpre = torch.empty((W, Bg), **i32), torch.empty((W, Bg), **i32)
         qown, qslot = torch.empty((nc, Bg), **i32), torch.empty((nc, Bg), **i32)
         summ = torch.empty(W * W + chunks * nc * W, **i32)
         rc = _lib.load().kge_shard_plan(pos_g.data_ptr(), neg_g.data_ptr(), neg_g.stride(0), Bg, N, sk.nentity, W,
-                                        chunks, mode, cnt.data_ptr(), hpre.data_ptr(), qown.data_ptr(),
+                                        chunks, mode, flags, cnt.data_ptr(), hpre.data_ptr(), qown.data_ptr(),
                                         qslot.data_ptr(), summ.data_ptr(), _st(neg_g))
         check(rc, "kge_shard_plan")
-        host = torch.empty(summ.shape, dtype=torch.int32, pin_memory=True)
+        host = sk._pinned(summ.numel())
         host.copy_(summ, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return ShardPlan(W, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summ, host, ev)
+        return ShardPlan(W, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summ, host, ev, flags)
 
     @staticmethod
-    def gather_queries(sk, plan, pos_g, row0, rows, cap, send, qidx):
+    def gather_queries(sk, plan, pos_g, k, send, qidx):
         rc = _lib.load().kge_shard_gather_queries(
-            sk.shard.data_ptr(), sk.shard.shape[0], sk.shard.stride(0), sk.lo, pos_g.data_ptr(), plan.Bg, row0, rows,
-            sk.entity_dim, sk.world, sk.rank, plan.mode, plan.qown.data_ptr(), plan.qslot.data_ptr(), cap,
-            send.data_ptr(), qidx.data_ptr(), _st(sk.shard))
+            sk.shard.data_ptr(), sk.shard.shape[0], sk.shard.stride(0), sk.lo, pos_g.data_ptr(), plan.Bg,
+            plan.chunks, k, sk.entity_dim, sk.world, sk.rank, plan.mode, plan.flags, plan.qown.data_ptr(),
+            plan.qslot.data_ptr(), plan._dev.data_ptr(), send.data_ptr() if send.numel() else None, qidx.data_ptr(),
+            _st(sk.shard))
         check(rc, "kge_shard_gather_queries")
 
     @staticmethod
-    def score_compact(sk, mode, qblock, qidx, pos_g, neg_g, plan, row0, rows, send):
-        """Owned scores of rows [row0, row0 + rows) (whole homes) -> send, compacted."""
-        N = 1 if mode == SINGLE else plan.N
-        Bg = plan.Bg
-        hB = Bg // sk.world
+    def score_compact(sk, positives, qblock, qidx, pos_g, neg_g, plan, row0, rows, send):
+        """Owned scores of rows [row0, row0 + rows) (whole homes) -> send, compacted: the negatives
+        (positives = 0) or the positives (1) of the plan's negative mode."""
+        N = plan.N
+        hB = plan.Bg // sk.world
         rel = sk.relation_embedding
         pos = pos_g[row0:row0 + rows]
-        neg = None if mode == SINGLE else neg_g[row0:row0 + rows]
+        neg = neg_g[row0:row0 + rows]
         rc = _lib.load().kge_score_sharded_compact(
-            sk.fn, mode, qblock.data_ptr(), qblock.shape[0], qblock.stride(0), qidx.data_ptr(), rel.data_ptr(),
-            rel.shape[0], rel.stride(0), sk.rel_off, sk.shard.data_ptr(), sk.shard.shape[0], sk.shard.stride(0),
-            sk.lo, pos.data_ptr(), None if neg is None else neg.data_ptr(), 0 if neg is None else neg.stride(0),
-            rows, N, sk.D, float(sk.gamma), float(sk.emb_range), float(sk.modulus),
-            plan.hpre[sk.rank, row0:].data_ptr(), plan.cnt[sk.rank, row0:].data_ptr(), plan._dev.data_ptr(),
-            sk.world, sk.rank, hB, row0 // hB, send.data_ptr(), _st(sk.shard))
+            sk.fn, plan.mode, int(positives), qblock.data_ptr(), qblock.shape[0], qblock.stride(0), qidx.data_ptr(),
+            rel.data_ptr(), rel.shape[0], rel.stride(0), sk.rel_off, sk.shard.data_ptr(), sk.shard.shape[0],
+            sk.shard.stride(0), sk.lo, pos.data_ptr(), neg.data_ptr(), neg.stride(0), rows, N, sk.D,
+            float(sk.gamma), float(sk.emb_range), float(sk.modulus), plan.hpre[sk.rank, row0:].data_ptr(),
+            plan.cnt[sk.rank, row0:].data_ptr(), plan._dev.data_ptr(), sk.world, sk.rank, hB, row0 // hB,
+            send.data_ptr() if send.numel() else None, _st(sk.shard))
         check(rc, "kge_score_sharded_compact")
 
     @staticmethod
@@ -339,9 +353,9 @@ class HipShardKernels:
         pos_raw, out_pos = torch.empty(B, **f32), torch.empty(B, **f32)
         rc = _lib.load().kge_shard_finish(
             recv.data_ptr() if recv.numel() else None, plan._dev.data_ptr(), plan.hpre.data_ptr(), pos_g.data_ptr(),
-            neg_g.data_ptr(), neg_g.stride(0), plan.Bg, N, sk.nentity, W, r, float(temperature), int(adversarial),
-            scores.data_ptr(), scores.stride(0), out_neg.data_ptr(), pos_raw.data_ptr(), out_pos.data_ptr(),
-            _st(neg_g))
+            neg_g.data_ptr(), neg_g.stride(0), plan.Bg, N, sk.nentity, W, r, plan.mode, float(temperature),
+            int(adversarial), scores.data_ptr(), scores.stride(0), out_neg.data_ptr(), pos_raw.data_ptr(),
+            out_pos.data_ptr(), _st(neg_g))
         check(rc, "kge_shard_finish")
         return out_neg, out_pos, scores
 
@@ -463,6 +477,7 @@ class ShardedKGE:
         self.step = 0
         self.loss_sum = None  # optional 0-dim fp32 device tensor: the step adds W * sum(replica losses)
         self._bufs = {}
+        self._pin, self._pin_i = [], 0
 
     @classmethod
     def from_model(cls, model, group=None, kernels=None, world=None, rank=None, comm=None):
@@ -508,7 +523,20 @@ class ShardedKGE:
         return self
 
     # ---- the exchange (§ module docstring) ----
-    def plan(self, pos_g, neg_g, mode, chunks=None):
+    def _pinned(self, n):
+        """A pinned host int32 buffer for a plan's summary (a ring of four: plans made ahead stay valid)."""
+        if len(self._pin) < 4 or self._pin[self._pin_i].numel() < n:
+            buf = torch.empty(max(n, 64), dtype=torch.int32, pin_memory=torch.cuda.is_available())
+            if len(self._pin) < 4:
+                self._pin.append(buf)
+                self._pin_i = len(self._pin) - 1
+            else:
+                self._pin[self._pin_i] = buf
+        out = self._pin[self._pin_i][:n]
+        self._pin_i = (self._pin_i + 1) % 4
+        return out
+
+    def plan(self, pos_g, neg_g, mode, chunks=None, flags=0):
         """The exchange plan of a global batch (kge_shard_plan, two launches on the current stream, the
         split sizes copied to the host asynchronously). Make it one step ahead and pass it to
         step_forward(plan=...) so the host never waits for it."""
@@ -518,40 +546,46 @@ class ShardedKGE:
         WB = neg_g.shape[0]
         if WB % self.world:
             raise ValueError("global batch must split evenly over ranks")
-        return self.kernels.plan(self, pos_g, neg_g, mode, default_chunks(self.world, chunks))
+        return self.kernels.plan(self, pos_g, neg_g, mode, default_chunks(self.world, chunks), flags)
 
-    def _gather_queries(self, plan, pos_g, k):
-        """Chunk k's query rows: each owner's compacted rows, all-gathered (async). Returns (block [W *
-        ncol * cap, ent_dim] viewed as rows, qidx [ncol, rows] into it, handle)."""
-        W, K, nc = self.world, plan.chunks, plan.ncol
+    def _exchange_queries(self, plan, pos_g, k):
+        """Chunk k's query rows: each owner's compacted rows sent to every rank (one all-to-all, async).
+        Returns (block [rows, ent_dim], qidx [ncol, Bg/K] into it, handle, buffers to keep alive)."""
+        W, me = self.world, self.rank
         _, qtot = plan.summary()
-        Rk = plan.Bg // K
-        cap = max(1, int(qtot[k].max()))
+        per = [int(qtot[k, :, o].sum()) for o in range(W)]
+        d = self.entity_dim
         f32 = dict(dtype=torch.float32, device=self.device)
-        send = torch.empty((nc, cap, self.entity_dim), **f32)
-        qidx = torch.empty((nc, Rk), dtype=torch.int64, device=self.device)
-        self.kernels.gather_queries(self, plan, pos_g, k * Rk, Rk, cap, send, qidx)
-        if W == 1:
-            return send.view(-1, self.entity_dim), qidx, _Done(), send
-        block = torch.empty((W * nc * cap, self.entity_dim), **f32)
-        h = self.comm.all_gather_into(block, send, async_op=True)
+        send = torch.empty((W, per[me], d), **f32)
+        qidx = torch.empty((plan.ncol, plan.Bg // plan.chunks), dtype=torch.int64, device=self.device)
+        self.kernels.gather_queries(self, plan, pos_g, k, send, qidx)
+        block = torch.empty((sum(per), d), **f32)
+        h = self.comm.all_to_all(block.view(-1), send.view(-1), [p * d for p in per], [per[me] * d] * W,
+                                 async_op=True)
         return block, qidx, h, send
 
     def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None, plan=None):
         """pos_g [W*B, 3], neg_g [W*B, N] (the global batch, identical on every rank) ->
         (out_neg [B], out_pos [B], scores [B, N]) for this rank's home rows [rank*B, (rank+1)*B).
-        Collectives: one all-gather of compacted query rows and one all-to-all of compacted owned
-        scores per chunk, every one through self.comm."""
+        Collectives: per chunk one all-to-all of compacted query rows and one all-to-all of compacted
+        owned scores, both through self.comm. At W = 1 the exchange is the identity and the step is the
+        unsharded fused forward (kge_step_forward; the same scores bitwise)."""
+        W, me = self.world, self.rank
+        if W == 1:
+            m = ops.mode_id(mode)
+            if m not in (HEAD_BATCH, TAIL_BATCH):
+                raise ValueError("step_forward needs a negative mode (0 or 1)")
+            return self.kernels.step_forward(self.fn, m, self.shard, self.relation_embedding, self.rel_off, pos_g,
+                                             neg_g, self.D, self.gamma, self.emb_range, self.modulus, temperature,
+                                             adversarial)
         if plan is None:
             plan = self.plan(pos_g, neg_g, mode, chunks)
-        mode = plan.mode
-        W, me, K = self.world, self.rank, plan.chunks
-        Bg = plan.Bg
-        Rk, hpc = Bg // K, W // K
+        K = plan.chunks
+        Rk, hpc = plan.Bg // K, W // K
         tot, _ = plan.summary()
         k_home = me // hpc
-        # 1. every chunk's query all-gather in flight before any scoring
-        qx = [self._gather_queries(plan, pos_g, k) for k in range(K)]
+        # 1. every chunk's query exchange in flight before any scoring
+        qx = [self._exchange_queries(plan, pos_g, k) for k in range(K)]
         # 2. owner-computes scores per chunk, compacted per home; 3. all-to-all to the home ranks
         pending, recv = [], None
         for k in range(K):
@@ -560,11 +594,8 @@ class ShardedKGE:
             homes = range(k * hpc, (k + 1) * hpc)
             in_splits = [int(tot[hh, me]) if hh in homes else 0 for hh in range(W)]
             send = torch.empty(sum(in_splits), dtype=torch.float32, device=self.device)
-            self.kernels.score_compact(self, mode, block, qidx[0], pos_g, neg_g, plan, k * Rk, Rk, send)
-            self.kernels.score_compact(self, SINGLE, block, qidx[-1], pos_g, neg_g, plan, k * Rk, Rk, send)
-            if W == 1:
-                recv = send
-                continue
+            self.kernels.score_compact(self, 0, block, qidx[0], pos_g, neg_g, plan, k * Rk, Rk, send)
+            self.kernels.score_compact(self, 1, block, qidx[-1], pos_g, neg_g, plan, k * Rk, Rk, send)
             out_splits = [int(tot[me, o]) for o in range(W)] if k == k_home else [0] * W
             out = torch.empty(sum(out_splits), dtype=torch.float32, device=self.device)
             if k == k_home:
@@ -579,21 +610,24 @@ class ShardedKGE:
         """Bytes this rank receives per step through the forward's collectives (payload only)."""
         tot, qtot = plan.summary()
         W, me = self.world, self.rank
-        caps = [max(1, int(qtot[k].max())) for k in range(plan.chunks)]
-        q = sum((W - 1) * plan.ncol * c * self.entity_dim * 4 for c in caps)
+        q = int(sum(qtot[k, :, o].sum() for k in range(plan.chunks) for o in range(W) if o != me)) * self.entity_dim * 4
         s = sum(int(tot[me, o]) for o in range(W) if o != me) * 4
-        return {"query_rows_allgather": q, "scores_alltoall": s}
+        return {"query_rows": q, "scores": s}
 
-    def assemble_queries(self, pos_g, mode, plan=None):
+    def assemble_queries(self, pos_g, mode):
         """The query-entity rows of every global batch row: (qent [Bg, ent_dim] = E[pos[:, 2 if head
-        else 0]], qent_pos [Bg, ent_dim] = E[pos[:, 0]]): owners' compacted rows, one all-gather, then a
+        else 0]], qent_pos [Bg, ent_dim] = E[pos[:, 0]]): owners' compacted rows, one all-to-all, then a
         local gather into batch-row order."""
-        if plan is None:
-            plan = self.plan(pos_g, pos_g[:, :0], mode, chunks=1)
-        block, qidx, h, _ = self._gather_queries(plan, pos_g, 0)
-        h.wait()
         Bg = pos_g.shape[0]
-        rows = torch.empty((plan.ncol, Bg, self.entity_dim), dtype=torch.float32, device=self.device)
+        rows = torch.empty((2 if ops.mode_id(mode) == HEAD_BATCH else 1, Bg, self.entity_dim), dtype=torch.float32,
+                           device=self.device)
+        if self.world == 1:
+            for i, c in enumerate(query_cols(ops.mode_id(mode), KGE_SHARD_TWO_COLUMNS)):
+                self.kernels.gather_rows(self.shard, self.lo, pos_g[:, c:], 3, Bg, rows[i])
+            return rows[0], rows[-1]
+        plan = self.plan(pos_g, pos_g[:, :0], mode, chunks=1, flags=KGE_SHARD_TWO_COLUMNS)
+        block, qidx, h, _ = self._exchange_queries(plan, pos_g, 0)
+        h.wait()
         for c in range(plan.ncol):
             self.kernels.gather_rows(block, 0, qidx[c], 1, Bg, rows[c])
         return rows[0], rows[-1]
@@ -603,7 +637,7 @@ class ShardedKGE:
         aggregation): pos_g [Bg, 3], neg_g [Bg, N], weight_g [Bg] — the global batch (home rank h's
         replica batch is rows [h Bg/W, (h+1) Bg/W)), identical on every rank. Updates this rank's
         shard and the relation table in place; returns this rank's replica loss (0-dim tensor).
-        Collectives per step: one all-gather of the compacted query rows, one all-gather of [Bg, 4] row
+        Collectives per step: one all-to-all of the compacted query rows, one all-gather of [Bg, 4] row
         statistics, one SUM all-reduce of the [2 Bg, nq D] query gradients."""
         if self.adam is None:
             self.configure_optimizer()

@@ -1,7 +1,7 @@
 """GPU tests of the row-sharded forward's O(information) exchange (kge_shard_plan,
 kge_shard_gather_queries, kge_score_sharded_compact, kge_shard_finish; distributed.ShardedKGE.step_forward):
-W ranks simulated as threads of one process on one device (ThreadComm: the same all-gather / all-to-all
-calls TorchComm makes over RCCL). Every score has one owner and moves once, so each home rank's scores
+W ranks simulated as threads of one process on one device (ThreadComm: the same all-to-all calls
+TorchComm makes over RCCL). Every score has one owner and moves once, so each home rank's scores
 must equal the unsharded kernel's bitwise, and its reductions kge_step_forward's."""
 import numpy as np
 import pytest
@@ -45,14 +45,16 @@ def _ranks(m, W, comm=None):
 
 @pytest.mark.parametrize("W,K", [(1, 1), (2, 1), (2, 2), (3, 3), (8, 4), (8, 2)])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_plan_matches_restatement(W, K, mode):
-    """kge_shard_plan's counts, prefixes, query owners / slots and summary equal the CPU restatement."""
+@pytest.mark.parametrize("flags", [0, 1])
+def test_plan_matches_restatement(W, K, mode, flags):
+    """kge_shard_plan's counts, prefixes, query owners / slots and summary equal the CPU restatement (the
+    forward's one query column with the head-batch positive on the head's owner, and the train step's two)."""
     E, R, Bh, N = 301, 7, 5, 70
     m = _model("DistMult", E, R, 8)
     pos, neg = _batch(E, R, W * Bh, N, seed=W + 10 * K, bad=True)
     sk = _ranks(m, W)[0]
-    got = sk.kernels.plan(sk, pos, neg, mode, K)
-    want = OracleShardKernels.plan(sk, pos.cpu(), neg.cpu(), mode, K)
+    got = sk.kernels.plan(sk, pos, neg, mode, K, flags)
+    want = OracleShardKernels.plan(sk, pos.cpu(), neg.cpu(), mode, K, flags)
     for a in ("cnt", "hpre", "qown", "qslot"):
         assert torch.equal(getattr(got, a).cpu().long(), getattr(want, a).long()), a
     gt, gq = got.summary()
@@ -116,8 +118,8 @@ def test_sharded_forward_plan_made_ahead_and_reused():
 
 
 def test_collective_bytes_are_payload_only():
-    """Per rank the all-to-all carries exactly the rank's home scores owned elsewhere, and the query
-    all-gather at most (W - 1) * cap rows per column: both O(B) per rank, not O(W B N)."""
+    """Per rank the score all-to-all carries exactly the rank's home scores owned elsewhere, and the query
+    all-to-all exactly the other owners' query rows, no padding: O(B) and O(W B) per rank, not O(W B N)."""
     E, R, d, W, Bh, N = 4001, 5, 16, 8, 16, 256
     m = _model("DistMult", E, R, d)
     pos, neg = _batch(E, R, W * Bh, N, seed=6)
@@ -125,11 +127,14 @@ def test_collective_bytes_are_payload_only():
     plan = sk.plan(pos, neg, 0)
     cb = sk.collective_bytes(plan)
     home = slice(3 * Bh, 4 * Bh)
-    cand = torch.cat([neg[home], pos[home, 2:3]], 1)
+    cand = torch.cat([neg[home], pos[home, 0:1]], 1)  # head-batch: the positive belongs to its head's owner
     foreign = int(((cand < sk.lo) | (cand >= sk.hi)).sum())
-    assert cb["scores_alltoall"] == foreign * 4
+    assert cb["scores"] == foreign * 4
     # the zero-padded reduce-scatter moved W * Bh * (N + 1) floats per rank per step
-    assert cb["scores_alltoall"] < Bh * (N + 1) * 4 < W * Bh * (N + 1) * 4
+    assert cb["scores"] < Bh * (N + 1) * 4 < W * Bh * (N + 1) * 4
+    # query rows: exactly the batch's tails owned by the other ranks, one row each
+    tails = pos[:, 2]
+    assert cb["query_rows"] == int(((tails < sk.lo) | (tails >= sk.hi)).sum()) * m.entity_embedding.shape[1] * 4
 
 
 def test_c4_full_size_simulated_8_ranks():

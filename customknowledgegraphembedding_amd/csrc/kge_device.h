@@ -1047,6 +1047,59 @@ __global__ __launch_bounds__(kBlock) void step_fwd_kernel(ScoreParams p) {
 //   RED: 0 mean, 1 self-adversarial with the softmax detached, 2 self-adversarial (TF semantics).
 // Scores, the row finish and the per-candidate code are the step forward's (bitwise the same scores).
 // ---------------------------------------------------------------------------------------------
+// InterHT's Jacobian sums on packed fp32 pairs (v_pk_mul / v_pk_fma_f32: two elements per instruction):
+//   x = q0 bh - ah q1 + q2 (tail) or ah q1 - q0 bh + q2 (head), J = -sgn(x) (bh, -ah, 1) resp. (-bh, ah, 1)
+// sgn(x) exactly (0 at x = 0, as tf.abs' gradient) as med3(x 2^127 2^127, -1, 1); the sums take nwa = -wa
+// and nwb = -wb so that nwa sgn(x) = wa Gx. No range mask: past D the candidate, q0, q1 and q2 are 0, so
+// x = 0 and the element adds nothing.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 sgn2(f32x2 x) {
+    x = x * 0x1p127f;
+    x = x * 0x1p127f;
+    return f32x2{__builtin_amdgcn_fmed3f(x.x, -1.f, 1.f), __builtin_amdgcn_fmed3f(x.y, -1.f, 1.f)};
+}
+template <bool CH, int V, bool TWO>
+__device__ __forceinline__ void group_jac_ih(const vecf<V>& ca, const vecf<V>& cb, const vecf<V>& q0,
+                                             const vecf<V>& q1, const vecf<V>& q2, float ia, float ib, float nwa,
+                                             float nwb, vecf<V>& a0, vecf<V>& a1, vecf<V>& a2, vecf<V>& b0,
+                                             vecf<V>& b1, vecf<V>& b2) {
+    static_assert(V % 2 == 0, "pairs");
+#pragma unroll
+    for (int i = 0; i < V; i += 2) {
+        const f32x2 ah = f32x2{ca.a[i], ca.a[i + 1]} * ia;
+        const f32x2 bh = f32x2{cb.a[i], cb.a[i + 1]} * ib + 1.f;
+        const f32x2 Q0{q0.a[i], q0.a[i + 1]}, Q1{q1.a[i], q1.a[i + 1]}, Q2{q2.a[i], q2.a[i + 1]};
+        const f32x2 x = CH ? (ah * Q1 - Q0 * bh + Q2) : (Q0 * bh - ah * Q1 + Q2);
+        const f32x2 sg = sgn2(x);
+        auto acc = [&](float nw, vecf<V>& s0, vecf<V>& s1, vecf<V>& s2) {
+            const f32x2 g = sg * nw;  // w Gx
+            f32x2 u0{s0.a[i], s0.a[i + 1]}, u1{s1.a[i], s1.a[i + 1]}, u2{s2.a[i], s2.a[i + 1]};
+            if (CH) {
+                u0 = u0 - g * bh;
+                u1 = u1 + g * ah;
+            } else {
+                u0 = u0 + g * bh;
+                u1 = u1 - g * ah;
+            }
+            u2 = u2 + g;
+            s0.a[i] = u0.x;
+            s0.a[i + 1] = u0.y;
+            s1.a[i] = u1.x;
+            s1.a[i + 1] = u1.y;
+            s2.a[i] = u2.x;
+            s2.a[i + 1] = u2.y;
+        };
+        acc(nwa, a0, a1, a2);
+        if constexpr (TWO) acc(nwb, b0, b1, b2);
+    }
+}
+
+// Softmax / sigmoid weights of the fused query pass on the hardware exp / log / rcp (v_exp_f32, v_log_f32,
+// v_rcp_f32). They weight gradient terms only (the forward's outputs are row_reduce's, in full precision).
+__device__ __forceinline__ float fexp(float x) { return __expf(x); }
+__device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float flog_sigmoid(float x) { return fminf(x, 0.f) - __logf(1.f + __expf(-fabsf(x))); }
+
 template <int FN, bool CH, int V, bool TWO>
 __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, const vecf<V>& q0, const vecf<V>& q1,
                                           const vecf<V>& q2, bool in, float ia, float ib, const ScoreParams& p,
@@ -1097,7 +1150,17 @@ __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, 
     }
 }
 
-#if KGE_FG_KEEPSGN
+// step_fwd_grad_kernel's query pass: gradient weights on the hardware exp / log / rcp and InterHT's Jacobian
+// sums on packed fp32 pairs with the sign recomputed (KGE_FG_FAST = 1), or the libm-accurate weights and
+// scalar sums with the score pass's kept signs (0, the round-2 form)
+#ifndef KGE_FG_FAST
+#define KGE_FG_FAST 1
+#endif
+#if KGE_FG_FAST
+#undef KGE_FG_KEEPSGN
+#define KGE_FG_KEEPSGN 0
+#endif
+#if KGE_FG_KEEPSGN || KGE_FG_FAST
 #define KGE_FG_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #else
 #define KGE_FG_ATTR
@@ -1143,13 +1206,22 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
         // one candidate's contribution (s is wave-uniform)
         auto accumulate = [&](const Cand<FN, V, G>& c, const LdsQuery<V>& q, float s, float2 nst,
                               const vecf<V>* nsg) {
+#if KGE_FG_FAST
+            auto xexp = [](float x) { return fexp(x); };
+            auto xsig = [](float x) { return fsigmoid(x); };
+            auto xlogsig = [](float x) { return flog_sigmoid(x); };
+#else
+            auto xexp = [](float x) { return expf(x); };
+            auto xsig = [](float x) { return sigmoidf(x); };
+            auto xlogsig = [](float x) { return log_sigmoid(x); };
+#endif
             float wa, wb = 0.f;
             if constexpr (RED == 0) {
-                wa = -sigmoidf(s);
+                wa = -xsig(s);
             } else {
                 const float t = T * s;
                 if (t > mrun) {  // online softmax: rescale the running sums to the new maximum
-                    const float sc = expf(mrun - t);
+                    const float sc = xexp(mrun - t);
                     Z *= sc;
                     Ln *= sc;
 #pragma unroll
@@ -1167,16 +1239,25 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
                         }
                     mrun = t;
                 }
-                const float e = expf(t - mrun);
-                const float f = log_sigmoid(-s);
+                const float e = xexp(t - mrun);
+                const float f = xlogsig(-s);
                 Z += e;
                 Ln += e * f;
-                wa = e * -sigmoidf(s);
+                wa = e * -xsig(s);
                 if constexpr (TWO) {
                     wa += e * (T * f);
                     wb = e;
                 }
             }
+#if KGE_FG_FAST
+            if constexpr (FN == KGE_INTERHT && V % 2 == 0) {
+#pragma unroll
+                for (int k = 0; k < G; ++k)
+                    group_jac_ih<CH, V, TWO>(c.ca[k], c.cb[k], q.q0[k], q.q1[k], q.q2[k], nst.x, nst.y, -wa, -wb, a0[k],
+                                             a1[k], a2[k], b0[k], b1[k], b2[k]);
+                return;
+            }
+#endif
 #pragma unroll
             for (int k = 0; k < G; ++k)
                 group_jac<FN, CH, V, TWO>(c.ca[k], c.cb[k], q.q0[k], q.q1[k], q.q2[k], (lane + k * kWave) < DV, nst.x,

@@ -205,10 +205,13 @@ __global__ __launch_bounds__(kBlock) void gather_queries_kernel(const float* __r
         if (lane == 0) qidx[t] = -1;
         return;
     }
+    // every cross-lane read happens with the whole wave active (inside `if (lane == 0)` the compiler may
+    // compute roff for lane 0 only and read garbage from lane o)
     const int64_t inner = (c ? __builtin_amdgcn_readlane(col0, o) : 0) + s;
-    if (lane == 0) qidx[t] = __builtin_amdgcn_readlane(roff, o) + inner;
-    if (o != rank) return;
+    const int64_t at = __builtin_amdgcn_readlane(roff, o) + inner;
     const int64_t per = __builtin_amdgcn_readlane(piece, rank);
+    if (lane == 0) qidx[t] = at;
+    if (o != rank) return;
     const int64_t r = pos[g * 3 + (c == 0 ? qc0 : qc1)] - lo;
     const bool ok = r >= 0 && r < shard_rows;  // o == rank implies it
     const float* src = shard + (ok ? r : 0) * ld;

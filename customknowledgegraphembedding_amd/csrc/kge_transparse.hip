@@ -143,6 +143,9 @@ __device__ __forceinline__ int acc_row(int wm, int i, int r, int half) {
 // by the whole block: bucket counts in LDS, the bucket holding position g (one wave, running prefix), then an
 // ordered ballot scan for the k-th row of that bucket. Every thread returns the same row.
 constexpr int kTsSortMaxRel = 1023;
+// Each block finds its batch row in (relation, row) order by scanning the whole batch: O(B) per block, O(B^2)
+// per launch, so the sorted order is used up to this many batch rows (natural order beyond).
+constexpr int64_t kTsSortMaxB = 8192;
 __device__ int64_t ts_sorted_row(const TsParams& p, int64_t g, int* hist, int* wcnt, int* sel) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int nb = (int)p.nrel + 1;
@@ -232,7 +235,7 @@ ts_rows_kernel(TsParams p) {
         int64_t b = grp;
         int ch = chunk;
         if constexpr (OP == TS_FWD) {
-            if (p.nrel <= kTsSortMaxRel) {
+            if (p.nrel <= kTsSortMaxRel && p.B <= kTsSortMaxB) {
                 // Relation-sorted order: blocks i and i + 8 share an XCD, each XCD takes a contiguous run of ranks,
                 // and rank k is the k-th batch row in (relation, row) order, so an XCD works through one or two
                 // relations at a time and their M_r tiles (1 MB at d = 500) stay in its L2 (scripts/ts_rel_probe.py:
@@ -585,6 +588,262 @@ ts_rows_kernel(TsParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Head-batch forward, 256-row blocks (ts_fwd_x3_kernel; the bf16x3 numerics of ts_rows_kernel<TS_FWD, 4,
+// true>). One block = one batch row's 256 negatives, which share M_r: each staged M_r chunk serves all 256
+// rows (the 128-row kernel stages the 1 MB M_r twice per batch row and its rows once per 128-column tile).
+//   * 8 waves, a 4 x 2 grid of 64-row x 128-column wave tiles (eight 32 x 32 accumulators, 128 AGPRs);
+//     the block's 256 x 256 tile sweeps the columns in ceil(d / 256) super-tiles;
+//   * K in chunks of 32, DOUBLE-buffered in LDS (2 x (256 + 256) x 34 dwords = 139 KB: one block per CU,
+//     2 waves per SIMD): the next chunk is loaded into registers while this one's 96 MFMAs per wave run,
+//     stored into the other buffer, and one barrier per chunk orders the two;
+//   * each finished super-tile is folded into per-row sums of p^2 and |p c| right away (half-wave shuffles,
+//     the two column waves added through LDS), so no per-row state lives in registers across super-tiles.
+// ---------------------------------------------------------------------------------------------
+constexpr int XBR = 256, XBC = 256, XLDB = 34, kXThreads = 1024, kXWaves = kXThreads / kWave;
+constexpr int kTsBigMaxDim = 3072;  // the dynamic u - 1 image (d floats) beside ~146 KB of static LDS
+
+// ts_sorted_row for a block of NT threads: the g-th batch row in (relation bucket, row) order. O(B) per
+// block (so O(B^2) per launch): used up to kTsSortMaxB batch rows.
+template <int NT>
+__device__ int64_t ts_sorted_row_nt(const TsParams& p, int64_t g, int* hist, int* wcnt, int* sel) {
+    constexpr int NW = NT / kWave;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int nb = (int)p.nrel + 1;
+    auto bucket = [&](int64_t bb) {
+        const int64_t rr = p.pos[bb * 3 + 1];
+        return (rr >= 0 && rr < p.nrel) ? (int)rr : (int)p.nrel;
+    };
+    for (int i = t; i < nb; i += NT) hist[i] = 0;
+    __syncthreads();
+    for (int64_t bb = t; bb < p.B; bb += NT) atomicAdd(&hist[bucket(bb)], 1);
+    __syncthreads();
+    if (wave == 0) {
+        int run = 0;
+        for (int base = 0; base < nb; base += kWave) {
+            const int i = base + lane;
+            const int c = i < nb ? hist[i] : 0;
+            int incl = c;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const int y = __shfl_up(incl, o, kWave);
+                if (lane >= o) incl += y;
+            }
+            const int excl = run + incl - c;
+            const uint64_t m = __ballot(i < nb && g >= excl && g < excl + c);
+            if (m) {
+                const int src = __builtin_ctzll(m);
+                if (lane == src) {
+                    sel[0] = i;
+                    sel[1] = (int)(g - excl);
+                }
+                break;
+            }
+            run += __shfl(incl, kWave - 1, kWave);
+        }
+    }
+    __syncthreads();
+    const int want = sel[0], k = sel[1];
+    int64_t seen = 0;
+    for (int64_t s0 = 0; s0 < p.B; s0 += NT) {
+        const int64_t bb = s0 + t;
+        const bool m = bb < p.B && bucket(bb) == want;
+        const uint64_t bal = __ballot(m);
+        if (lane == 0) wcnt[wave] = __popcll(bal);
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int w = 0; w < NW; ++w) {
+            before += (w < wave) ? wcnt[w] : 0;
+            total += wcnt[w];
+        }
+        if (m && seen + before + __popcll(bal & ((1ull << lane) - 1ull)) == k) sel[2] = (int)bb;
+        seen += total;
+        __syncthreads();
+        if (seen > k) break;  // uniform
+    }
+    return sel[2];
+}
+
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(4))) void
+ts_fwd_x3_kernel(TsParams p) {
+    __shared__ __attribute__((aligned(16))) float Ax[2][XBR * XLDB];
+    __shared__ __attribute__((aligned(16))) float Bx[2][XBC * XLDB];
+    __shared__ const float* rowp[XBR];
+    __shared__ float2 red[2][XBR];
+    __shared__ float wsum[kXWaves];
+    __shared__ int wcnt[kXWaves];
+    __shared__ int hist[kTsSortMaxRel + 1];
+    __shared__ int sel[3];
+    extern __shared__ float cs[];  // u - 1, d floats
+
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int half = lane >> 5, col = lane & 31;
+    const int wr = wave >> 1, wc = wave & 1;  // wave tile: rows [32 wr, 32 wr + 32), columns [128 wc, 128 wc + 128)
+    const int d = p.d;
+    const int64_t blk = blockIdx.x;
+    int64_t b = blk / p.nchunk;
+    int ch = (int)(blk % p.nchunk);
+    if (p.nrel <= kTsSortMaxRel && p.B <= kTsSortMaxB) {
+        // relation-sorted order (ts_rows_kernel's): blocks i and i + 8 share an XCD, each XCD takes a contiguous
+        // run of ranks, rank k = the k-th batch row in (relation, row) order: M_r stays in the XCD's L2
+        const int64_t nblk = p.B * p.nchunk, q8 = nblk / 8, r8 = nblk % 8, x = blk % 8;
+        const int64_t rank = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blk / 8;
+        ch = (int)(rank % p.nchunk);
+        b = ts_sorted_row_nt<kXThreads>(p, rank / p.nchunk, hist, wcnt, sel);
+    }
+    const int64_t r = p.pos[b * 3 + 1];
+    const bool rok = r >= 0 && r < p.nrel;
+    const int64_t n0 = (int64_t)ch * XBR;
+    const int nrows = (int)min<int64_t>(XBR, p.N - n0);
+    if (t < XBR) {
+        const float* rp = nullptr;
+        if (t < nrows) {
+            const int64_t id = p.neg[b * p.neg_ld + n0 + t];
+            if (id >= 0 && id < p.nent) rp = p.ent + id * p.ent_ld;
+        }
+        rowp[t] = rp;
+        red[0][t] = red[1][t] = make_float2(0.f, 0.f);
+    }
+    // u - 1 for the relation row
+    {
+        float ss = 0.f;
+        for (int j = t; j < d; j += kXThreads) {
+            const float v = rok ? p.rel[r * p.rel_ld + j] : 0.f;
+            cs[j] = v;
+            ss += v * v;
+        }
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, kWave);
+        if (lane == 0) wsum[wave] = ss;
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < kXWaves; ++w) tot += wsum[w];
+        const float rnorm = sqrtf(tot);
+        for (int j = t; j < d; j += kXThreads) cs[j] = cs[j] / rnorm - 1.f;
+    }
+    const float* Wr = rok ? (p.Mpre ? p.Mpre : p.W) + r * (int64_t)d * d : nullptr;
+    const float* Mr = (rok && !p.Mpre) ? p.mask + r * (int64_t)d * d : nullptr;
+    __syncthreads();
+
+    // staging: thread t, unit u < 4: A row (f >> 3), k 4 (f & 7), f = t + 512 u; B k = lane & 31, columns
+    // 4 ((lane >> 5) + 2 (wave + 8 u)) .. + 3 of the super-tile (transposed into Bx[col][k])
+    constexpr int XU = (XBR * TBK / 4) / kXThreads;  // float4 per thread per operand and K chunk
+    float4 ra[XU], rbv[XU];
+    const int nk = (d + TBK - 1) / TBK, nct = (d + XBC - 1) / XBC;
+    auto gload = [&](int ct, int k0) {
+#pragma unroll
+        for (int u = 0; u < XU; ++u) {
+            const int f = t + kXThreads * u, ka = k0 + 4 * (f & 7);
+            const float* arow = rowp[f >> 3];  // re-read from LDS: no 64-bit pointers held across the loop
+            ra[u] = arow ? ld4<4>(arow, ka, d - ka) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int kb = k0 + (lane & 31), j = ct * XBC + 4 * ((lane >> 5) + 2 * (wave + kXWaves * u));
+            if (Wr && kb < d) {
+                const int64_t off = (int64_t)kb * d + j;
+                rbv[u] = Mr ? mul4(ld4<4>(Wr, off, d - j), ld4<4>(Mr, off, d - j)) : ld4<4>(Wr, off, d - j);
+            } else {
+                rbv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < XU; ++u) {
+            const int f = t + kXThreads * u, o = (f >> 3) * XLDB + 4 * (f & 7);
+            *reinterpret_cast<float2*>(&Ax[buf][o]) = make_float2(ra[u].x, ra[u].y);
+            *reinterpret_cast<float2*>(&Ax[buf][o + 2]) = make_float2(ra[u].z, ra[u].w);
+            const int kb = lane & 31, cg = 4 * ((lane >> 5) + 2 * (wave + kXWaves * u));
+            Bx[buf][(cg + 0) * XLDB + kb] = rbv[u].x;
+            Bx[buf][(cg + 1) * XLDB + kb] = rbv[u].y;
+            Bx[buf][(cg + 2) * XLDB + kb] = rbv[u].z;
+            Bx[buf][(cg + 3) * XLDB + kb] = rbv[u].w;
+        }
+    };
+    auto frag = [&](const float* base) {
+        f32x8 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float2 x = *reinterpret_cast<const float2*>(base + 2 * q);
+            v[2 * q] = x.x;
+            v[2 * q + 1] = x.y;
+        }
+        return v;
+    };
+    constexpr int XI = 1;  // 32-row tiles per wave
+    for (int ct = 0; ct < nct; ++ct) {
+        f32x16 acc[XI][4];
+#pragma unroll
+        for (int i = 0; i < XI; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r2 = 0; r2 < 16; ++r2) acc[i][j][r2] = 0.f;
+        gload(ct, 0);
+        sstore(0);
+        __syncthreads();
+        for (int kc = 0; kc < nk; ++kc) {
+            const int buf = kc & 1;
+            if (kc + 1 < nk) gload(ct, (kc + 1) * TBK);
+#pragma unroll
+            for (int s2 = 0; s2 < TBK / 16; ++s2) {
+                const int ko = 16 * s2 + 8 * half;
+                bf16x8 a[XI][3];
+#pragma unroll
+                for (int i = 0; i < XI; ++i)
+                    split3_bf16(frag(&Ax[buf][(wr * 32 * XI + i * 32 + col) * XLDB + ko]), a[i][0], a[i][1], a[i][2]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bf16x8 bb[3];
+                    split3_bf16(frag(&Bx[buf][(wc * 128 + j * 32 + col) * XLDB + ko]), bb[0], bb[1], bb[2]);
+#pragma unroll
+                    for (int q = 0; q < 6; ++q)
+#pragma unroll
+                        for (int i = 0; i < XI; ++i)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0,
+                                                                               0, 0);
+                    // keep each column tile's fragment reads and splits next to its MFMAs (no hoisting of the
+                    // next tiles' operands: register pressure)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            if (kc + 1 < nk) sstore(buf ^ 1);
+            __syncthreads();
+        }
+        // fold the super-tile: per row sum over this wave's 128 columns of p^2 and |p c|
+#pragma unroll
+        for (int i = 0; i < XI; ++i)
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) {
+                float sq = 0.f, ab = 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int cg = ct * XBC + wc * 128 + j * 32 + col;
+                    const float c = cg < d ? cs[cg] : 0.f;
+                    const float v = acc[i][j][r2];
+                    sq = fmaf(v, v, sq);
+                    ab += fabsf(v * c);
+                }
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) {
+                    sq += __shfl_xor(sq, o, kWave);
+                    ab += __shfl_xor(ab, o, kWave);
+                }
+                if (col == 0) {
+                    const int row = wr * 32 * XI + i * 32 + (r2 & 3) + 8 * (r2 >> 2) + 4 * half;
+                    float2& x = red[wc][row];
+                    x = make_float2(x.x + sq, x.y + ab);
+                }
+            }
+    }
+    __syncthreads();
+    if (t < nrows) {
+        const float2 x0 = red[0][t], x1 = red[1][t];
+        const float2 x = make_float2(x0.x + x1.x, x0.y + x1.y);
+        const int64_t n = n0 + t;
+        p.out[b * p.out_ld + n] = p.gamma - x.y / sqrtf(x.x);
+        if (p.stats) p.stats[b * p.N + n] = x;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void ts_premul_kernel(const float4* __restrict__ W, const float4* __restrict__ mask,
                                                           float4* __restrict__ M, int64_t n4) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock)
@@ -905,6 +1164,18 @@ void launch_rows(const TsParams& p, hipStream_t st) {
             return e && e[0] == '1';
         }();
         if (use_v4(p) && !f32) {
+            // head-batch rows beyond one 128-row block: 256-row blocks that stage each M_r chunk once for all the
+            // batch row's negatives (KGE_TS_BIG=0 keeps the 128-row form, for A/B runs)
+            static const bool big_off = [] {
+                const char* e = getenv("KGE_TS_BIG");
+                return e && e[0] == '0';
+            }();
+            if (!p.grouped && p.N > TBM && p.d <= kTsBigMaxDim && !big_off) {
+                TsParams q = p;
+                q.nchunk = (int)((p.N + XBR - 1) / XBR);
+                hipLaunchKernelGGL(ts_fwd_x3_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);
+                return;
+            }
             hipLaunchKernelGGL((ts_rows_kernel<OP, 4, true>), dim3(blocks), dim3(kBlock), lds, st, p);
             return;
         }

@@ -275,6 +275,8 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
         plans = {}
 
         def step(b, i):
+            if sk.world == 1:  # no exchange: the step is the unsharded fused forward
+                return sk.step_forward(b[0], b[1], i % 2)
             nb = batches[(i + 1) % 4]
             plan = plans.pop(i, None) or sk.plan(b[0], b[1], i % 2)
             plans[i + 1] = sk.plan(nb[0], nb[1], (i + 1) % 2)
@@ -293,6 +295,61 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
     if dist_on:
         tdist.barrier()
     return time.perf_counter() - t0
+
+
+def rank0_step_parts(ranks, pos, neg, mode, chunks=None):
+    """Rank 0's device work of one row-sharded forward step, as closures over inputs prepared untimed
+    with every simulated rank's contributions (ranks: ShardedKGE of ranks 0..W-1 on one GPU): plan_fn,
+    gather (the query gathers), score (compact scoring of every chunk), finish (scatter + reductions)."""
+    from customknowledgegraphembedding_amd.distributed import HipShardKernels as HK
+    r0 = ranks[0]
+    world, device = r0.world, r0.device
+    Bg = pos.shape[0]
+    plan = r0.plan(pos, neg, mode, chunks)
+    tot, qtot = plan.summary()
+    K = plan.chunks
+    Rk, hpc = Bg // K, world // K
+    blocks, qidxs, sends = [], [], []
+    for k in range(K):
+        per = [int(qtot[k, :, o].sum()) for o in range(world)]
+        pieces = []
+        for sk in ranks:  # every owner's compacted rows: the query all-to-all's output
+            snd = torch.empty((world, per[sk.rank], r0.entity_dim), dtype=torch.float32, device=device)
+            qidx = torch.empty((plan.ncol, Rk), dtype=torch.int64, device=device)
+            HK.gather_queries(sk, plan, pos, k, snd, qidx)
+            pieces.append(snd[0])
+        blocks.append(torch.cat(pieces))
+        qidxs.append(qidx)
+        sends.append(torch.empty(int(sum(tot[h, 0] for h in range(k * hpc, (k + 1) * hpc))), dtype=torch.float32,
+                                 device=device))
+    # home 0's score all-to-all output: every owner's block of home 0's rows, in rank order
+    recv = []
+    for sk in ranks:
+        snd = torch.empty(int(sum(tot[h, sk.rank] for h in range(hpc))), dtype=torch.float32, device=device)
+        HK.score_compact(sk, 0, blocks[0], qidxs[0][0], pos, neg, plan, 0, Rk, snd)
+        HK.score_compact(sk, 1, blocks[0], qidxs[0][-1], pos, neg, plan, 0, Rk, snd)
+        recv.append(snd[:int(tot[0, sk.rank])])
+    recv = torch.cat(recv)
+    q_sends = [torch.empty((world, int(qtot[k, :, 0].sum()), r0.entity_dim), dtype=torch.float32, device=device)
+               for k in range(K)]
+    q_idx_scratch = torch.empty_like(qidxs[0])
+
+    def gather():
+        for k in range(K):
+            HK.gather_queries(r0, plan, pos, k, q_sends[k], q_idx_scratch)
+
+    def score():
+        for k in range(K):
+            HK.score_compact(r0, 0, blocks[k], qidxs[k][0], pos, neg, plan, k * Rk, Rk, sends[k])
+            HK.score_compact(r0, 1, blocks[k], qidxs[k][-1], pos, neg, plan, k * Rk, Rk, sends[k])
+
+    def score_neg():
+        for k in range(K):
+            HK.score_compact(r0, 0, blocks[k], qidxs[k][0], pos, neg, plan, k * Rk, Rk, sends[k])
+
+    return {"plan": plan, "chunks": K, "plan_fn": lambda: HK.plan(r0, pos, neg, mode, K), "gather": gather,
+            "score": score, "score_neg": score_neg,
+            "finish": lambda: HK.shard_finish(r0, plan, recv, pos, neg, 1.0, True)}
 
 
 def shard_sim_bench(device, world=8, reps=10, v1=None):
@@ -343,48 +400,12 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
     # rank 0 alone: the kernels of one step, with the other ranks' contributions prepared untimed
     HK = HipShardKernels
     r0 = ranks[0]
-    plan = r0.plan(pos, neg, 0)
-    tot, qtot = plan.summary()
-    K = plan.chunks
-    Rk, hpc = Bg // K, world // K
-    blocks, qidxs, sends = [], [], []
-    for k in range(K):
-        per = [int(qtot[k, :, o].sum()) for o in range(world)]
-        parts = []
-        for sk in ranks:  # every owner's compacted rows: the query all-to-all's output
-            snd = torch.empty((world, per[sk.rank], r0.entity_dim), dtype=torch.float32, device=device)
-            qidx = torch.empty((plan.ncol, Rk), dtype=torch.int64, device=device)
-            HK.gather_queries(sk, plan, pos, k, snd, qidx)
-            parts.append(snd[0])
-        blocks.append(torch.cat(parts))
-        qidxs.append(qidx)
-        sends.append(torch.empty(int(sum(tot[h, 0] for h in range(k * hpc, (k + 1) * hpc))), dtype=torch.float32,
-                                 device=device))
-    # home 0's score all-to-all output: every owner's block of home 0's rows, in rank order
-    recv = []
-    for sk in ranks:
-        snd = torch.empty(int(sum(tot[h, sk.rank] for h in range(hpc))), dtype=torch.float32, device=device)
-        HK.score_compact(sk, 0, blocks[0], qidxs[0][0], pos, neg, plan, 0, Rk, snd)
-        HK.score_compact(sk, 1, blocks[0], qidxs[0][-1], pos, neg, plan, 0, Rk, snd)
-        recv.append(snd[:int(tot[0, sk.rank])])
-    recv = torch.cat(recv)
-    q_sends = [torch.empty((world, int(qtot[k, :, 0].sum()), r0.entity_dim), dtype=torch.float32, device=device)
-               for k in range(K)]
-    q_idx_scratch = torch.empty_like(qidxs[0])
-
-    def rank0_gather():
-        for k in range(K):
-            HK.gather_queries(r0, plan, pos, k, q_sends[k], q_idx_scratch)
-
-    def rank0_score():
-        for k in range(K):
-            HK.score_compact(r0, 0, blocks[k], qidxs[k][0], pos, neg, plan, k * Rk, Rk, sends[k])
-            HK.score_compact(r0, 1, blocks[k], qidxs[k][-1], pos, neg, plan, k * Rk, Rk, sends[k])
-
-    t_plan = timed(lambda: HK.plan(r0, pos, neg, 0, K))
-    t_gather = timed(rank0_gather)
-    t_score = timed(rank0_score)
-    t_finish = timed(lambda: HK.shard_finish(r0, plan, recv, pos, neg, 1.0, True))
+    parts = rank0_step_parts(ranks, pos, neg, 0)
+    plan, K = parts["plan"], parts["chunks"]
+    t_plan = timed(parts["plan_fn"])
+    t_gather = timed(parts["gather"])
+    t_score = timed(parts["score"])
+    t_finish = timed(parts["finish"])
     rank_us = t_plan + t_gather + t_score + t_finish
     cb = r0.collective_bytes(plan)
     coll = cb["query_rows"] + cb["scores"]

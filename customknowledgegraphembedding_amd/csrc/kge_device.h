@@ -1160,8 +1160,14 @@ __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, 
 #undef KGE_FG_KEEPSGN
 #define KGE_FG_KEEPSGN 0
 #endif
+#ifndef KGE_FG_WPE
+#define KGE_FG_WPE 2
+#endif
+#ifndef KGE_FG_DEPTH
+#define KGE_FG_DEPTH 2
+#endif
 #if KGE_FG_KEEPSGN || KGE_FG_FAST
-#define KGE_FG_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#define KGE_FG_ATTR __attribute__((amdgpu_waves_per_eu(KGE_FG_WPE)))
 #else
 #define KGE_FG_ATTR
 #endif
@@ -1314,6 +1320,15 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
                 accumulate(c, q, s, nst, nullptr);
 #endif
             };
+#if KGE_FG_DEPTH == 1
+            // one row in registers at a time (more waves per SIMD hide the gather latency instead)
+            for (int j = 0; j < nc; ++j) {
+                x0.load(cand_row(p, readlane64(my_id, j), ok0), ok0, p.D, lane);
+                one(x0, j);
+            }
+            (void)x1;
+            (void)ok1;
+#else
             // software pipeline (as score_run): row j + 1 is in flight while row j is reduced
             x0.load(cand_row(p, readlane64(my_id, 0), ok0), ok0, p.D, lane);
             int j = 0;
@@ -1330,6 +1345,7 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
             } else {
                 one(x0, j);
             }
+#endif
             if (lane < nc) p.out[b * p.out_ld + c0 + src] = my_score;
         }
     }

@@ -600,7 +600,7 @@ ts_rows_kernel(TsParams p) {
 //   * each finished super-tile is folded into per-row sums of p^2 and |p c| right away (half-wave shuffles,
 //     the two column waves added through LDS), so no per-row state lives in registers across super-tiles.
 // ---------------------------------------------------------------------------------------------
-constexpr int XBR = 256, XBC = 256, XLDB = 34, kXThreads = 1024, kXWaves = kXThreads / kWave;
+constexpr int XBR = 256, XBC = 256, XLDB = 34, kXThreads = 512, kXWaves = kXThreads / kWave;
 constexpr int kTsBigMaxDim = 3072;  // the dynamic u - 1 image (d floats) beside ~146 KB of static LDS
 
 // ts_sorted_row for a block of NT threads: the g-th batch row in (relation bucket, row) order. O(B) per
@@ -664,7 +664,7 @@ __device__ int64_t ts_sorted_row_nt(const TsParams& p, int64_t g, int* hist, int
     return sel[2];
 }
 
-__global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(4))) void
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(2))) void
 ts_fwd_x3_kernel(TsParams p) {
     __shared__ __attribute__((aligned(16))) float Ax[2][XBR * XLDB];
     __shared__ __attribute__((aligned(16))) float Bx[2][XBC * XLDB];
@@ -678,7 +678,7 @@ ts_fwd_x3_kernel(TsParams p) {
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int half = lane >> 5, col = lane & 31;
-    const int wr = wave >> 1, wc = wave & 1;  // wave tile: rows [32 wr, 32 wr + 32), columns [128 wc, 128 wc + 128)
+    const int wr = wave >> 1, wc = wave & 1;
     const int d = p.d;
     const int64_t blk = blockIdx.x;
     int64_t b = blk / p.nchunk;
@@ -727,15 +727,16 @@ ts_fwd_x3_kernel(TsParams p) {
 
     // staging: thread t, unit u < 4: A row (f >> 3), k 4 (f & 7), f = t + 512 u; B k = lane & 31, columns
     // 4 ((lane >> 5) + 2 (wave + 8 u)) .. + 3 of the super-tile (transposed into Bx[col][k])
-    constexpr int XU = (XBR * TBK / 4) / kXThreads;  // float4 per thread per operand and K chunk
-    float4 ra[XU], rbv[XU];
+    const float* arow[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) arow[u] = rowp[(t + kXThreads * u) >> 3];
+    float4 ra[4], rbv[4];
     const int nk = (d + TBK - 1) / TBK, nct = (d + XBC - 1) / XBC;
     auto gload = [&](int ct, int k0) {
 #pragma unroll
-        for (int u = 0; u < XU; ++u) {
+        for (int u = 0; u < 4; ++u) {
             const int f = t + kXThreads * u, ka = k0 + 4 * (f & 7);
-            const float* arow = rowp[f >> 3];  // re-read from LDS: no 64-bit pointers held across the loop
-            ra[u] = arow ? ld4<4>(arow, ka, d - ka) : make_float4(0.f, 0.f, 0.f, 0.f);
+            ra[u] = arow[u] ? ld4<4>(arow[u], ka, d - ka) : make_float4(0.f, 0.f, 0.f, 0.f);
             const int kb = k0 + (lane & 31), j = ct * XBC + 4 * ((lane >> 5) + 2 * (wave + kXWaves * u));
             if (Wr && kb < d) {
                 const int64_t off = (int64_t)kb * d + j;
@@ -747,7 +748,7 @@ ts_fwd_x3_kernel(TsParams p) {
     };
     auto sstore = [&](int buf) {
 #pragma unroll
-        for (int u = 0; u < XU; ++u) {
+        for (int u = 0; u < 4; ++u) {
             const int f = t + kXThreads * u, o = (f >> 3) * XLDB + 4 * (f & 7);
             *reinterpret_cast<float2*>(&Ax[buf][o]) = make_float2(ra[u].x, ra[u].y);
             *reinterpret_cast<float2*>(&Ax[buf][o + 2]) = make_float2(ra[u].z, ra[u].w);
@@ -768,11 +769,10 @@ ts_fwd_x3_kernel(TsParams p) {
         }
         return v;
     };
-    constexpr int XI = 1;  // 32-row tiles per wave
     for (int ct = 0; ct < nct; ++ct) {
-        f32x16 acc[XI][4];
+        f32x16 acc[2][4];
 #pragma unroll
-        for (int i = 0; i < XI; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -786,10 +786,10 @@ ts_fwd_x3_kernel(TsParams p) {
 #pragma unroll
             for (int s2 = 0; s2 < TBK / 16; ++s2) {
                 const int ko = 16 * s2 + 8 * half;
-                bf16x8 a[XI][3];
+                bf16x8 a[2][3];
 #pragma unroll
-                for (int i = 0; i < XI; ++i)
-                    split3_bf16(frag(&Ax[buf][(wr * 32 * XI + i * 32 + col) * XLDB + ko]), a[i][0], a[i][1], a[i][2]);
+                for (int i = 0; i < 2; ++i)
+                    split3_bf16(frag(&Ax[buf][(wr * 64 + i * 32 + col) * XLDB + ko]), a[i][0], a[i][1], a[i][2]);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     bf16x8 bb[3];
@@ -797,12 +797,9 @@ ts_fwd_x3_kernel(TsParams p) {
 #pragma unroll
                     for (int q = 0; q < 6; ++q)
 #pragma unroll
-                        for (int i = 0; i < XI; ++i)
+                        for (int i = 0; i < 2; ++i)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0,
                                                                                0, 0);
-                    // keep each column tile's fragment reads and splits next to its MFMAs (no hoisting of the
-                    // next tiles' operands: register pressure)
-                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
             if (kc + 1 < nk) sstore(buf ^ 1);
@@ -810,7 +807,7 @@ ts_fwd_x3_kernel(TsParams p) {
         }
         // fold the super-tile: per row sum over this wave's 128 columns of p^2 and |p c|
 #pragma unroll
-        for (int i = 0; i < XI; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int r2 = 0; r2 < 16; ++r2) {
                 float sq = 0.f, ab = 0.f;
@@ -828,7 +825,7 @@ ts_fwd_x3_kernel(TsParams p) {
                     ab += __shfl_xor(ab, o, kWave);
                 }
                 if (col == 0) {
-                    const int row = wr * 32 * XI + i * 32 + (r2 & 3) + 8 * (r2 >> 2) + 4 * half;
+                    const int row = wr * 64 + i * 32 + (r2 & 3) + 8 * (r2 >> 2) + 4 * half;
                     float2& x = red[wc][row];
                     x = make_float2(x.x + sq, x.y + ab);
                 }

@@ -26,3 +26,6 @@ print('$v$i', 'kernel_us', round(r['kernel_avg_us'],1), 'fp32eq_TF', round(r['fp
   done
 done
 echo session-b done
+VARIANTS="main=customknowledgegraphembedding_amd/libkge_hip.so d1w3=abtmp/d1w3/libkge_hip.so" \
+  TESTS="tests/test_train_gpu.py" bash scripts/ab_lib.sh || exit $?
+echo session-b2 done

@@ -271,15 +271,17 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
     else:
         # the exchange plan of step i + 1 (kge_shard_plan: ownership counts and ranks from the ids, its
         # split sizes copied to the host asynchronously) is issued before step i's work, so the host
-        # never waits for it; it is device work inside the timed region like the rest of the step
+        # never waits for it; it is device work inside the timed region like the rest of the step, on a
+        # side stream (KGE_PLAN_STREAM=main: the step's own stream) where it overlaps step i's scoring
         plans = {}
+        side = torch.cuda.Stream(device) if os.environ.get("KGE_PLAN_STREAM", "side") == "side" else None
 
         def step(b, i):
             if sk.world == 1:  # no exchange: the step is the unsharded fused forward
                 return sk.step_forward(b[0], b[1], i % 2)
             nb = batches[(i + 1) % 4]
             plan = plans.pop(i, None) or sk.plan(b[0], b[1], i % 2)
-            plans[i + 1] = sk.plan(nb[0], nb[1], (i + 1) % 2)
+            plans[i + 1] = sk.plan(nb[0], nb[1], (i + 1) % 2, stream=side)
             return sk.step_forward(b[0], b[1], i % 2, plan=plan)
     for i in range(a.warmup):
         step(batches[i % 4], i)
@@ -299,13 +301,15 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
 
 def rank0_step_parts(ranks, pos, neg, mode, chunks=None):
     """Rank 0's device work of one row-sharded forward step, as closures over inputs prepared untimed
-    with every simulated rank's contributions (ranks: ShardedKGE of ranks 0..W-1 on one GPU): plan_fn,
-    gather (the query gathers), score (compact scoring of every chunk), finish (scatter + reductions)."""
+    with every simulated rank's contributions (ranks: ShardedKGE of ranks 0..W-1 on one GPU): plan_fn
+    (the plan with rank 0's bucket), gather (the query gather of every chunk, one launch), score (compact
+    scoring of every chunk), finish (scatter + reductions)."""
     from customknowledgegraphembedding_amd.distributed import HipShardKernels as HK
     r0 = ranks[0]
     world, device = r0.world, r0.device
     Bg = pos.shape[0]
-    plan = r0.plan(pos, neg, mode, chunks)
+    plans = [sk.plan(pos, neg, mode, chunks) for sk in ranks]  # identical but for each rank's bucket
+    plan = plans[0]
     tot, qtot = plan.summary()
     K = plan.chunks
     Rk, hpc = Bg // K, world // K
@@ -316,7 +320,7 @@ def rank0_step_parts(ranks, pos, neg, mode, chunks=None):
         for sk in ranks:  # every owner's compacted rows: the query all-to-all's output
             snd = torch.empty((world, per[sk.rank], r0.entity_dim), dtype=torch.float32, device=device)
             qidx = torch.empty((plan.ncol, Rk), dtype=torch.int64, device=device)
-            HK.gather_queries(sk, plan, pos, k, snd, qidx)
+            HK.gather_queries(sk, plans[sk.rank], pos, k, snd, qidx)
             pieces.append(snd[0])
         blocks.append(torch.cat(pieces))
         qidxs.append(qidx)
@@ -326,29 +330,19 @@ def rank0_step_parts(ranks, pos, neg, mode, chunks=None):
     recv = []
     for sk in ranks:
         snd = torch.empty(int(sum(tot[h, sk.rank] for h in range(hpc))), dtype=torch.float32, device=device)
-        HK.score_compact(sk, 0, blocks[0], qidxs[0][0], pos, neg, plan, 0, Rk, snd)
-        HK.score_compact(sk, 1, blocks[0], qidxs[0][-1], pos, neg, plan, 0, Rk, snd)
+        HK.score_compact(sk, blocks[0], qidxs[0][0], pos, neg, plans[sk.rank], 0, Rk, snd)
         recv.append(snd[:int(tot[0, sk.rank])])
     recv = torch.cat(recv)
-    q_sends = [torch.empty((world, int(qtot[k, :, 0].sum()), r0.entity_dim), dtype=torch.float32, device=device)
-               for k in range(K)]
-    q_idx_scratch = torch.empty_like(qidxs[0])
-
-    def gather():
-        for k in range(K):
-            HK.gather_queries(r0, plan, pos, k, q_sends[k], q_idx_scratch)
+    q_send = torch.empty(sum(world * int(qtot[k, :, 0].sum()) for k in range(K)) * r0.entity_dim,
+                         dtype=torch.float32, device=device)
+    q_idx = torch.empty((plan.ncol, Bg), dtype=torch.int64, device=device)
 
     def score():
         for k in range(K):
-            HK.score_compact(r0, 0, blocks[k], qidxs[k][0], pos, neg, plan, k * Rk, Rk, sends[k])
-            HK.score_compact(r0, 1, blocks[k], qidxs[k][-1], pos, neg, plan, k * Rk, Rk, sends[k])
+            HK.score_compact(r0, blocks[k], qidxs[k][0], pos, neg, plan, k * Rk, Rk, sends[k])
 
-    def score_neg():
-        for k in range(K):
-            HK.score_compact(r0, 0, blocks[k], qidxs[k][0], pos, neg, plan, k * Rk, Rk, sends[k])
-
-    return {"plan": plan, "chunks": K, "plan_fn": lambda: HK.plan(r0, pos, neg, mode, K), "gather": gather,
-            "score": score, "score_neg": score_neg,
+    return {"plan": plan, "chunks": K, "plan_fn": lambda: HK.plan(r0, pos, neg, mode, K),
+            "gather": lambda: HK.gather_queries(r0, plan, pos, -1, q_send, q_idx), "score": score,
             "finish": lambda: HK.shard_finish(r0, plan, recv, pos, neg, 1.0, True)}
 
 
@@ -406,7 +400,8 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
     t_gather = timed(parts["gather"])
     t_score = timed(parts["score"])
     t_finish = timed(parts["finish"])
-    rank_us = t_plan + t_gather + t_score + t_finish
+    # the plan is made a step ahead on a side stream (sharded_bench, KGE_PLAN_STREAM): off the critical path
+    rank_us = t_gather + t_score + t_finish
     cb = r0.collective_bytes(plan)
     coll = cb["query_rows"] + cb["scores"]
     B_ = Bg // world
@@ -414,8 +409,8 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
                        f"entity table split over {world} simulated ranks",
            "step_us_all_ranks_one_gpu": sim_dev_us,
            "step_wall_us_all_ranks_one_gpu": sim_wall_us,
-           "rank_step_kernels_us": {"plan": t_plan, "query_gather": t_gather, "compact_scoring": t_score,
-                                    "finish": t_finish, "total": rank_us},
+           "rank_step_kernels_us": {"plan_side_stream": t_plan, "query_gather": t_gather, "compact_scoring": t_score,
+                                    "finish": t_finish, "critical_path": rank_us},
            "unsharded_global_kernel_us": unsharded_us,
            "unsharded_global_step_us": step_us,
            "rank_scoring_over_unsharded": t_score / unsharded_us,
@@ -424,7 +419,8 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
                                                        "scores_reduce_scatter": (world - 1) * B_ * (N + 1) * 4},
            "chunks": K,
            "what": "rank_step_kernels_us: rank 0's kernels of one 8-rank step, device time (queued behind a sleep "
-                   "kernel): its per-GPU compute in an 8-GPU step; step_us_all_ranks_one_gpu: the whole 8-rank "
+                   "kernel): its per-GPU compute in an 8-GPU step (critical_path: without the plan, which the "
+                   "step makes a step ahead on a side stream); step_us_all_ranks_one_gpu: the whole 8-rank "
                    "ShardedKGE.step_forward by 8 threads on this GPU (every rank's kernels serialised, ThreadComm "
                    "device copies standing in for RCCL, host-bound)"}
     if v1:

@@ -61,14 +61,15 @@ SIGNATURES = {
     "kge_build_id": (ctypes.c_char_p, []),
     "kge_source_hash": (ctypes.c_char_p, []),
     "kge_shard_plan": (
-        _c_i, [_c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+        _c_i, [_c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p,
+               _c_p, _c_p, _c_p]),
     "kge_shard_gather_queries": (
         _c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i, _c_i, _c_i64, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p,
                _c_p, _c_p, _c_p, _c_p]),
-    "kge_score_sharded_compact": (
+    "kge_shard_score": (
         _c_i,
-        [_c_i, _c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64,
-         _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i64,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64,
+         _c_p, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i64,
          _c_i64, _c_p, _c_p],
     ),
     "kge_shard_finish": (

@@ -465,9 +465,9 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM || kind == KIND_STEP_FWD ||
                kind == KIND_STEP_FWD_STATS || kind == KIND_STEP_FWD_GRAD || kind == KIND_SHARD_FWD_GRAD) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
-    } else if (kind == KIND_STEP_FWD_XCD || kind == KIND_SCORE_SHARD_XCD) {
+    } else if (kind == KIND_STEP_FWD_XCD || kind == KIND_SCORE_SHARD_XCD || kind == KIND_SHARD_BUCKET) {
         waves = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock * 8;  // 8 slice blocks per 4 rows
-    } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS || kind == KIND_SHARD_POS_HEAD) {
+    } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS) {
         waves = p.B;  // one wave per slot
     } else if (kind == KIND_STEP_EPILOGUE) {
         // one wave per slot (negative rows' chains, positives, negative rows' score gradients), then the
@@ -486,7 +486,6 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         // sharded scoring compacts each wave's owned candidates: long runs (up to 512 ids, ~64 owned
         // at 8 shards) keep the per-wave query build amortised; >= 8192 waves still fill the chip
         p.cpw = p.skip_foreign ? pick_cpw_sharded(p.B, p.N) : pick_cpw(p.B, p.N);
-        if (p.cmp_pre) p.cpw = (int)std::max<int64_t>(p.N, 1);  // compact ranks: one wave walks the whole row
         p.wpr = (int)((p.N + p.cpw - 1) / p.cpw);
         waves = p.B * p.wpr;
     }
@@ -724,52 +723,51 @@ int kge_score_sharded(int fn, int mode, const float* qent, int64_t q_ld, const f
     return run_score(fn, mode, p, KIND_FWD, stream);
 }
 
-int kge_score_sharded_compact(int fn, int mode, int positives, const float* qent, int64_t q_rows, int64_t q_ld,
-                              const int64_t* q_idx, const float* rel, int64_t nrelation, int64_t rel_ld,
-                              int64_t rel_off, const float* shard, int64_t shard_rows, int64_t shard_ld,
-                              int64_t shard_lo, const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t B,
-                              int64_t N, int64_t D, float gamma, float emb_range, float modulus, const int* pre,
-                              const int* cnt, const int* tot, int world, int rank, int64_t home_B, int64_t home0,
-                              float* send, void* stream) {
+int kge_shard_score(int fn, int mode, const float* qent, int64_t q_rows, int64_t q_ld, const int64_t* q_idx,
+                    const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off, const float* shard,
+                    int64_t shard_rows, int64_t shard_ld, int64_t shard_lo, const int64_t* pos, int64_t B, int64_t N,
+                    int64_t D, float gamma, float emb_range, float modulus, const int* bucket,
+                    const int* bucket_start, const int* pre, const int* cnt, const int* tot, int world, int rank,
+                    int64_t home_B, int64_t home0, float* send, void* stream) {
     if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH)
-        return fail(KGE_EINVAL, "kge_score_sharded_compact: mode must be 0 (head-batch) or 1 (tail-batch)");
-    const int smode = positives ? KGE_SINGLE : mode;
-    int rc = check_fn_mode(fn, smode);
+        return fail(KGE_EINVAL, "kge_shard_score: mode must be 0 (head-batch) or 1 (tail-batch)");
+    int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
-    if (B < 0 || N < 0 || D <= 0 || shard_rows < 0 || q_rows < 0) return fail(KGE_EINVAL, "bad shape");
+    if (B < 0 || N < 0 || D <= 0 || shard_rows <= 0 || q_rows < 0) return fail(KGE_EINVAL, "bad shape");
     if (world < 1 || rank < 0 || rank >= world || home_B <= 0 || B % home_B || home0 < 0 ||
         home0 + B / home_B > world)
-        return fail(KGE_EINVAL, "kge_score_sharded_compact: rows must be whole homes of home_B rows");
-    if (empty(B, positives ? 1 : N)) return ok();
-    if (!pos || (!positives && !neg) || !send || !qent || !q_idx || !shard || !pre || !cnt || !tot)
+        return fail(KGE_EINVAL, "kge_shard_score: rows must be whole homes of home_B rows");
+    if (shard_lo < 0 || shard_rows >= ((int64_t)1 << 25))
+        return fail(KGE_ENOTSUP, "kge_shard_score: the shard must hold < 2^25 rows");
+    if (B == 0) return ok();
+    if (!pos || !send || !qent || !q_idx || !shard || !bucket || !bucket_start || !pre || !cnt || !tot)
         return fail(KGE_EINVAL, "null pointer");
     ScoreParams p;
-    fill_indexed(p, fn, smode, shard, shard_rows, shard_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
+    fill_indexed(p, fn, mode, shard, shard_rows, shard_ld, rel, nrelation, rel_ld, rel_off, pos, nullptr, 0, B, N + 1,
                  D, gamma, emb_range, modulus);
-    // query entity rows: row q_idx[b] of the exchanged query block
+    // query entity rows: row q_idx[b] of the exchanged query block; candidates: the bucket's shard rows
     p.qent = qent;
     p.q_idx = q_idx;
     p.q_stride = 1;
     p.q_ld = q_ld;
     p.q_rows = q_rows;
+    p.c_idx = nullptr;
     p.c_base = shard_lo;
     p.skip_foreign = 1;
     p.pos_base = pos;
+    p.bk_ent = reinterpret_cast<const int2*>(bucket);
+    p.bk_start = bucket_start;
+    p.bk_ld = N + 1;
     p.cmp_pre = pre;
     p.cmp_cnt = cnt;
     p.cmp_tot = tot;
     p.cmp_home0 = home0;
-    p.cmp_last = positives != 0;
     p.home_B = home_B;
     p.world = world;
     p.rank = rank;
     p.out = send;
     p.out_ld = 0;
-    if (positives && mode == KGE_HEAD_BATCH)  // the head's owner: query from its shard, the tail from the block
-        return run_score(fn, KGE_SINGLE, p, KIND_SHARD_POS_HEAD, stream);
-    if (!positives && shard_lo >= 0 && shard_lo + shard_rows < ((int64_t)1 << 31) && use_xcd_order(shard_rows, N))
-        return run_score(fn, mode, p, KIND_SCORE_SHARD_XCD, stream);
-    return run_score(fn, smode, p, KIND_FWD, stream);
+    return run_score(fn, mode, p, KIND_SHARD_BUCKET, stream);
 }
 
 int kge_gather_rows(const float* table, int64_t rows, int64_t ld, int64_t lo, const int64_t* ids, int64_t id_stride,

@@ -586,8 +586,8 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Start of batch row b's run in the compact send block (ScoreParams::cmp_pre): the row's home-local
-// prefix plus this rank's owned counts of the launch's earlier homes.
+// Start of batch row b's run in the compact send block (ScoreParams::cmp_pre, kge_shard_score): the row's
+// home-local prefix plus this rank's owned counts of the launch's earlier homes.
 __device__ __forceinline__ int64_t cmp_row_off(const ScoreParams& p, int64_t b) {
     const int64_t h = b / p.home_B;
     int64_t off = p.cmp_pre[b];
@@ -598,12 +598,11 @@ __device__ __forceinline__ int64_t cmp_row_off(const ScoreParams& p, int64_t b) 
 // Walks candidates [lo, hi) of batch row b and calls body(row, n, cnt) with the owned ones compacted
 // into lanes 0..cnt-1 (row: local shard row, n: candidate column), in candidate order; every call but
 // the last has cnt = 64. With zero_out, a foreign candidate's score slot p.out[b, n] is written 0 (the
-// partial score block a SUM over shards assembles). In compact mode (p.cmp_pre) n is instead the
-// candidate's rank among the row's owned ones (the walk then covers the whole row: lo = 0).
+// partial score block a SUM over shards assembles).
 template <class Body>
 __device__ __forceinline__ void for_owned_runs(const ScoreParams& p, int64_t b, int64_t lo, int64_t hi, int lane,
                                                bool zero_out, Body&& body) {
-    int buf_row = 0, buf_n = 0, fill = 0, run = 0;
+    int buf_row = 0, buf_n = 0, fill = 0;
     for (int64_t c0 = lo; c0 < hi; c0 += kWave) {
         const int64_t n = c0 + lane;
         int64_t row = -1;
@@ -612,11 +611,7 @@ __device__ __forceinline__ void for_owned_runs(const ScoreParams& p, int64_t b, 
         if (zero_out && n < hi && !own) p.out[b * p.out_ld + n] = 0.f;
         const uint64_t m = __ballot(own);
         const int cnt = __popcll(m);
-        int n32 = (int)n;
-        if (p.cmp_pre) {
-            n32 = run + lanes_below(m);
-            run += cnt;
-        }
+        const int n32 = (int)n;
         if (cnt == 0) continue;  // wave-uniform
         const int row32 = (int)row;
         // lanes [fill, min(fill + cnt, 64)) take the first owned candidates of this chunk
@@ -647,14 +642,11 @@ __device__ __forceinline__ void for_owned_runs(const ScoreParams& p, int64_t b, 
 template <int FN, bool CH, int V, int G>
 __device__ __forceinline__ void score_owned(const ScoreParams& p, const Query<FN, CH, V, G>& q, int64_t b, int64_t lo,
                                             int64_t hi, int lane) {
-    const bool cmp = p.cmp_pre != nullptr;
-    const int64_t off = cmp ? cmp_row_off(p, b) : 0;
-    for_owned_runs(p, b, lo, hi, lane, !cmp, [&](int row, int n, int cnt) {
+    for_owned_runs(p, b, lo, hi, lane, true, [&](int row, int n, int cnt) {
         const int64_t my_id = (int64_t)row + p.c_base;
         float2 st;
         const float s = score_lanes<FN, CH, V, G, false>(p, q, my_id, cnt, lane, st);
-        if (lane < cnt)
-            p.out[cmp ? (p.cmp_last ? off + p.cmp_cnt[b] - 1 : off + n) : b * p.out_ld + n] = s;
+        if (lane < cnt) p.out[b * p.out_ld + n] = s;
     });
 }
 
@@ -678,7 +670,7 @@ __device__ __forceinline__ void score_owned(const ScoreParams& p, const Query<FN
 template <class Body>
 __device__ __forceinline__ void for_slice_runs_sorted(const ScoreParams& p, int64_t b, int64_t e_lo, int64_t e_hi,
                                                       bool take_invalid, bool zero_foreign, int lane, Body&& body) {
-    int buf_key = INT32_MAX, buf_id = -1, buf_n = 0, fill = 0, run = 0;
+    int buf_key = INT32_MAX, buf_id = -1, buf_n = 0, fill = 0;
     auto flush = [&](int cnt) {
         // sort key: (id - e_lo) << 6 | source lane (invalid ids first, as id - e_lo = 0)
         const int key = wave_sort_asc(lane < cnt ? buf_key : INT32_MAX, lane);
@@ -693,12 +685,7 @@ __device__ __forceinline__ void for_slice_runs_sorted(const ScoreParams& p, int6
         const bool valid = id >= p.c_base && id < p.c_base + p.c_rows;
         const bool own = n < p.N && (valid ? (id >= e_lo && id < e_hi) : take_invalid);
         if (zero_foreign && n < p.N && !valid) p.out[b * p.out_ld + n] = 0.f;
-        int n32 = (int)n;
-        if (p.cmp_pre) {  // compact mode: n becomes the rank among the row's candidates in the table
-            const uint64_t mv = __ballot(n < p.N && valid);
-            n32 = run + lanes_below(mv);
-            run += __popcll(mv);
-        }
+        const int n32 = (int)n;
         const uint64_t m = __ballot(own);
         const int cnt = __popcll(m);
         if (cnt == 0) continue;  // wave-uniform
@@ -812,14 +799,12 @@ score_sharded_xcd_kernel(ScoreParams p) {
     int64_t qi, ri;
     bool qok, rok;
     build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
-    const bool cmp = p.cmp_pre != nullptr;
-    const int64_t off = cmp ? cmp_row_off(p, b) : 0;
     auto run = [&](const auto& qq) {
         const bool sh = p.skip_foreign != 0;
-        for_slice_runs_sorted(p, b, e_lo, e_hi, !sh && x == 0, sh && !cmp && x == 0, lane, [&](int id, int n, int cnt) {
+        for_slice_runs_sorted(p, b, e_lo, e_hi, !sh && x == 0, sh && x == 0, lane, [&](int id, int n, int cnt) {
             float2 st;
             const float s = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, 1>(p, qq, (int64_t)id, cnt, lane, st);
-            if (lane < cnt) p.out[cmp ? off + n : b * p.out_ld + n] = s;
+            if (lane < cnt) p.out[b * p.out_ld + n] = s;
         });
     };
     if constexpr (FN == KGE_INTERHT) {
@@ -837,27 +822,88 @@ score_sharded_xcd_kernel(ScoreParams p) {
     }
 }
 
-// The row-sharded forward's positives in head-batch mode (kge_score_sharded_compact, positives = 1): the
-// exchanged query block holds the negatives' query entity, the TAIL, so the owner of the HEAD scores the
-// positive: query (h, r) built from its shard row, candidate t read from the block (q_idx[b]), the
-// single-mode (tail) formula as every positive (bitwise step_fwd_xcd_kernel's). One wave per batch row; the
-// score takes the last slot of the row's compact run.
-template <int FN, int V, int G>
-__global__ __launch_bounds__(kBlock) void shard_pos_head_kernel(ScoreParams p) {
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+// ---------------------------------------------------------------------------------------------
+// The row-sharded forward's owner-computes scoring (kge_shard_score, KIND_SHARD_BUCKET). Block i scores,
+// for the 4 batch rows b = 4 (i / 8) + w, slice x = i % 8 of each row's bucket (kge_shard_plan: this
+// rank's owned candidates grouped by XCD slice of S = ceil(rows / 8) shard rows), so, as in
+// step_fwd_xcd_kernel, every gather of a shard row is issued by one XCD and each XCD's waves sweep their
+// slice together (3.9 MB at the north star's 8-way YAGO3-10 split: the XCD's L2 holds it). A wave reads its
+// ~N / 64 entries with one load per 64 (no walk over the row's ids), sorts them by row, gathers and scores
+// them KGE_SHARD_DEPTH rows deep and writes each score at the row's compact run start + its rank: the send
+// block of the score all-to-all. Head-batch positives: the exchanged block holds the TAIL (the negatives'
+// query entity), so the wave of the head's slice on the head's owner scores query (h, r), built from its
+// shard row, against the tail row (the single-mode formula, bitwise every other positive's).
+// ---------------------------------------------------------------------------------------------
+#ifndef KGE_SHARD_DEPTH
+#define KGE_SHARD_DEPTH 2
+#endif
+template <int FN, bool CH, int V, int G>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(G <= 4 ? 4 : 1))) void
+shard_bucket_kernel(ScoreParams p) {
+    __shared__ vecf<V> q2img[kWavesPerBlock][FN == KGE_INTERHT ? G * kWave : 1];
+    const int x = blockIdx.x & 7;
+    const int w = threadIdx.x >> 6;
+    const int64_t b = (int64_t)(blockIdx.x >> 3) * kWavesPerBlock + w;
     if (b >= p.B) return;
     const int lane = threadIdx.x & 63;
-    const int64_t h = p.pos_base[b * 3] - p.c_base, rj = p.pos_base[b * 3 + 1];
-    if (h < 0 || h >= p.c_rows) return;  // another rank's head (wave-uniform)
-    const bool rok = rj >= 0 && rj < p.r_rows;
-    Query<FN, false, V, G> q;
-    q.build(p.cent + h * p.c_ld, true, p.rel + (rok ? rj : 0) * p.r_ld + p.r_off, rok, p.D, lane, p);
-    const int64_t ti = p.q_idx[b];
-    const bool tok = ti >= 0 && ti < p.q_rows;
-    Cand<FN, V, G> c;
-    c.load(p.qent + (tok ? ti : 0) * p.q_ld, tok, p.D, lane);
-    const float s = cand_score<FN, false, V, G>(c, q, p);
-    if (lane == 0) p.out[cmp_row_off(p, b) + p.cmp_cnt[b] - 1] = s;
+    const int e0 = p.bk_start[b * 9 + x], e1 = p.bk_start[b * 9 + x + 1];
+    const int64_t S = (p.c_rows + 7) / 8;
+    int64_t hloc = -1;
+    bool pos_here = false;
+    if constexpr (CH) {
+        hloc = p.pos_base[b * 3] - p.c_base;
+        pos_here = hloc >= 0 && hloc < p.c_rows && hloc / S == x;
+    }
+    if (e0 >= e1 && !pos_here) return;  // wave-uniform
+    const int64_t off = cmp_row_off(p, b);
+    if (e0 < e1) {
+        Query<FN, CH, V, G> q;
+        int64_t qi, ri;
+        bool qok, rok;
+        build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
+        const int2* ent = p.bk_ent + b * p.bk_ld;
+        const int sl0 = (int)(x * S);
+        auto run = [&](const auto& qq) {
+            for (int s0 = e0; s0 < e1; s0 += kWave) {
+                const int cnt = min(kWave, e1 - s0);
+                const int2 e = lane < cnt ? ent[s0 + lane] : make_int2(0, 0);
+                // ascending rows: key = (row - slice start) << 6 | lane
+                const int key = wave_sort_asc(lane < cnt ? ((e.x - sl0) << 6) | lane : INT32_MAX, lane);
+                const int src = key & (kWave - 1);
+                const int row = lane_pull(e.x, src), k = lane_pull(e.y, src);
+                float2 st;
+                const float sc = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, (FN == KGE_INTERHT ? 1 : KGE_SHARD_DEPTH)>(
+                    p, qq, (int64_t)row + p.c_base, cnt, lane, st);
+                if (lane < cnt) p.out[off + k] = sc;
+            }
+        };
+        if constexpr (FN == KGE_INTERHT) {
+            QueryL2<FN, CH, V, G> ql;
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                q2img[w][lane + k * kWave] = q.q2[k];
+                ql.q0[k] = q.q0[k];
+                ql.q1[k] = q.q1[k];
+            }
+            ql.q2 = LdsOperand<V>{q2img[w], lane};
+            run(ql);
+        } else {
+            run(q);
+        }
+    }
+    if constexpr (CH) {
+        if (!pos_here) return;  // wave-uniform
+        const int64_t rj = p.pos_base[b * 3 + 1];
+        const bool rok = rj >= 0 && rj < p.r_rows;
+        Query<FN, false, V, G> qp;
+        qp.build(p.cent + hloc * p.c_ld, true, p.rel + (rok ? rj : 0) * p.r_ld + p.r_off, rok, p.D, lane, p);
+        const int64_t ti = p.q_idx[b * p.q_stride];
+        const bool tok = ti >= 0 && ti < p.q_rows;
+        Cand<FN, V, G> c;
+        c.load(p.qent + (tok ? ti : 0) * p.q_ld, tok, p.D, lane);
+        const float sc = cand_score<FN, false, V, G>(c, qp, p);
+        if (lane == 0) p.out[off + p.cmp_cnt[b] - 1] = sc;
+    }
 }
 
 template <int FN, bool CH, int V, int G, bool ST = false>
@@ -2788,9 +2834,8 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         hipLaunchKernelGGL((step_fwd_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_SCORE_SHARD_XCD)
         hipLaunchKernelGGL((score_sharded_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
-    else if (kind == KIND_SHARD_POS_HEAD) {
-        if constexpr (!CH) hipLaunchKernelGGL((shard_pos_head_kernel<FN, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
-    }
+    else if (kind == KIND_SHARD_BUCKET)
+        hipLaunchKernelGGL((shard_bucket_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_STEP_FWD_GRAD) {
         if constexpr (FN != KGE_PROTATE && G <= kFwdGradMaxG) {
             if (!p.adversarial)

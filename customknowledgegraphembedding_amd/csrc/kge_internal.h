@@ -33,7 +33,7 @@ enum Kind {
     KIND_SHARD_EPILOGUE = 15,  // row-sharded train step: owned score gradients, every slot's chain, loss
     KIND_STEP_FWD_XCD = 16,    // kge_step_forward's negatives, XCD-sliced entity table, ascending ids per wave
     KIND_SCORE_SHARD_XCD = 17, // kge_score_indexed / kge_score_sharded in the same order (no positives)
-    KIND_SHARD_POS_HEAD = 18,  // row-sharded forward, head-batch positives on the head's owner (compact out)
+    KIND_SHARD_BUCKET = 18,    // row-sharded forward: this rank's bucket (kge_shard_plan) scored, compact out
 };
 // query operands a score function's gradient has (q0 always; q1 for the complex / split forms; q2 InterHT)
 constexpr int shard_nq(int fn) {
@@ -57,15 +57,17 @@ struct ScoreParams {
     int64_t c_ld, c_stride, c_rows, c_dense;
     int64_t c_base;    // candidate ids are global: row = id - c_base (row-sharded tables)
     int skip_foreign;  // sharded scoring: a candidate outside [c_base, c_base + c_rows) scores 0, no work
-    // compact output of the row-sharded score exchange (kge_score_sharded_compact): only this rank's owned
-    // scores are written, row b's at out[cmp_off(b) + k], k = the candidate's rank among the row's owned
-    // ones in column order (the positive, scored by a second launch, last). cmp_off(b) = cmp_pre[b] + the
-    // owned counts of the launch's earlier homes: the send block of an all-to-all, home-major.
-    const int* cmp_pre;   // [B] home-local exclusive prefix of this rank's owned counts (null: dense out)
+    // compact output of the row-sharded score exchange (kge_shard_score): only this rank's owned scores are
+    // written, row b's at out[cmp_off(b) + k], k = the candidate's rank among the row's owned ones in column
+    // order (the positive last). cmp_off(b) = cmp_pre[b] + the owned counts of the launch's earlier homes:
+    // the send block of an all-to-all, home-major.
+    const int* cmp_pre;   // [B] home-local exclusive prefix of this rank's owned counts
     const int* cmp_cnt;   // [B] this rank's owned candidates of each row (negatives + the positive)
     const int* cmp_tot;   // [W * W] tot[h * W + o]: candidates of home h's rows owned by rank o
     int64_t cmp_home0;    // home of the launch's row 0 (its rows are whole homes of home_B rows)
-    int cmp_last;         // the positives' launch: a row's score takes the last slot of its run
+    const int2* bk_ent;   // [B, bk_ld] kge_shard_plan's bucket: (local row, rank k) per owned candidate
+    const int* bk_start;  // [B, 9] the bucket's XCD-slice starts per row
+    int64_t bk_ld;
     float* out;
     int64_t out_ld;
     int64_t B, N;

@@ -9,11 +9,14 @@ Two layouts:
   owning rows [h B, (h+1) B)) is known to every rank (the sampler seed is replicated, so no ids move),
   so every rank can work out from the ids alone who owns which row and in which order it will send it:
   the collectives carry payload only. One step (`step_forward`):
-    0. plan: ownership counts and ranks of the batch's candidates and query rows      kge_shard_plan
+    0. plan: ownership counts and ranks of the batch's candidates and query rows,     kge_shard_plan
+       and this rank's bucket: its owned candidates per row grouped by XCD slice
+       (made a step ahead, on a side stream: it overlaps the previous step's scoring)
     1. query rows (the negative call's query entity only): each owner gathers the
        rows it owns, compacted; one ALL-TO-ALL sends that block to every rank           RCCL
-    2. every rank scores only the candidates it owns, writing the scores compacted
-       per row (column order, the row's positive last) into one block per home rank    kge_score_sharded_compact
+    2. every rank scores only the candidates it owns (its bucket: no walk over the
+       other ranks' ids), writing the scores compacted per row (column order, the
+       row's positive last) into one block per home rank                               kge_shard_score
        (head-batch positives: the owner of the head, with the tail from step 1)
     3. one ALL-TO-ALL: home h receives exactly the scores of its rows, no indices       RCCL
     4. home rank: scatter by the same ranks, self-adversarial reduction, logsigmoid     kge_shard_finish
@@ -69,8 +72,10 @@ def shard_bounds(nentity: int, world: int, rank: int):
 
 def default_chunks(world: int, chunks=None) -> int:
     """Chunks of the pipelined sharded forward: a divisor of W (each chunk is W/K whole homes),
-    the largest <= the request (default 4)."""
-    want = max(1, min(int(chunks if chunks is not None else 4), world))
+    the largest <= the request (default 2: at the C4 size on MI355X a rank's scoring takes 63 us in one
+    launch, 69 us in two, 85 us in four (launch ramp-up and tail per chunk), while two chunks already
+    hide half of each all-to-all behind scoring)."""
+    want = max(1, min(int(chunks if chunks is not None else 2), world))
     while world % want:
         want -= 1
     return want
@@ -245,20 +250,34 @@ def run_threads(fns):
 # the exchange plan of one global batch
 # ------------------------------------------------------------------------------------------------
 class ShardPlan:
-    """Ownership counts and ranks of one global batch (kge_shard_plan; identical on every rank).
-    Device arrays: cnt, hpre [W, Bg], qown, qslot [ncol, Bg]; `summary()` -> (tot [W, W], qtot [K,
-    ncol, W]) on the host: tot[h, o] = scores of home h's rows owned by rank o (the score all-to-all's
-    split sizes), qtot[k, c, o] = chunk k's column-c query rows owned by o (the query all-to-all's). The
-    host copy is issued asynchronously when the plan is made: a plan made one step ahead costs no host
-    wait."""
+    """Ownership counts and ranks of one global batch (kge_shard_plan; identical on every rank but for
+    the bucket). Device arrays: cnt, hpre [W, Bg], qown, qslot [ncol, Bg], and (the forward's plans)
+    rank `rank`'s bucket [Bg, N+1, 2] / bucket_start [Bg, 9]: its owned candidates per row grouped by XCD
+    slice, the input of kge_shard_score. `summary()` -> (tot [W, W], qtot [K, ncol, W]) on the host:
+    tot[h, o] = scores of home h's rows owned by rank o (the score all-to-all's split sizes), qtot[k, c,
+    o] = chunk k's column-c query rows owned by o (the query all-to-all's). The host copy is issued
+    asynchronously when the plan is made: a plan made one step ahead costs no host wait."""
 
     def __init__(self, world, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summary_dev, summary_host, event,
-                 flags=0):
+                 flags=0, rank=None, bucket=None, bucket_start=None):
         self.world, self.chunks, self.mode, self.Bg, self.N, self.flags = world, chunks, mode, Bg, N, flags
         self.ncol = len(query_cols(mode, flags))
         self.cnt, self.hpre, self.qown, self.qslot = cnt, hpre, qown, qslot
+        self.rank, self.bucket, self.bucket_start = rank, bucket, bucket_start
         self._dev, self._host, self._event = summary_dev, summary_host, event
         self._parsed = None
+
+    def use_on(self, stream):
+        """A plan made on a side stream (ShardedKGE.plan(stream=...)): `stream` waits for it, and its device
+        arrays are marked as used there (the caching allocator must not hand them to the side stream's next
+        plan while this stream's kernels still read them)."""
+        if getattr(self, "stream", None) is None or self.stream == stream:
+            return
+        stream.wait_event(self._event)
+        for t in (self.cnt, self.hpre, self.qown, self.qslot, self._dev, self.bucket, self.bucket_start):
+            if t is not None:
+                t.record_stream(stream)
+        self.stream = stream
 
     def summary(self):
         if self._parsed is None:
@@ -307,18 +326,25 @@ class HipShardKernels:
         cnt, hpre = torch.empty((W, Bg), **i32), torch.empty((W, Bg), **i32)
         qown, qslot = torch.empty((nc, Bg), **i32), torch.empty((nc, Bg), **i32)
         summ = torch.empty(W * W + chunks * nc * W, **i32)
+        bucket = bstart = None
+        if flags == 0:  # the forward: this rank's bucket for kge_shard_score
+            bucket, bstart = torch.empty((Bg, N + 1, 2), **i32), torch.empty((Bg, 9), **i32)
         rc = _lib.load().kge_shard_plan(pos_g.data_ptr(), neg_g.data_ptr(), neg_g.stride(0), Bg, N, sk.nentity, W,
-                                        chunks, mode, flags, cnt.data_ptr(), hpre.data_ptr(), qown.data_ptr(),
-                                        qslot.data_ptr(), summ.data_ptr(), _st(neg_g))
+                                        chunks, mode, flags, sk.rank, cnt.data_ptr(), hpre.data_ptr(),
+                                        qown.data_ptr(), qslot.data_ptr(), summ.data_ptr(),
+                                        None if bucket is None else bucket.data_ptr(),
+                                        None if bstart is None else bstart.data_ptr(), _st(neg_g))
         check(rc, "kge_shard_plan")
         host = sk._pinned(summ.numel())
         host.copy_(summ, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return ShardPlan(W, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summ, host, ev, flags)
+        return ShardPlan(W, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summ, host, ev, flags, sk.rank, bucket,
+                         bstart)
 
     @staticmethod
     def gather_queries(sk, plan, pos_g, k, send, qidx):
+        """Query rows this rank owns -> send (chunk k's block, or k = -1: every chunk's, back to back)."""
         rc = _lib.load().kge_shard_gather_queries(
             sk.shard.data_ptr(), sk.shard.shape[0], sk.shard.stride(0), sk.lo, pos_g.data_ptr(), plan.Bg,
             plan.chunks, k, sk.entity_dim, sk.world, sk.rank, plan.mode, plan.flags, plan.qown.data_ptr(),
@@ -327,22 +353,24 @@ class HipShardKernels:
         check(rc, "kge_shard_gather_queries")
 
     @staticmethod
-    def score_compact(sk, positives, qblock, qidx, pos_g, neg_g, plan, row0, rows, send):
-        """Owned scores of rows [row0, row0 + rows) (whole homes) -> send, compacted: the negatives
-        (positives = 0) or the positives (1) of the plan's negative mode."""
-        N = plan.N
+    def score_compact(sk, qblock, qidx, pos_g, neg_g, plan, row0, rows, send):
+        """Owned scores (negatives and positives) of rows [row0, row0 + rows) (whole homes) -> send,
+        compacted (kge_shard_score over the plan's bucket)."""
+        if plan.rank != sk.rank or plan.bucket is None:
+            raise ValueError("kge_shard_score needs a forward plan made by this rank (its bucket)")
+        if send.numel() == 0:  # this rank owns none of these rows' candidates
+            return
         hB = plan.Bg // sk.world
         rel = sk.relation_embedding
         pos = pos_g[row0:row0 + rows]
-        neg = neg_g[row0:row0 + rows]
-        rc = _lib.load().kge_score_sharded_compact(
-            sk.fn, plan.mode, int(positives), qblock.data_ptr(), qblock.shape[0], qblock.stride(0), qidx.data_ptr(),
+        rc = _lib.load().kge_shard_score(
+            sk.fn, plan.mode, qblock.data_ptr(), qblock.shape[0], qblock.stride(0), qidx.data_ptr(),
             rel.data_ptr(), rel.shape[0], rel.stride(0), sk.rel_off, sk.shard.data_ptr(), sk.shard.shape[0],
-            sk.shard.stride(0), sk.lo, pos.data_ptr(), neg.data_ptr(), neg.stride(0), rows, N, sk.D,
-            float(sk.gamma), float(sk.emb_range), float(sk.modulus), plan.hpre[sk.rank, row0:].data_ptr(),
-            plan.cnt[sk.rank, row0:].data_ptr(), plan._dev.data_ptr(), sk.world, sk.rank, hB, row0 // hB,
-            send.data_ptr() if send.numel() else None, _st(sk.shard))
-        check(rc, "kge_score_sharded_compact")
+            sk.shard.stride(0), sk.lo, pos.data_ptr(), rows, plan.N, sk.D, float(sk.gamma), float(sk.emb_range),
+            float(sk.modulus), plan.bucket[row0].data_ptr(), plan.bucket_start[row0].data_ptr(),
+            plan.hpre[sk.rank, row0:].data_ptr(), plan.cnt[sk.rank, row0:].data_ptr(), plan._dev.data_ptr(),
+            sk.world, sk.rank, hB, row0 // hB, send.data_ptr() if send.numel() else None, _st(sk.shard))
+        check(rc, "kge_shard_score")
 
     @staticmethod
     def shard_finish(sk, plan, recv, pos_g, neg_g, temperature, adversarial):
@@ -536,33 +564,49 @@ class ShardedKGE:
         self._pin_i = (self._pin_i + 1) % 4
         return out
 
-    def plan(self, pos_g, neg_g, mode, chunks=None, flags=0):
-        """The exchange plan of a global batch (kge_shard_plan, two launches on the current stream, the
-        split sizes copied to the host asynchronously). Make it one step ahead and pass it to
-        step_forward(plan=...) so the host never waits for it."""
+    def plan(self, pos_g, neg_g, mode, chunks=None, flags=0, stream=None):
+        """The exchange plan of a global batch (kge_shard_plan, two launches, the split sizes copied to the
+        host asynchronously). Make it one step ahead and pass it to step_forward(plan=...) so the host never
+        waits for it; with `stream` (a side stream) its integer work also overlaps the current step's
+        gather-bound scoring on the device (the side stream first waits for the current stream's queued
+        work, which made the ids)."""
         mode = ops.mode_id(mode)
         if mode not in (HEAD_BATCH, TAIL_BATCH):
             raise ValueError("the sharded step needs a negative mode (0 or 1)")
         WB = neg_g.shape[0]
         if WB % self.world:
             raise ValueError("global batch must split evenly over ranks")
-        return self.kernels.plan(self, pos_g, neg_g, mode, default_chunks(self.world, chunks), flags)
+        K = default_chunks(self.world, chunks)
+        if stream is None:
+            return self.kernels.plan(self, pos_g, neg_g, mode, K, flags)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(stream):
+            p = self.kernels.plan(self, pos_g, neg_g, mode, K, flags)
+        p.stream = stream
+        return p
 
-    def _exchange_queries(self, plan, pos_g, k):
-        """Chunk k's query rows: each owner's compacted rows sent to every rank (one all-to-all, async).
-        Returns (block [rows, ent_dim], qidx [ncol, Bg/K] into it, handle, buffers to keep alive)."""
-        W, me = self.world, self.rank
+    def _exchange_queries(self, plan, pos_g):
+        """Every chunk's query rows: each owner's compacted rows sent to every rank (one gather launch for
+        all chunks, then one async all-to-all per chunk). Returns [(block [rows, ent_dim], qidx [ncol,
+        Bg/K] into it, handle)] per chunk and the send buffer to keep alive."""
+        W, me, K = self.world, self.rank, plan.chunks
         _, qtot = plan.summary()
-        per = [int(qtot[k, :, o].sum()) for o in range(W)]
         d = self.entity_dim
         f32 = dict(dtype=torch.float32, device=self.device)
-        send = torch.empty((W, per[me], d), **f32)
-        qidx = torch.empty((plan.ncol, plan.Bg // plan.chunks), dtype=torch.int64, device=self.device)
-        self.kernels.gather_queries(self, plan, pos_g, k, send, qidx)
-        block = torch.empty((sum(per), d), **f32)
-        h = self.comm.all_to_all(block.view(-1), send.view(-1), [p * d for p in per], [per[me] * d] * W,
-                                 async_op=True)
-        return block, qidx, h, send
+        per = [[int(qtot[k, :, o].sum()) for o in range(W)] for k in range(K)]
+        send = torch.empty(sum(W * per[k][me] for k in range(K)) * d, **f32)
+        qidx = torch.empty((plan.ncol, plan.Bg), dtype=torch.int64, device=self.device)
+        self.kernels.gather_queries(self, plan, pos_g, -1, send, qidx)
+        Rk = plan.Bg // K
+        out, at = [], 0
+        for k in range(K):
+            n = W * per[k][me] * d
+            block = torch.empty((sum(per[k]), d), **f32)
+            h = self.comm.all_to_all(block.view(-1), send[at:at + n], [p * d for p in per[k]], [per[k][me] * d] * W,
+                                     async_op=True)
+            out.append((block, qidx[:, k * Rk:(k + 1) * Rk], h))
+            at += n
+        return out, send
 
     def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None, plan=None):
         """pos_g [W*B, 3], neg_g [W*B, N] (the global batch, identical on every rank) ->
@@ -580,22 +624,25 @@ class ShardedKGE:
                                              adversarial)
         if plan is None:
             plan = self.plan(pos_g, neg_g, mode, chunks)
+        if plan.rank != me:
+            raise ValueError("the plan was made by another rank (its bucket is that rank's)")
+        if getattr(plan, "stream", None) is not None:  # made on a side stream
+            plan.use_on(torch.cuda.current_stream(self.device))
         K = plan.chunks
         Rk, hpc = plan.Bg // K, W // K
         tot, _ = plan.summary()
         k_home = me // hpc
         # 1. every chunk's query exchange in flight before any scoring
-        qx = [self._exchange_queries(plan, pos_g, k) for k in range(K)]
+        qx, _qsend = self._exchange_queries(plan, pos_g)
         # 2. owner-computes scores per chunk, compacted per home; 3. all-to-all to the home ranks
         pending, recv = [], None
         for k in range(K):
-            block, qidx, h, _ = qx[k]
+            block, qidx, h = qx[k]
             h.wait()
             homes = range(k * hpc, (k + 1) * hpc)
             in_splits = [int(tot[hh, me]) if hh in homes else 0 for hh in range(W)]
             send = torch.empty(sum(in_splits), dtype=torch.float32, device=self.device)
-            self.kernels.score_compact(self, 0, block, qidx[0], pos_g, neg_g, plan, k * Rk, Rk, send)
-            self.kernels.score_compact(self, 1, block, qidx[-1], pos_g, neg_g, plan, k * Rk, Rk, send)
+            self.kernels.score_compact(self, block, qidx[0], pos_g, neg_g, plan, k * Rk, Rk, send)
             out_splits = [int(tot[me, o]) for o in range(W)] if k == k_home else [0] * W
             out = torch.empty(sum(out_splits), dtype=torch.float32, device=self.device)
             if k == k_home:
@@ -626,8 +673,9 @@ class ShardedKGE:
                 self.kernels.gather_rows(self.shard, self.lo, pos_g[:, c:], 3, Bg, rows[i])
             return rows[0], rows[-1]
         plan = self.plan(pos_g, pos_g[:, :0], mode, chunks=1, flags=KGE_SHARD_TWO_COLUMNS)
-        block, qidx, h, _ = self._exchange_queries(plan, pos_g, 0)
+        ((block, qidx, h),), qsend = self._exchange_queries(plan, pos_g)
         h.wait()
+        del qsend
         for c in range(plan.ncol):
             self.kernels.gather_rows(block, 0, qidx[c], 1, Bg, rows[c])
         return rows[0], rows[-1]

@@ -21,7 +21,8 @@ neg = torch.from_numpy(g.randint(E, size=(Bg, N))).cuda()
 tables = (m.entity_embedding.detach(), m.relation_embedding.detach(), m._gamma_f, m._range_f, 0.0)
 comm = ThreadComm(W)
 ranks = [ShardedKGE(name, E, R, d, 9.0, device="cuda", world=W, rank=r, comm=comm, full_tables=tables) for r in range(W)]
-plan = HK.plan(ranks[0], pos, neg, mode, K)
+plans = [HK.plan(sk, pos, neg, mode, K) for sk in ranks]  # identical but for each rank's bucket
+plan = plans[0]
 tot, qtot = plan.summary()
 print("tot", tot.tolist(), "qtot", qtot.tolist())
 Rk, hpc = Bg // K, W // K
@@ -31,7 +32,7 @@ for k in range(K):
     for sk in ranks:
         snd = torch.empty((W, per[sk.rank], d), device="cuda")
         qidx = torch.empty((plan.ncol, Rk), dtype=torch.int64, device="cuda")
-        HK.gather_queries(sk, plan, pos, k, snd, qidx)
+        HK.gather_queries(sk, plans[sk.rank], pos, k, snd, qidx)
         snd_o = torch.zeros((W, per[sk.rank], d))
         qidx_o = torch.zeros((plan.ncol, Rk), dtype=torch.int64)
         skc = ShardedKGE(name, E, R, d, 9.0, device="cpu", world=W, rank=sk.rank,
@@ -46,14 +47,12 @@ for k in range(K):
     for sk in ranks:
         n_send = int(sum(tot[h, sk.rank] for h in range(k * hpc, (k + 1) * hpc)))
         send = torch.full((n_send,), -7.0, device="cuda")
-        HK.score_compact(sk, 0, block, qidx_d[0], pos, neg, plan, k * Rk, Rk, send)
-        HK.score_compact(sk, 1, block, qidx_d[-1], pos, neg, plan, k * Rk, Rk, send)
+        HK.score_compact(sk, block, qidx_d[0], pos, neg, plans[sk.rank], k * Rk, Rk, send)
         skc = ShardedKGE(name, E, R, d, 9.0, device="cpu", world=W, rank=sk.rank,
                          full_tables=tuple(x.cpu() if torch.is_tensor(x) else x for x in tables))
         plan_c = OK.plan(skc, pos.cpu(), neg.cpu(), mode, K)
         send_o = torch.full((n_send,), -7.0, dtype=torch.float64)
-        OK.score_compact(skc, 0, block.cpu(), qidx_d[0].cpu(), pos.cpu(), neg.cpu(), plan_c, k * Rk, Rk, send_o)
-        OK.score_compact(skc, 1, block.cpu(), qidx_d[-1].cpu(), pos.cpu(), neg.cpu(), plan_c, k * Rk, Rk, send_o)
+        OK.score_compact(skc, block.cpu(), qidx_d[0].cpu(), pos.cpu(), neg.cpu(), plan_c, k * Rk, Rk, send_o)
         diff = (send.cpu().double() - send_o).abs()
         print("chunk", k, "rank", sk.rank, "send", n_send, "max diff", float(diff.max()) if n_send else 0,
               "bad idx", (diff > 1e-4).nonzero().reshape(-1)[:10].tolist())

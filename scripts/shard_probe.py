@@ -1,6 +1,6 @@
 """Rank 0's kernels of the 8-rank row-sharded forward (C4: YAGO3-10 DistMult d=500, N=1024, global batch
 8 x 512) on one GPU, per chunk count: device time of the plan, the query gathers, the compact scoring
-(all, negatives only) and the finish, queued behind a sleep kernel so the events bracket GPU work only.
+(negatives and positives) and the finish, queued behind a sleep kernel so the events bracket GPU work only.
 Run it under `rocprofv3 --kernel-trace --stats` to cross-check the per-kernel durations.
 
     python scripts/shard_probe.py [--chunks 1,2,4] [--reps 20] [--mode 0]
@@ -52,7 +52,7 @@ def main():
     for k in [int(x) for x in a.chunks.split(",")]:
         p = bench.rank0_step_parts(ranks, pos, neg, a.mode, k)
         r = {name: timed(p[key]) for name, key in (("plan", "plan_fn"), ("gather", "gather"), ("score", "score"),
-                                                  ("score_neg", "score_neg"), ("finish", "finish"))}
+                                                  ("finish", "finish"))}
         r["total"] = round(r["plan"] + r["gather"] + r["score"] + r["finish"], 1)
         out[f"chunks{p['chunks']}"] = r
         print(json.dumps({f"chunks{p['chunks']}": r}), flush=True)

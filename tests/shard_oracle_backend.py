@@ -51,7 +51,8 @@ class OracleShardKernels:
         Bg, N = neg_g.shape
         W, cols = sk.world, query_cols(mode, flags)
         nc, hB, Rk = len(cols), Bg // W, Bg // chunks
-        own = cls._owner(sk, torch.cat([neg_g, pos_g[:, positive_col(mode, flags)].view(-1, 1)], 1))
+        cand = torch.cat([neg_g, pos_g[:, positive_col(mode, flags)].view(-1, 1)], 1)
+        own = cls._owner(sk, cand)
         cnt = torch.stack([(own == o).sum(1) for o in range(W)])  # [W, Bg]
         hpre = torch.zeros_like(cnt)
         tot = torch.zeros((W, W), dtype=torch.int64)
@@ -70,32 +71,69 @@ class OracleShardKernels:
                     qslot[c, k * Rk:(k + 1) * Rk][m] = torch.arange(int(m.sum()))
                     qtot[k, c, o] = int(m.sum())
         summ = torch.cat([tot.reshape(-1), qtot.reshape(-1)]).to(torch.int32)
-        return ShardPlan(W, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summ, summ, None, flags)
+        bucket = bstart = None
+        if flags == 0:
+            bucket, bstart = cls.bucket(sk, cand, own, mode)
+        return ShardPlan(W, chunks, mode, Bg, N, cnt, hpre, qown, qslot, summ, summ, None, flags, sk.rank, bucket,
+                         bstart)
+
+    @staticmethod
+    def bucket(sk, cand, own, mode):
+        """Rank sk.rank's bucket (include/kge_hip.h kge_shard_plan): per row its owned negatives (and,
+        tail-batch, positive) as (local row, rank among the row's owned candidates in column order),
+        grouped by XCD slice local_row // ceil(rows / 8) (column order inside a slice here; the kernel's
+        order inside a slice is unspecified); only the entries [g, 0 .. start[g, 8]) are defined."""
+        Bg, N1 = cand.shape
+        rows = sk.hi - sk.lo
+        S = (rows + 7) // 8
+        bucket = torch.full((Bg, N1, 2), -1, dtype=torch.int32)
+        start = torch.zeros((Bg, 9), dtype=torch.int32)
+        for g in range(Bg):
+            mine = (own[g] == sk.rank).nonzero().reshape(-1).tolist()
+            ents = []
+            for r, n in enumerate(mine):
+                if n == N1 - 1 and mode == HEAD_BATCH:
+                    continue  # the head's owner scores a head-batch positive, not from the bucket
+                loc = int(cand[g, n]) - sk.lo
+                ents.append((loc // S, loc, r))
+            ents.sort(key=lambda e: e[0])  # stable: column order inside a slice
+            for i, (_, loc, r) in enumerate(ents):
+                bucket[g, i, 0], bucket[g, i, 1] = loc, r
+            for x in range(9):
+                start[g, x] = sum(1 for e in ents if e[0] < x)
+        return bucket, start
 
     @staticmethod
     def gather_queries(sk, plan, pos_g, k, send, qidx):
-        """send [W, P, d]: this rank's rows [column 0 | column 1] in slot order, once per destination;
-        qidx [ncol, rows]: row index in the received block (owners' pieces in rank order)."""
+        """send: this rank's rows [column 0 | column 1] in slot order, once per destination ([W, P, d] per
+        chunk; k = -1: every chunk's block back to back); qidx [ncol, rows]: row index in the received
+        block (owners' pieces in rank order)."""
         _, qtot = plan.summary()
         cols = query_cols(plan.mode, plan.flags)
-        W, me = sk.world, sk.rank
+        W, me, d = sk.world, sk.rank, sk.entity_dim
         rows = plan.Bg // plan.chunks
-        piece = [int(qtot[k, :, o].sum()) for o in range(W)]
-        for c, col in enumerate(cols):
-            for i in range(rows):
-                g = k * rows + i
-                o, s = int(plan.qown[c, g]), int(plan.qslot[c, g])
-                if o < 0:
-                    qidx[c, i] = -1
-                    continue
-                inner = (int(qtot[k, 0, o]) if c else 0) + s
-                qidx[c, i] = sum(piece[:o]) + inner
-                if o == me:
-                    for d in range(W):
-                        send[d, (int(qtot[k, 0, me]) if c else 0) + s] = sk.shard[int(pos_g[g, col]) - sk.lo]
+        flat = send.reshape(-1)
+        at = 0
+        for kk in (range(plan.chunks) if k < 0 else [k]):
+            piece = [int(qtot[kk, :, o].sum()) for o in range(W)]
+            blk = flat[at:at + W * piece[me] * d].view(W, piece[me], d)
+            at += W * piece[me] * d
+            for c, col in enumerate(cols):
+                for i in range(rows):
+                    g = kk * rows + i
+                    qi = (g if k < 0 else i)
+                    o, s = int(plan.qown[c, g]), int(plan.qslot[c, g])
+                    if o < 0:
+                        qidx[c, qi] = -1
+                        continue
+                    inner = (int(qtot[kk, 0, o]) if c else 0) + s
+                    qidx[c, qi] = sum(piece[:o]) + inner
+                    if o == me:
+                        for dd in range(W):
+                            blk[dd, (int(qtot[kk, 0, me]) if c else 0) + s] = sk.shard[int(pos_g[g, col]) - sk.lo]
 
     @classmethod
-    def score_compact(cls, sk, positives, block, qidx, pos_g, neg_g, plan, row0, rows, send):
+    def score_compact(cls, sk, block, qidx, pos_g, neg_g, plan, row0, rows, send):
         tot, _ = plan.summary()
         hB = plan.Bg // sk.world
         name = NAMES[sk.fn]
@@ -107,21 +145,21 @@ class OracleShardKernels:
             qi = int(qidx[i])
             qrow = (block[qi] if qi >= 0 else zero).double().view(1, 1, -1)
             r = sk.relation_embedding[int(pos_g[g, 1])].double().view(1, 1, -1)
-            if positives:
-                last = off + int(plan.cnt[sk.rank, g]) - 1
-                if mode == HEAD_BATCH and not plan.flags:  # the head's owner; the tail from the block
-                    hr = int(pos_g[g, 0]) - sk.lo
-                    if 0 <= hr < sk.shard.shape[0]:
-                        h = sk.shard[hr].double().view(1, 1, -1)
-                        send[last] = float(O.model_func(name, h, r, qrow, "tail-batch", sk.gamma, sk.emb_range,
-                                                        sk.modulus)[0, 0])
-                    continue
+            last = off + int(plan.cnt[sk.rank, g]) - 1
+            # the positive (the tail formula): head-batch on the head's owner (the tail from the block),
+            # tail-batch on the tail's owner
+            if mode == HEAD_BATCH:
+                hr = int(pos_g[g, 0]) - sk.lo
+                if 0 <= hr < sk.shard.shape[0]:
+                    h = sk.shard[hr].double().view(1, 1, -1)
+                    send[last] = float(O.model_func(name, h, r, qrow, "tail-batch", sk.gamma, sk.emb_range,
+                                                    sk.modulus)[0, 0])
+            else:
                 tr = int(pos_g[g, 2]) - sk.lo
                 if 0 <= tr < sk.shard.shape[0]:
                     t = sk.shard[tr].double().view(1, 1, -1)
                     send[last] = float(O.model_func(name, qrow, r, t, "tail-batch", sk.gamma, sk.emb_range,
                                                     sk.modulus)[0, 0])
-                continue
             k = 0
             for n in range(neg_g.shape[1]):
                 row = int(neg_g[g, n]) - sk.lo

@@ -120,17 +120,22 @@ def test_sharded_exchange_rejects_bad_arguments():
     lib = kge.load()
     d = ctypes.c_void_p(16)
     # chunks must divide the world; world limit; modes
-    assert lib.kge_shard_plan(d, d, 4, 8, 4, 100, 4, 3, 0, 0, d, d, d, d, d, None) == -22
-    assert lib.kge_shard_plan(d, d, 4, 130, 4, 1000, 65, 1, 0, 0, d, d, d, d, d, None) == -95
-    assert lib.kge_shard_plan(d, d, 4, 8, 4, 100, 2, 1, 3, 0, d, d, d, d, d, None) == -22
-    assert lib.kge_shard_plan(d, d, 4, 9, 4, 100, 2, 1, 1, 0, d, d, d, d, d, None) == -22  # Bg % W
-    assert lib.kge_shard_plan(d, d, 4, 0, 4, 100, 2, 1, 1, 0, d, d, d, d, d, None) == 0    # empty
+    assert lib.kge_shard_plan(d, d, 4, 8, 4, 100, 4, 3, 0, 0, 0, d, d, d, d, d, None, None, None) == -22
+    assert lib.kge_shard_plan(d, d, 4, 130, 4, 1000, 65, 1, 0, 0, 0, d, d, d, d, d, None, None, None) == -95
+    assert lib.kge_shard_plan(d, d, 4, 8, 4, 100, 2, 1, 3, 0, 0, d, d, d, d, d, None, None, None) == -22
+    assert lib.kge_shard_plan(d, d, 4, 9, 4, 100, 2, 1, 1, 0, 0, d, d, d, d, d, None, None, None) == -22  # Bg % W
+    assert lib.kge_shard_plan(d, d, 4, 0, 4, 100, 2, 1, 1, 0, 0, d, d, d, d, d, None, None, None) == 0    # empty
+    # the bucket: both arrays or neither, the forward's flags and a valid rank
+    assert lib.kge_shard_plan(d, d, 4, 8, 4, 100, 2, 1, 1, 0, 0, d, d, d, d, d, d, None, None) == -22
+    rc = lib.kge_shard_plan(d, d, 4, 8, 4, 100, 2, 1, 0, 1, 0, d, d, d, d, d, d, d, None)
+    assert rc == -22 and b"bucket" in lib.kge_last_error()
+    assert lib.kge_shard_plan(d, d, 4, 8, 4, 100, 2, 1, 0, 0, 2, d, d, d, d, d, d, d, None) == -22
     # compact scoring: rows must be whole homes; the negative mode, not single
-    rc = lib.kge_score_sharded_compact(1, 1, 0, d, 8, 4, d, d, 2, 4, 0, d, 10, 4, 0, d, d, 4, 3, 4, 4, 1.0, 1.0, 0.0,
-                                       d, d, d, 2, 0, 2, 0, d, None)
+    rc = lib.kge_shard_score(1, 1, d, 8, 4, d, d, 2, 4, 0, d, 10, 4, 0, d, 3, 4, 4, 1.0, 1.0, 0.0,
+                             d, d, d, d, d, 2, 0, 2, 0, d, None)
     assert rc == -22 and b"whole homes" in lib.kge_last_error()
-    rc = lib.kge_score_sharded_compact(1, 3, 1, d, 8, 4, d, d, 2, 4, 0, d, 10, 4, 0, d, d, 4, 4, 4, 4, 1.0, 1.0, 0.0,
-                                       d, d, d, 2, 0, 2, 0, d, None)
+    rc = lib.kge_shard_score(1, 3, d, 8, 4, d, d, 2, 4, 0, d, 10, 4, 0, d, 4, 4, 4, 1.0, 1.0, 0.0,
+                             d, d, d, d, d, 2, 0, 2, 0, d, None)
     assert rc == -22 and b"mode" in lib.kge_last_error()
     assert lib.kge_shard_finish(d, d, d, d, d, 4, 8, 4, 100, 2, 2, 0, 1.0, 1, d, 4, d, d, d, None) == -22
     assert lib.kge_shard_gather_queries(d, 10, 4, 0, d, 8, 3, 0, 4, 2, 0, 0, 0, d, d, d, d, d, None) == -22

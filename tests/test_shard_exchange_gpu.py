@@ -1,5 +1,5 @@
 """GPU tests of the row-sharded forward's O(information) exchange (kge_shard_plan,
-kge_shard_gather_queries, kge_score_sharded_compact, kge_shard_finish; distributed.ShardedKGE.step_forward):
+kge_shard_gather_queries, kge_shard_score, kge_shard_finish; distributed.ShardedKGE.step_forward):
 W ranks simulated as threads of one process on one device (ThreadComm: the same all-to-all calls
 TorchComm makes over RCCL). Every score has one owner and moves once, so each home rank's scores
 must equal the unsharded kernel's bitwise, and its reductions kge_step_forward's."""
@@ -46,20 +46,35 @@ def _ranks(m, W, comm=None):
 @pytest.mark.parametrize("W,K", [(1, 1), (2, 1), (2, 2), (3, 3), (8, 4), (8, 2)])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("flags", [0, 1])
-def test_plan_matches_restatement(W, K, mode, flags):
+@pytest.mark.parametrize("N", [70, 300])
+def test_plan_matches_restatement(W, K, mode, flags, N):
     """kge_shard_plan's counts, prefixes, query owners / slots and summary equal the CPU restatement (the
-    forward's one query column with the head-batch positive on the head's owner, and the train step's two)."""
-    E, R, Bh, N = 301, 7, 5, 70
+    forward's one query column with the head-batch positive on the head's owner, and the train step's two),
+    and so does the forward plan's bucket of the first and the last rank (owned candidates grouped by XCD
+    slice; the order inside a slice is the LDS atomics' and not specified)."""
+    E, R, Bh = 301, 7, 5
     m = _model("DistMult", E, R, 8)
     pos, neg = _batch(E, R, W * Bh, N, seed=W + 10 * K, bad=True)
-    sk = _ranks(m, W)[0]
-    got = sk.kernels.plan(sk, pos, neg, mode, K, flags)
-    want = OracleShardKernels.plan(sk, pos.cpu(), neg.cpu(), mode, K, flags)
-    for a in ("cnt", "hpre", "qown", "qslot"):
-        assert torch.equal(getattr(got, a).cpu().long(), getattr(want, a).long()), a
-    gt, gq = got.summary()
-    wt, wq = want.summary()
-    assert np.array_equal(gt, wt) and np.array_equal(gq, wq)
+    ranks = _ranks(m, W)
+    for sk in {0: ranks[0], W - 1: ranks[-1]}.values():
+        got = sk.kernels.plan(sk, pos, neg, mode, K, flags)
+        want = OracleShardKernels.plan(sk, pos.cpu(), neg.cpu(), mode, K, flags)
+        for a in ("cnt", "hpre", "qown", "qslot"):
+            assert torch.equal(getattr(got, a).cpu().long(), getattr(want, a).long()), a
+        gt, gq = got.summary()
+        wt, wq = want.summary()
+        assert np.array_equal(gt, wt) and np.array_equal(gq, wq)
+        if flags:
+            assert got.bucket is None
+            continue
+        start = got.bucket_start.cpu()
+        assert torch.equal(start, want.bucket_start), sk.rank
+        gb = got.bucket.cpu()
+        for g in range(W * Bh):  # a slice's entries in any order (each carries its rank)
+            for x in range(8):
+                lo, hi = int(start[g, x]), int(start[g, x + 1])
+                key = lambda e: sorted(map(tuple, e.tolist()))  # noqa: E731
+                assert key(gb[g, lo:hi]) == key(want.bucket[g, lo:hi]), (sk.rank, g, x)
 
 
 def _check_world(name, W, K, E, R, d, Bh, N, seed, bad=False):
@@ -87,14 +102,15 @@ def _check_world(name, W, K, E, R, d, Bh, N, seed, bad=False):
 @pytest.mark.parametrize("name", list(CFG))
 @pytest.mark.parametrize("W,K", [(1, 1), (2, 2), (4, 2)])
 def test_sharded_forward_bitwise_every_function(name, W, K):
-    """N < 128: the batch-row-major compact path (one wave walks a whole row)."""
+    """N < 128 (a slice's run well under one 64-lane run)."""
     _check_world(name, W, K, E=997, R=6, d=40, Bh=6, N=37, seed=1)
 
 
 @pytest.mark.parametrize("name", ["InterHT", "DistMult", "RotatE"])
 @pytest.mark.parametrize("W,K", [(2, 1), (4, 4), (8, 4)])
 def test_sharded_forward_bitwise_xcd_order(name, W, K):
-    """N >= 128: the XCD-sliced compact scorer (compact ranks carried through the per-slice id sort)."""
+    """N >= 128: the unsharded reference is the XCD-sliced kernel (compact ranks carried through the
+    bucket scorer's per-run row sort)."""
     _check_world(name, W, K, E=5003, R=5, d=64, Bh=8, N=300, seed=2)
 
 
@@ -104,7 +120,8 @@ def test_sharded_forward_ids_without_owner():
 
 
 def test_sharded_forward_plan_made_ahead_and_reused():
-    """A plan made one step ahead (the bench's pipelining) gives the same results as an inline one."""
+    """A plan made one step ahead (the bench's pipelining), also on a side stream, gives the same results
+    as an inline one."""
     E, R, d, W, Bh, N = 3001, 5, 32, 4, 8, 200
     m = _model("DistMult", E, R, d)
     pos, neg = _batch(E, R, W * Bh, N, seed=5)
@@ -112,9 +129,12 @@ def test_sharded_forward_plan_made_ahead_and_reused():
     plans = [sk.plan(pos, neg, 1) for sk in ranks]
     a = run_threads([lambda sk=sk, p=p: sk.step_forward(pos, neg, 1, plan=p) for sk, p in zip(ranks, plans)])
     b = run_threads([lambda sk=sk: sk.step_forward(pos, neg, 1) for sk in ranks])
-    for x, y in zip(a, b):
-        for u, v in zip(x, y):
-            assert torch.equal(u, v)
+    side = torch.cuda.Stream()  # plans made on a side stream, waited for by the step's stream
+    plans = [sk.plan(pos, neg, 1, stream=side) for sk in ranks]
+    c = run_threads([lambda sk=sk, p=p: sk.step_forward(pos, neg, 1, plan=p) for sk, p in zip(ranks, plans)])
+    for x, y, z in zip(a, b, c):
+        for u, v, t in zip(x, y, z):
+            assert torch.equal(u, v) and torch.equal(u, t)
 
 
 def test_collective_bytes_are_payload_only():

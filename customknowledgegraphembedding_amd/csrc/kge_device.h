@@ -377,7 +377,40 @@ template <int FN, bool CH, int V, int G, class Q>
 __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Q& q, const ScoreParams& p,
                                             float2* stats = nullptr, vecf<V>* nsg = nullptr) {
     float acc = 0.f;
-    if constexpr (FN == KGE_INTERHT) {
+    if constexpr (FN == KGE_INTERHT && V % 2 == 0) {
+        // on packed fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32: two elements per instruction): the fused
+        // train forward is VALU-bound and this is most of its per-candidate work
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 sa2 = {0.f, 0.f}, sb2 = {0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int i = 0; i < V; i += 2) {
+                const f2 a{c.ca[k].a[i], c.ca[k].a[i + 1]}, bb{c.cb[k].a[i], c.cb[k].a[i + 1]};
+                sa2 = a * a + sa2;
+                sb2 = bb * bb + sb2;
+            }
+        const float ia = rsqrt_f(wave_sum(sa2.x + sa2.y)), ib = rsqrt_f(wave_sum(sb2.x + sb2.y));
+        if (stats) *stats = make_float2(ia, ib);  // kept for the streaming phase-1 backward
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const vecf<V> q0 = q.q0[k], q1 = q.q1[k], q2 = q.q2[k];
+#pragma unroll
+            for (int i = 0; i < V; i += 2) {
+                const f2 ah = f2{c.ca[k].a[i], c.ca[k].a[i + 1]} * ia;        // normalised candidate a-half
+                const f2 bh = f2{c.cb[k].a[i], c.cb[k].a[i + 1]} * ib + 1.f;  // normalised b-half + u
+                const f2 Q0{q0.a[i], q0.a[i + 1]}, Q1{q1.a[i], q1.a[i + 1]}, Q2{q2.a[i], q2.a[i + 1]};
+                // head: a_head * b_tail - a_tail * b_head + re_mid; tail: the other way round (model.py:222)
+                const f2 x = CH ? (ah * Q1 - Q0 * bh + Q2) : (Q0 * bh - ah * Q1 + Q2);
+                acc += fabsf(x.x);
+                acc += fabsf(x.y);
+                if (nsg) {  // the Jacobian's sign (0 past D: x = 0 there)
+                    nsg[k].a[i] = -sgnf(x.x);
+                    nsg[k].a[i + 1] = -sgnf(x.y);
+                }
+            }
+        }
+    } else if constexpr (FN == KGE_INTERHT) {
         float sa = 0.f, sb = 0.f;
 #pragma unroll
         for (int k = 0; k < G; ++k)

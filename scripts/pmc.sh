@@ -13,7 +13,7 @@ for CTRS in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_
   i=$((i+1))
   echo "== pass $i: $CTRS"
   timeout -k 10 300 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d "$R/gpurun_out/pmc/$W/p$i" -o run -- \
-      python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --workload "$W" > "$R/gpurun_out/pmc/$W/p$i.log" 2>&1
+      python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --sharded-steps 0 --train-steps 5 --workload "$W" > "$R/gpurun_out/pmc/$W/p$i.log" 2>&1
   rc=$?
   echo "rc=$rc"
   if [ $rc -ge 124 ]; then echo "fatal rc=$rc: stopping"; exit $rc; fi

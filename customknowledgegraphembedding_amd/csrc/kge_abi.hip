@@ -467,6 +467,7 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
     } else if (kind == KIND_STEP_FWD_XCD || kind == KIND_SCORE_SHARD_XCD || kind == KIND_SHARD_BUCKET) {
         waves = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock * 8;  // 8 slice blocks per 4 rows
+        if (kind == KIND_STEP_FWD_XCD && p.xcd_phases > 1) waves *= p.xcd_phases;
     } else if (kind == KIND_BWD_CHAIN || kind == KIND_SHARD_POS) {
         waves = p.B;  // one wave per slot
     } else if (kind == KIND_STEP_EPILOGUE) {
@@ -577,6 +578,21 @@ void fill_dense(ScoreParams& p, int fn, int mode, const float* head, int64_t hea
 
 bool empty(int64_t B, int64_t N) { return B == 0 || N == 0; }
 
+// phases of kge_step_forward's XCD-sliced order (step_fwd_xcd_kernel): KGE_XCD_PHASES overrides (A/B runs)
+int xcd_phases(int64_t nentity, int64_t ent_ld) {
+    static const int forced = [] {
+        const char* s = getenv("KGE_XCD_PHASES");
+        return s ? atoi(s) : 0;
+    }();
+    if (forced > 0) return std::min(forced, 16);
+    // a table larger than the 256 MB Infinity Cache is swept in phases of ~96 MB (C2's 327.5 MB: 4 phases,
+    // 139 -> 128.5 us); a table that fits gains nothing and pays the extra id walks (C3's 116 MB at 4
+    // phases: 144 -> 162 us)
+    const int64_t bytes = nentity * ent_ld * 4, mall = (int64_t)256 << 20, phase = (int64_t)96 << 20;
+    if (bytes <= mall) return 1;
+    return (int)std::min<int64_t>((bytes + phase - 1) / phase, 8);
+}
+
 // kge_step_forward's candidate order: XCD-sliced ascending ids (KIND_STEP_FWD_XCD) or batch-row-major
 // (KIND_STEP_FWD). KGE_STEP_ORDER=xcd|row overrides the choice (A/B runs).
 bool use_xcd_order(int64_t nentity, int64_t N) {
@@ -684,6 +700,7 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
     if (!(cand_stats && fn == KGE_INTERHT) && use_xcd_order(nentity, N)) {
         // two launches: the negatives (and the positives) in XCD-sliced ascending-id order, then the rows'
         // self-adversarial reductions
+        p.xcd_phases = xcd_phases(nentity, ent_ld);
         rc = run_score(fn, mode, p, KIND_STEP_FWD_XCD, stream);
         if (rc) return rc;
         const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;

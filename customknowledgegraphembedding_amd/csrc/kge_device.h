@@ -753,16 +753,24 @@ __device__ __forceinline__ void for_slice_runs_sorted(const ScoreParams& p, int6
 // One candidate row in registers at a time (score_lanes<DEPTH = 1>) and 4 waves per SIMD up to D = 1024:
 // every wave of a C2-sized launch (8 x 512) is resident at once, so the XCDs' sweeps stay together
 // (2-deep pipelining at 3 waves per SIMD measured 140 us against 133 us for this form at C2).
+// Phases (p.xcd_phases = P > 1): the table is cut into 8 P slices and the grid into P consecutive runs of
+// blocks, run f taking slices 8 f .. 8 f + 7: blocks are dispatched in order, so the chip sweeps 1/P of
+// the table at a time and the repeat gathers of a phase hit a working set P times smaller (the Infinity
+// Cache's 256 MB against a C2 table of 327.5 MB). Every candidate is still scored by the same code.
 template <int FN, bool CH, int V, int G>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(G <= 4 ? 4 : 1))) void
 step_fwd_xcd_kernel(ScoreParams p) {
     __shared__ vecf<V> q2img[kWavesPerBlock][FN == KGE_INTERHT ? G * kWave : 1];
-    const int x = blockIdx.x & 7;
+    const int P = p.xcd_phases > 1 ? p.xcd_phases : 1;
+    const int64_t per_phase = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * 8;  // blocks of one phase
+    const int phase = (int)(blockIdx.x / per_phase);
+    const int64_t bi = blockIdx.x - phase * per_phase;
+    const int x = (int)(bi & 7) + 8 * phase;  // slice
     const int w = threadIdx.x >> 6;
-    const int64_t b = (int64_t)(blockIdx.x >> 3) * kWavesPerBlock + w;
+    const int64_t b = (bi >> 3) * kWavesPerBlock + w;
     if (b >= p.B) return;
     const int lane = threadIdx.x & 63;
-    const int64_t S = (p.c_rows + 7) / 8;
+    const int64_t S = (p.c_rows + 8 * P - 1) / (8 * P);
     const int64_t e_lo = min((int64_t)x * S, p.c_rows), e_hi = min(p.c_rows, e_lo + S);
     const int64_t t = p.pos_base[b * 3 + 2];
     const bool t_here = (t >= 0 && t < p.c_rows) ? (t >= e_lo && t < e_hi) : x == 0;

@@ -68,6 +68,7 @@ struct ScoreParams {
     const int2* bk_ent;   // [B, bk_ld] kge_shard_plan's bucket: (local row, rank k) per owned candidate
     const int* bk_start;  // [B, 9] the bucket's XCD-slice starts per row
     int64_t bk_ld;
+    int xcd_phases;       // step_fwd_xcd_kernel: the table's 8 slices cut again into this many phases (1: none)
     float* out;
     int64_t out_ld;
     int64_t B, N;

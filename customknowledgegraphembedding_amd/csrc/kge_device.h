@@ -91,6 +91,12 @@ constexpr int kAuxNT = 2, kAuxSC1 = 16;
 #ifndef KGE_FG_KEEPSGN
 #define KGE_FG_KEEPSGN 1
 #endif
+// step_fwd_grad_kernel's query pass: gradient weights on the hardware exp / log / rcp, InterHT's Jacobian
+// sums on packed fp32 pairs with the sign recomputed and RotatE's on the hardware rsq (KGE_FG_FAST = 1),
+// or the libm-accurate weights and scalar sums with the score pass's kept signs (0, the round-2 form)
+#ifndef KGE_FG_FAST
+#define KGE_FG_FAST 1
+#endif
 
 template <int V, int AUX = 0>
 __device__ __forceinline__ vecf<V> bload(rsrc_t r, uint32_t off) {
@@ -248,6 +254,9 @@ constexpr bool rel_split(int fn) { return fn == KGE_COMPLEX; }
 //   q0,q1,q2: per-element query operands kept in VGPRs; zero on groups past D.
 //   na_inv,nb_inv: InterHT query reciprocal norms (1/||a||, 1/||b||; no epsilon, Q7)
 // ---------------------------------------------------------------------------------------------
+#ifndef KGE_ROT_CHUNK
+#define KGE_ROT_CHUNK 4  // RotatE query build: cos / sin of this many elements per iteration of a rolled loop
+#endif
 template <int FN, bool CH, int V, int G>
 struct Query {
     vecf<V> q0[G], q1[G], q2[G];
@@ -293,6 +302,35 @@ struct Query {
             na_inv = rsqrt_f(wave_sum(sa));
             nb_inv = rsqrt_f(wave_sum(sb));
         }
+        // RotatE: the relation phases' cos / sin one element at a time (a rolled loop picking the element
+        // with wave-uniform selects): libm's cosf / sinf carry their large-argument reduction state, and
+        // G V of them interleaved made the XCD-sliced kernels spill (98 VGPRs at D = 1000)
+        float rc[G][V], rs[G][V];
+        if constexpr (FN == KGE_ROTATE) {
+            constexpr int RU = KGE_ROT_CHUNK < G * V ? KGE_ROT_CHUNK : G * V;  // elements per iteration
+#pragma unroll 1
+            for (int e0 = 0; e0 < G * V; e0 += RU) {
+#pragma unroll
+                for (int u = 0; u < RU; ++u) {
+                    float r = 0.f;
+#pragma unroll
+                    for (int k = 0; k < G; ++k)
+#pragma unroll
+                        for (int i = 0; i < V; ++i)
+                            if (k * V + i == e0 + u) r = ra[k].a[i];
+                    const float ph = r / p.phase_div;
+                    const float c = cosf(ph), sn = sinf(ph);
+#pragma unroll
+                    for (int k = 0; k < G; ++k)
+#pragma unroll
+                        for (int i = 0; i < V; ++i)
+                            if (k * V + i == e0 + u) {
+                                rc[k][i] = c;
+                                rs[k][i] = sn;
+                            }
+                }
+            }
+        }
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             const bool in = (lane + k * kWave) < DV;
@@ -316,8 +354,7 @@ struct Query {
                         o1 = r * y - s * x;
                     }
                 } else if constexpr (FN == KGE_ROTATE) {
-                    const float ph = r / p.phase_div;
-                    const float c = cosf(ph), sn = sinf(ph);
+                    const float c = rc[k][i], sn = rs[k][i];
                     if (!CH) {  // re_h*re_r - im_h*im_r ; re_h*im_r + im_h*re_r
                         o0 = x * c - y * sn;
                         o1 = x * sn + y * c;
@@ -781,6 +818,7 @@ step_fwd_xcd_kernel(ScoreParams p) {
     auto run = [&](const auto& qq) {
         for_slice_runs_sorted(p, b, e_lo, e_hi, x == 0, false, lane, [&](int id, int n, int cnt) {
             float2 st;
+            // one row in flight: two (C4, DistMult d = 500, 59 VGPRs) measured 128.5-129 us against 124-126 us
             const float s = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, 1>(p, qq, (int64_t)id, cnt, lane, st);
             if (lane < cnt) p.out[b * p.out_ld + n] = s;
         });
@@ -1222,9 +1260,18 @@ __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, 
             j1 = cb.a[i];
         } else if constexpr (FN == KGE_ROTATE) {
             const float xr = q0.a[i] - x, xi = q1.a[i] - cb.a[i];
+#if KGE_FG_FAST
+            // d|x|/dx = x / |x| on the hardware reciprocal square root (one instruction for both
+            // components instead of a square root and two IEEE divisions; 0 at x = 0 as before)
+            const float s2 = xr * xr + xi * xi;
+            const float im = s2 > 0.f ? __builtin_amdgcn_rsqf(s2) : 0.f;
+            j0 = -(xr * im);
+            j1 = -(xi * im);
+#else
             const float m = sqrtf(xr * xr + xi * xi);
             j0 = -((m > 0.f) ? xr / m : 0.f);
             j1 = -((m > 0.f) ? xi / m : 0.f);
+#endif
         }
         a0.a[i] += wa * j0;
         a1.a[i] += wa * j1;
@@ -1237,12 +1284,6 @@ __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, 
     }
 }
 
-// step_fwd_grad_kernel's query pass: gradient weights on the hardware exp / log / rcp and InterHT's Jacobian
-// sums on packed fp32 pairs with the sign recomputed (KGE_FG_FAST = 1), or the libm-accurate weights and
-// scalar sums with the score pass's kept signs (0, the round-2 form)
-#ifndef KGE_FG_FAST
-#define KGE_FG_FAST 1
-#endif
 #if KGE_FG_FAST
 #undef KGE_FG_KEEPSGN
 #define KGE_FG_KEEPSGN 0

@@ -580,10 +580,8 @@ bool empty(int64_t B, int64_t N) { return B == 0 || N == 0; }
 
 // phases of kge_step_forward's XCD-sliced order (step_fwd_xcd_kernel): KGE_XCD_PHASES overrides (A/B runs)
 int xcd_phases(int64_t nentity, int64_t ent_ld) {
-    static const int forced = [] {
-        const char* s = getenv("KGE_XCD_PHASES");
-        return s ? atoi(s) : 0;
-    }();
+    const char* env = getenv("KGE_XCD_PHASES");  // read per call: tests switch it inside one process
+    const int forced = env ? atoi(env) : 0;
     if (forced > 0) return std::min(forced, 16);
     // a table larger than the 256 MB Infinity Cache is swept in phases of ~96 MB (C2's 327.5 MB: 4 phases,
     // 139 -> 128.5 us); a table that fits gains nothing and pays the extra id walks (C3's 116 MB at 4

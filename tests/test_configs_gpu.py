@@ -65,6 +65,37 @@ def test_c2_wn18rr_interht_full_size_real_positives():
     _step_forward_vs_oracle("InterHT", 40943, 11, 1000, 24.0, True, False, True, "wn18rr", 512, 256)
 
 
+def test_c2_xcd_phases_bitwise():
+    """The XCD-sliced step swept in phases (the C2 table exceeds the Infinity Cache: 4 phases by default)
+    scores every candidate with the same code: outputs bitwise equal for 1, 2, 3, 4 and 8 phases, and equal
+    to the plain scorer's scores."""
+    name, E, R, d = "InterHT", 40943, 11, 1000
+    m = kge.TFKGEModel(name, E, R, d, 24.0, double_entity_embedding=True, triple_relation_embedding=True,
+                       device=DEV, seed=0)
+    pos, neg = _batch("wn18rr", E, 512, 256, seed=2)
+    pos, neg = pos.to(DEV), neg.to(DEV)
+    ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
+    fn = FN_IDS[name]
+    old = os.environ.get("KGE_XCD_PHASES")
+    try:
+        for mode in (0, 1):
+            outs = []
+            for ph in ("1", "2", "3", "4", "8"):
+                os.environ["KGE_XCD_PHASES"] = ph
+                outs.append(ops.step_forward_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f,
+                                                 m._range_f)[:3])
+            want_s = ops.score_indexed_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
+            torch.cuda.synchronize()
+            for o in outs:
+                assert all(torch.equal(x, y) for x, y in zip(o, outs[0])), mode
+            assert torch.equal(outs[0][2], want_s), mode
+    finally:
+        if old is None:
+            os.environ.pop("KGE_XCD_PHASES", None)
+        else:
+            os.environ["KGE_XCD_PHASES"] = old
+
+
 def test_c3_fb15k237_rotate_full_size():
     """C3: FB15k-237 RotatE d=1000 -de, E=14541, R=237, B=512, N=256 (valid+test positives)."""
     _step_forward_vs_oracle("RotatE", 14541, 237, 1000, 9.0, True, False, False, "fb15k237", 512, 256)

@@ -96,7 +96,8 @@ def pmc_traffic(workload, kernel_prefixes):
     this workload (profiles/pmc_<workload>.json, scripts/pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x 2
     + WRITE_SIZE, the gfx950 corrections). (None, reason) when no summary was committed, or when it was
     measured on a library built from other sources than the one loaded now (kge_source_hash: stale)."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    # KGE_PMC_DIR: summaries made in this same session (scripts/gpu_r03_final.sh) before they are committed
+    path = os.path.join(os.environ.get("KGE_PMC_DIR") or os.path.join(ROOT, "profiles"), f"pmc_{workload}.json")
     try:
         with open(path) as f:
             summ = json.load(f)

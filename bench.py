@@ -534,7 +534,7 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                          "kernel_avg_us": gemm_s * 1e6,
                          "fp32_equivalent_tflops": flops / gemm_s / 1e12,
                          "fp32_equivalent_over_fp32_mfma_peak": flops / gemm_s / 1e12 / 157.3},
-            "filtered_metrics": met}
+            "filtered_metrics": met, "build": kge.build_id()}
 
 
 def transparse_bench(w, a, device):
@@ -608,15 +608,18 @@ def transparse_bench(w, a, device):
             "config": {"workload": w["name"], "global_batch": B, "n_neg": N, "d": d},
             "roofline": ({"bound": "mfma", "achieved": mfma_flops / k_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                           "frac": mfma_flops / k_s / 1e12 / 2500.0, "traffic": None,
-                          "kernel": "ts_rows_kernel<TS_FWD, 4, true> (bf16x3 split in registers, six products on "
-                                    "v_mfma_f32_32x32x16_bf16, fp32 accumulation)",
+                          "kernel": ("ts_fwd_x3_kernel (256 negatives of one batch row per block, M_r chunks staged "
+                                     "once for all of them; bf16x3 split in registers, six products on "
+                                     "v_mfma_f32_32x32x16_bf16, fp32 accumulation)"
+                                     if os.environ.get("KGE_TS_BIG", "1") != "0" else
+                                     "ts_rows_kernel<TS_FWD, 4, true> (128-row blocks, bf16x3 on the bf16 MFMA)"),
                           "kernel_avg_us": k_s * 1e6, "fp32_equivalent_tflops": flops / k_s / 1e12,
                           "fp32_equivalent_over_fp32_mfma_peak": flops / k_s / 1e12 / 157.3}
                          if x3 else
                          {"bound": "mfma", "achieved": flops / k_s / 1e12, "peak": 157.3, "unit": "TFLOP/s",
                           "frac": flops / k_s / 1e12 / 157.3, "traffic": None,
                           "kernel": "ts_rows_kernel<TS_FWD> (v_mfma_f32_32x32x2_f32)", "kernel_avg_us": k_s * 1e6}),
-            "train_step": train}
+            "train_step": train, "build": kge.build_id()}
 
 
 def train_step_bench(m, batches, steps, warmup):

@@ -465,6 +465,11 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     } else if (kind == KIND_BWD_ROWS || kind == KIND_BWD_STREAM || kind == KIND_STEP_FWD ||
                kind == KIND_STEP_FWD_STATS || kind == KIND_STEP_FWD_GRAD || kind == KIND_SHARD_FWD_GRAD) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
+    } else if (kind == KIND_STEP_FWD_TILE || kind == KIND_SCORE_TILE) {
+        if (p.tile_rows < 1 || p.tile_lds > kTileLdsMax) return fail(KGE_EINVAL, "tile plan missing");
+        // one block of kTileWaves waves per (group of tile_rows batch rows, entity slice): run_score's
+        // block count is waves / kWavesPerBlock
+        waves = (p.B + p.tile_rows - 1) / p.tile_rows * 8 * kWavesPerBlock;
     } else if (kind == KIND_STEP_FWD_XCD || kind == KIND_SCORE_SHARD_XCD || kind == KIND_SHARD_BUCKET) {
         waves = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock * 8;  // 8 slice blocks per 4 rows
         if (kind == KIND_STEP_FWD_XCD && p.xcd_phases > 1) waves *= p.xcd_phases;
@@ -591,17 +596,34 @@ int xcd_phases(int64_t nentity, int64_t ent_ld) {
     return (int)std::min<int64_t>((bytes + phase - 1) / phase, 8);
 }
 
-// kge_step_forward's candidate order: XCD-sliced ascending ids (KIND_STEP_FWD_XCD) or batch-row-major
-// (KIND_STEP_FWD). KGE_STEP_ORDER=xcd|row overrides the choice (A/B runs).
-bool use_xcd_order(int64_t nentity, int64_t N) {
-    static const int forced = [] {
-        const char* s = getenv("KGE_STEP_ORDER");
-        if (!s) return -1;
-        return strcmp(s, "xcd") == 0 ? 1 : (strcmp(s, "row") == 0 ? 0 : -1);
-    }();
-    if (nentity >= (int64_t)8 << 25) return false;  // sort keys hold (id - slice start) << 6
-    if (forced >= 0) return forced == 1;
-    return N >= 128;
+// kge_step_forward's candidate order: 0 batch-row-major (KIND_STEP_FWD), 1 XCD-sliced ascending ids per wave
+// (KIND_STEP_FWD_XCD), 2 row-group x XCD-slice tiles (KIND_STEP_FWD_TILE, when its LDS plan fits).
+// KGE_STEP_ORDER=row|xcd|tile overrides the choice (A/B runs; read per call: tests switch it in one process).
+int step_order(int64_t nentity, int64_t N) {
+    const char* s = getenv("KGE_STEP_ORDER");
+    const int forced =
+        !s ? -1 : (strcmp(s, "tile") == 0 ? 2 : (strcmp(s, "xcd") == 0 ? 1 : (strcmp(s, "row") == 0 ? 0 : -1)));
+    if (nentity >= (int64_t)8 << 25) return 0;  // sort keys hold (id - slice start) << 6
+    if (forced >= 0) return forced;
+    return N >= 128 ? 2 : 0;
+}
+bool use_xcd_order(int64_t nentity, int64_t N) { return step_order(nentity, N) != 0; }
+
+// Rows per block of the tile kernel (step_fwd_tile_kernel) and its dynamic LDS: 0 when the plan does not fit
+// (then the XCD-sliced form runs). KGE_TILE_ROWS caps the row count (A/B runs).
+int tile_plan(int fn, ScoreParams& p) {
+    int V = 1, G = 1;
+    if (pick_vg(p, V, G)) return 0;
+    if (G > kFwdGradMaxG || p.N + 1 > 65536 || p.c_rows <= 0) return 0;
+    const int64_t qrow = (int64_t)tile_nq(fn) * G * kWave * V * 4 + 8, lrow = (p.N + 1) * 4;
+    const int64_t fixed = kTileBuckets * 4 + 16;
+    int64_t R = std::min<int64_t>(kTileMaxRows, (kTileLdsMax - fixed) / (qrow + lrow));
+    const char* env = getenv("KGE_TILE_ROWS");
+    if (env && atoi(env) > 0) R = std::min<int64_t>(R, atoi(env));
+    if (R < 1) return 0;
+    p.tile_rows = (int)R;
+    p.tile_lds = (int)(R * (qrow + lrow) + fixed);
+    return 1;
 }
 
 }  // namespace
@@ -625,7 +647,7 @@ int64_t kge_max_dim(int fn) {
     return (int64_t)kMaxG * kWave * 4;
 }
 
-int kge_step_forward_order(int64_t nentity, int64_t N) { return use_xcd_order(nentity, N) ? 1 : 0; }
+int kge_step_forward_order(int64_t nentity, int64_t N) { return step_order(nentity, N); }
 
 int kge_score_indexed(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
                       int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
@@ -695,11 +717,17 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
     p.out_neg = out_neg;
     p.out_pos_raw = pos_scores;
     p.out_pos_ls = out_pos;
-    if (!(cand_stats && fn == KGE_INTERHT) && use_xcd_order(nentity, N)) {
-        // two launches: the negatives (and the positives) in XCD-sliced ascending-id order, then the rows'
-        // self-adversarial reductions
-        p.xcd_phases = xcd_phases(nentity, ent_ld);
-        rc = run_score(fn, mode, p, KIND_STEP_FWD_XCD, stream);
+    const int order = step_order(nentity, N);
+    if (!(cand_stats && fn == KGE_INTERHT) && order != 0) {
+        // two launches: the negatives (and the positives) in row-group x XCD-slice tiles or in XCD-sliced
+        // ascending-id order, then the rows' self-adversarial reductions
+        if (order == 2 && tile_plan(fn, p)) {
+            p.tile_pos = 1;
+            rc = run_score(fn, mode, p, KIND_STEP_FWD_TILE, stream);
+        } else {
+            p.xcd_phases = xcd_phases(nentity, ent_ld);
+            rc = run_score(fn, mode, p, KIND_STEP_FWD_XCD, stream);
+        }
         if (rc) return rc;
         const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
         hipLaunchKernelGGL(neg_rows_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, p);

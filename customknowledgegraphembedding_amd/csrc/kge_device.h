@@ -873,6 +873,203 @@ step_fwd_xcd_kernel(ScoreParams p) {
 }
 
 
+// ---------------------------------------------------------------------------------------------
+// Row-group tiles (kge_step_forward KIND_STEP_FWD_TILE, kge_score_indexed KIND_SCORE_TILE). Block i takes
+// entity slice x = i % 8 of the table (S = ceil(c_rows / 8) rows; blocks i and i + 8 share an XCD) and the
+// R = p.tile_rows batch rows [g R, g R + R), g = i / 8:
+//   1. the R rows' query operands are built once into LDS (InterHT's third operand, the relation's middle
+//      third, stays in the relation table: it is re-read per candidate from L2);
+//   2. the rows' candidates that fall in slice x (slice 0 also takes the out-of-range ids, which score
+//      against a zero row), plus, with tile_pos, each row's positive whose tail falls there, are counting-
+//      sorted into kTileBuckets entity buckets in LDS (order inside a bucket: arbitrary);
+//   3. the block's kTileWaves waves take the sorted list round-robin, one candidate row in registers each.
+// The block sweeps its slice in ONE ascending front, and the ~32 blocks of an XCD sweep the same slice
+// together, so the ~3.4 gathers of an entity row (C2) are issued by one XCD close in time and the repeats
+// hit its L2. Against step_fwd_xcd_kernel (one wave per (row, slice, phase), which rebuilds its row's query
+// and walks its row's ids once per phase) a row's query is built 8 times per launch, not 8 P times.
+// Every candidate is scored by cand_score with the same operand values as every other form: the scores
+// are bitwise those of step_fwd_kernel / step_fwd_xcd_kernel.
+// LDS (dynamic, p.tile_lds bytes): query images [R][tile_nq][G * 64] vecf<V>, relation rows [R] (int64),
+// bucket counts / cursors [kTileBuckets], the item count, the sorted list [R (N + 1)] of (row << 16 | column)
+// (column N: the row's positive).
+// ---------------------------------------------------------------------------------------------
+template <int V, int G>
+struct TileQueryIH {  // InterHT: q0, q1 from LDS, the relation third in registers
+    LdsOperand<V> q0, q1;
+    vecf<V> q2[G];
+};
+
+template <int FN, bool CH, int V, int G>
+__global__ __launch_bounds__(kTileWaves * kWave) void step_fwd_tile_kernel(ScoreParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char tile_smem[];
+    constexpr int NQ = tile_nq(FN);
+    constexpr int W = G * kWave;
+    constexpr int NT = kTileWaves * kWave;
+    const int R = p.tile_rows;
+    vecf<V>* qimg = reinterpret_cast<vecf<V>*>(tile_smem);  // [R][NQ][W]
+    int64_t* rrow = reinterpret_cast<int64_t*>(qimg + (size_t)R * NQ * W);
+    int* hist = reinterpret_cast<int*>(rrow + R);
+    int* cntp = hist + kTileBuckets;
+    int* list = cntp + 4;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int x = (int)(blockIdx.x & 7);
+    const int64_t b0 = (int64_t)(blockIdx.x >> 3) * R;
+    const int nr = (int)min<int64_t>(R, p.B - b0);
+    if (nr <= 0) return;  // block-uniform
+    const int64_t S = (p.c_rows + 7) / 8;
+    const int64_t e_lo = min((int64_t)x * S, p.c_rows), e_hi = min(p.c_rows, e_lo + S);
+    const int64_t Np = p.tile_pos ? p.N + 1 : p.N;  // column N: the row's positive (its tail)
+
+    // 1. the rows' query operands
+    for (int r = w; r < nr; r += kTileWaves) {
+        Query<FN, CH, V, G> q;
+        int64_t qi, ri;
+        bool qok, rok;
+        build_query_for<FN, CH, V, G>(p, b0 + r, lane, q, qi, ri, qok, rok);
+        vecf<V>* qr = qimg + (size_t)r * NQ * W;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            qr[lane + k * kWave] = q.q0[k];
+            if constexpr (NQ > 1) qr[W + lane + k * kWave] = q.q1[k];
+        }
+        if (lane == 0) rrow[r] = rok ? ri : -1;
+    }
+    for (int i = t; i < kTileBuckets; i += NT) hist[i] = 0;
+    __syncthreads();
+
+    // 2. counting sort of the block's items of slice x by entity bucket
+    const int64_t nf = (int64_t)nr * Np;
+    auto item = [&](int64_t f, int& bucket, int& code) -> bool {
+        const int r = (int)(f / Np);
+        const int64_t n = f - (int64_t)r * Np, b = b0 + r;
+        const int64_t id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
+        const int64_t row = id - p.c_base;
+        const bool valid = row >= 0 && row < p.c_rows;
+        if (valid ? (row < e_lo || row >= e_hi) : x != 0) return false;
+        bucket = valid ? (int)((row - e_lo) * kTileBuckets / S) : 0;
+        code = (r << 16) | (int)n;
+        return true;
+    };
+    for (int64_t f = t; f < nf; f += NT) {
+        int bk, code;
+        if (item(f, bk, code)) atomicAdd(&hist[bk], 1);
+    }
+    __syncthreads();
+    if (w == 0) {  // exclusive scan of the bucket counts (4 per lane)
+        constexpr int PL = kTileBuckets / kWave;
+        int v[PL], s = 0;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) {
+            v[i] = hist[lane * PL + i];
+            s += v[i];
+        }
+        int incl = s;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const int y = __shfl_up(incl, o, kWave);
+            if (lane >= o) incl += y;
+        }
+        int run = incl - s;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) {
+            hist[lane * PL + i] = run;
+            run += v[i];
+        }
+        if (lane == kWave - 1) cntp[0] = incl;
+    }
+    __syncthreads();
+    for (int64_t f = t; f < nf; f += NT) {
+        int bk, code;
+        if (item(f, bk, code)) list[atomicAdd(&hist[bk], 1)] = code;
+    }
+    __syncthreads();
+    const int cnt = cntp[0];
+
+    // 3. the sweep: wave w takes items w, w + NWV, w + 2 NWV, ...; with KGE_TILE_DEPTH = 2 the next item's
+    // candidate row (and InterHT's relation third) is in flight while this one is scored
+    struct Item {
+        Cand<FN, V, G> c;
+        vecf<V> q2[FN == KGE_INTERHT ? G : 1];
+    };
+    for (int c0 = w; c0 < cnt; c0 += NT) {
+        const int nc = min(kWave, (cnt - c0 + kTileWaves - 1) / kTileWaves);
+        int code = 0;
+        int64_t my_id = 0;
+        if (lane < nc) {
+            code = list[c0 + kTileWaves * lane];
+            const int r = code >> 16, n = code & 0xFFFF;
+            const int64_t b = b0 + r;
+            my_id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
+        }
+        auto load = [&](Item& it, int j) {
+            bool ok;
+            it.c.load(cand_row(p, readlane64(my_id, j), ok), ok, p.D, lane);
+            if constexpr (FN == KGE_INTERHT) {
+                const int64_t ri = rrow[__builtin_amdgcn_readlane(code, j) >> 16];
+                const rsrc_t sr = make_rsrc(p.rel + (ri >= 0 ? ri : 0) * p.r_ld + p.r_off,
+                                            ri >= 0 ? (uint32_t)p.D * 4u : 0u);
+#pragma unroll
+                for (int k = 0; k < G; ++k) it.q2[k] = bload<V>(sr, goff<V>(lane, k));
+            }
+        };
+        auto score = [&](const Item& it, int j) -> float {
+            const int cj = __builtin_amdgcn_readlane(code, j);
+            const int r = cj >> 16, n = cj & 0xFFFF;
+            const vecf<V>* qr = qimg + (size_t)r * NQ * W;
+            if (CH && n == p.N) {
+                // head-batch positive: the single-mode (h, r) query, tail formula (model.py:127-146)
+                Query<FN, false, V, G> qp;
+                const int64_t b = b0 + r;
+                const int64_t hi = p.pos_base[b * 3], rj = p.pos_base[b * 3 + 1];
+                const bool hok = hi >= 0 && hi < p.q_rows, rjok = rj >= 0 && rj < p.r_rows;
+                qp.build(p.qent + (hok ? hi : 0) * p.q_ld, hok, p.rel + (rjok ? rj : 0) * p.r_ld + p.r_off, rjok, p.D,
+                         lane, p);
+                return cand_score<FN, false, V, G>(it.c, qp, p);
+            } else if constexpr (FN == KGE_INTERHT) {
+                TileQueryIH<V, G> q{{qr, lane}, {qr + W, lane}, {}};
+#pragma unroll
+                for (int k = 0; k < G; ++k) q.q2[k] = it.q2[k];
+                return cand_score<FN, CH, V, G>(it.c, q, p);
+            } else {
+                const LdsQuery<V> q{{qr, lane}, {qr + (NQ > 1 ? W : 0), lane}, {qr, lane}};
+                return cand_score<FN, CH, V, G>(it.c, q, p);
+            }
+        };
+        float my_score = 0.f;
+        if constexpr (KGE_TILE_DEPTH == 1) {
+            for (int j = 0; j < nc; ++j) {
+                Item it;
+                load(it, j);
+                const float s = score(it, j);
+                if (lane == j) my_score = s;
+            }
+        } else {
+            Item x0, x1;
+            load(x0, 0);
+            for (int j = 0; j < nc; j += 2) {
+                if (j + 1 < nc) load(x1, j + 1);
+                float s = score(x0, j);
+                if (lane == j) my_score = s;
+                if (j + 1 < nc) {
+                    if (j + 2 < nc) load(x0, j + 2);
+                    s = score(x1, j + 1);
+                    if (lane == j + 1) my_score = s;
+                }
+            }
+        }
+        if (lane < nc) {
+            const int r = code >> 16, n = code & 0xFFFF;
+            const int64_t b = b0 + r;
+            if (n < p.N) {
+                p.out[b * p.out_ld + n] = my_score;
+            } else {
+                if (p.out_pos_raw) p.out_pos_raw[b] = my_score;
+                p.out_pos_ls[b] = log_sigmoid(my_score);
+            }
+        }
+    }
+}
+
 // Scoring in the XCD-sliced order (kge_score_indexed / kge_score_sharded, N >= 128): the table's rows
 // [c_base, c_base + c_rows) are cut into 8 slices and scored as step_fwd_xcd_kernel scores them, without the
 // positives. Sharded (skip_foreign): a candidate outside the shard scores 0 (written by the slice-0 wave);
@@ -2939,6 +3136,17 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, false>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_STEP_FWD_XCD)
         hipLaunchKernelGGL((step_fwd_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_STEP_FWD_TILE || kind == KIND_SCORE_TILE) {
+        if constexpr (G <= kFwdGradMaxG) {
+            // up to the whole 160 KB of a CU's LDS per block (set once per instantiation)
+            static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G>),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           kTileLdsMax) == hipSuccess;
+            (void)lds_ok;
+            hipLaunchKernelGGL((step_fwd_tile_kernel<FN, CH, V, G>), dim3(blocks), dim3(kTileWaves * kWave),
+                               p.tile_lds, st, p);
+        }
+    }
     else if (kind == KIND_SCORE_SHARD_XCD)
         hipLaunchKernelGGL((score_sharded_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_SHARD_BUCKET)

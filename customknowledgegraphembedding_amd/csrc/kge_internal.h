@@ -34,7 +34,22 @@ enum Kind {
     KIND_STEP_FWD_XCD = 16,    // kge_step_forward's negatives, XCD-sliced entity table, ascending ids per wave
     KIND_SCORE_SHARD_XCD = 17, // kge_score_indexed / kge_score_sharded in the same order (no positives)
     KIND_SHARD_BUCKET = 18,    // row-sharded forward: this rank's bucket (kge_shard_plan) scored, compact out
+    KIND_STEP_FWD_TILE = 19,   // kge_step_forward's negatives + positives: row-group x XCD-slice tiles, one
+                               // entity-sorted sweep per block (queries in LDS)
+    KIND_SCORE_TILE = 20,      // kge_score_indexed in the same order (no positives)
 };
+#ifndef KGE_TILE_WAVES
+#define KGE_TILE_WAVES 8
+#endif
+#ifndef KGE_TILE_DEPTH
+#define KGE_TILE_DEPTH 2
+#endif
+constexpr int kTileWaves = KGE_TILE_WAVES;  // waves per row-group tile block
+constexpr int kTileBuckets = 256;  // entity buckets of a slice (the block's counting sort)
+constexpr int kTileMaxRows = 16;
+constexpr int kTileLdsMax = 160 * 1024;
+// LDS query operands per batch row of the tile kernel (InterHT's third, the relation, is read per candidate)
+constexpr int tile_nq(int fn) { return (fn == KGE_COMPLEX || fn == KGE_ROTATE || fn == KGE_INTERHT) ? 2 : 1; }
 // query operands a score function's gradient has (q0 always; q1 for the complex / split forms; q2 InterHT)
 constexpr int shard_nq(int fn) {
     return fn == KGE_INTERHT ? 3 : ((fn == KGE_COMPLEX || fn == KGE_ROTATE) ? 2 : 1);
@@ -69,6 +84,9 @@ struct ScoreParams {
     const int* bk_start;  // [B, 9] the bucket's XCD-slice starts per row
     int64_t bk_ld;
     int xcd_phases;       // step_fwd_xcd_kernel: the table's 8 slices cut again into this many phases (1: none)
+    int tile_rows;        // step_fwd_tile_kernel: batch rows per block (their queries staged in LDS)
+    int tile_lds;         // step_fwd_tile_kernel: dynamic LDS bytes of one block
+    int tile_pos;         // step_fwd_tile_kernel: also score the rows' positives (kge_step_forward)
     float* out;
     int64_t out_ld;
     int64_t B, N;

@@ -1,0 +1,117 @@
+"""kge_step_forward's row-group x XCD-slice tile form (step_fwd_tile_kernel, KGE_STEP_ORDER=tile, the default
+for N >= 128): every candidate and positive goes through the same cand_score as the batch-row-major form
+(step_fwd_kernel) and the XCD-sliced form (step_fwd_xcd_kernel), so all four outputs must be BITWISE equal
+across the three orders, for every score function, both negative modes, any rows-per-block cap, ragged
+batches, out-of-range ids, skewed id distributions and the full C2 size (reference: model.py:114-205,
+supervisor.py:17-18). The fp64 oracle check of the default (tile) order is in test_configs_gpu.py."""
+import contextlib
+import os
+
+import pytest
+import torch
+
+import customknowledgegraphembedding_amd as kge
+from customknowledgegraphembedding_amd import ops
+from customknowledgegraphembedding_amd._lib import FN_IDS
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+FNS = ["TransE", "DistMult", "ComplEx", "RotatE", "pRotatE", "InterHT"]
+
+
+@contextlib.contextmanager
+def _env(**kv):
+    old = {k: os.environ.get(k) for k in kv}
+    try:
+        for k, v in kv.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _model(name, E, R, d, seed=0):
+    return kge.TFKGEModel(name, E, R, d, 12.0, double_entity_embedding=name in ("ComplEx", "RotatE", "InterHT"),
+                          double_relation_embedding=name == "ComplEx", triple_relation_embedding=name == "InterHT",
+                          device=DEV, seed=seed)
+
+
+def _run(m, mode, pos, neg, order, rows=None):
+    with _env(KGE_STEP_ORDER=order, KGE_TILE_ROWS=rows):
+        out = ops.step_forward_raw(FN_IDS[m.model_name], mode, m.entity_embedding.detach(),
+                                   m.relation_embedding.detach(), m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f,
+                                   modulus=float(m.modulus.detach().reshape(-1)[0]) if m.model_name == "pRotatE" else 0.0)
+    torch.cuda.synchronize()
+    return out
+
+
+def _same(a, b):
+    """Bitwise equal, NaN where the other is NaN (a zero query row gives NaN: no epsilon, Q7)."""
+    return all(bool(((x == y) | (torch.isnan(x) & torch.isnan(y))).all()) for x, y in zip(a, b))
+
+
+def test_order_query_reports_tile_for_large_n():
+    lib = kge.load()
+    with _env(KGE_STEP_ORDER=None):
+        assert lib.kge_step_forward_order(40943, 256) == 2
+        assert lib.kge_step_forward_order(40943, 64) == 0
+    with _env(KGE_STEP_ORDER="xcd"):
+        assert lib.kge_step_forward_order(40943, 256) == 1
+
+
+@pytest.mark.parametrize("name", FNS)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_tile_bitwise_equals_row_and_xcd(name, mode):
+    E, R, d, B, N = 3001, 7, 96, 37, 200  # B not a multiple of the rows per block
+    m = _model(name, E, R, d)
+    g = torch.Generator().manual_seed(5)
+    pos = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(0, R, (B,), generator=g),
+                       torch.randint(0, E, (B,), generator=g)], 1)
+    neg = torch.randint(0, E, (B, N), generator=g)
+    # out-of-range ids (zero row, TF-GPU gather), in candidates, positives' tails and query rows
+    neg[0, :5] = torch.tensor([-1, E, E + 7, -100, 0])
+    pos[1, 2] = E + 3
+    pos[2, 0] = -2
+    pos[3, 1] = R + 1
+    pos, neg = pos.to(DEV), neg.to(DEV)
+    want = _run(m, mode, pos, neg, "row")
+    assert _same(_run(m, mode, pos, neg, "xcd"), want)
+    for rows in (None, 1, 3, 16):
+        assert _same(_run(m, mode, pos, neg, "tile", rows), want), rows
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_tile_skewed_ids_one_slice_and_tiny_shapes(mode):
+    """Every candidate in slice 0 (one block of each row group holds all R (N + 1) items), duplicates of
+    one id, N = 1 and B = 1."""
+    name, E, R, d = "InterHT", 4000, 5, 64
+    m = _model(name, E, R, d, seed=1)
+    g = torch.Generator().manual_seed(9)
+    for B, N, hi in ((33, 300, 400), (5, 128, 1), (1, 1, E), (17, 1, E)):
+        pos = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(0, R, (B,), generator=g),
+                           torch.randint(0, hi, (B,), generator=g)], 1).to(DEV)
+        neg = torch.randint(0, hi, (B, N), generator=g).to(DEV)
+        want = _run(m, mode, pos, neg, "row")
+        assert _same(_run(m, mode, pos, neg, "tile"), want), (B, N, hi)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_tile_c2_full_size_bitwise(mode):
+    """C2: WN18RR InterHT d=1000 -de -tr, B=512, N=256: tile == XCD-sliced == row-major, bitwise."""
+    name, E, R, d, B, N = "InterHT", 40943, 11, 1000, 512, 256
+    m = kge.TFKGEModel(name, E, R, d, 24.0, double_entity_embedding=True, triple_relation_embedding=True,
+                       device=DEV, seed=0)
+    g = torch.Generator().manual_seed(3)
+    pos = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(0, R, (B,), generator=g),
+                       torch.randint(0, E, (B,), generator=g)], 1).to(DEV)
+    neg = torch.randint(0, E, (B, N), generator=g).to(DEV)
+    want = _run(m, mode, pos, neg, "xcd")
+    assert _same(_run(m, mode, pos, neg, "tile"), want)
+    assert _same(_run(m, mode, pos, neg, "row"), want)

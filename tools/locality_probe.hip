@@ -177,6 +177,84 @@ __global__ __launch_bounds__(256) void gather_pairs(const float* __restrict__ ta
     }
 }
 
+// row-group tiles: block = (group of R batch rows, entity slice x = blockIdx % 8). The R rows' queries (q0, q1:
+// 2 x 1000 floats each) are staged once into LDS; the block's (entity, row) pairs, sorted by entity, are dealt
+// round-robin to its NWV waves, so the block sweeps its slice in one ascending front and the slice's 32 blocks
+// on one XCD sweep it together. Per pair: the candidate row from global (8 KB), the query from LDS (8 KB), the
+// relation third from a small global table (L2-resident).
+template <int R, int NWV, int DEPTH>
+__global__ __launch_bounds__(NWV * 64) void tile_pairs(const float* __restrict__ tab, const float* __restrict__ qbuf,
+                                                       const float* __restrict__ rel, const int* __restrict__ off,
+                                                       const int* __restrict__ pe, const int* __restrict__ pb,
+                                                       float* __restrict__ out) {
+    __shared__ float4 q[R][2][64 * GH];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int blk = blockIdx.x, grp = blk / 8;
+    for (int i = t; i < R * 2 * 64 * GH; i += NWV * 64) {
+        const int r = i / (2 * 64 * GH), j = i % (2 * 64 * GH), hf = j / (64 * GH), k = j % (64 * GH);
+        q[r][hf][k] = k < 250 ? reinterpret_cast<const float4*>(qbuf)[(int64_t)(grp * R + r) * 500 + hf * 250 + k]
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const int lo = off[blk], hi = off[blk + 1];
+    const uint32_t hb = 1000 * 4;
+    auto score = [&](const Half& ea, const Half& eb, int b) {
+        Half q2;
+        load_half(q2, rel + (int64_t)((grp * R + b) % 11) * 1000, lane, hb);
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < GH; ++k) {
+            const float4 a = q[b][0][lane + 64 * k], c = q[b][1][lane + 64 * k];
+            s += fabsf(a.x * eb.a[k][0] - ea.a[k][0] * c.x + q2.a[k][0]);
+            s += fabsf(a.y * eb.a[k][1] - ea.a[k][1] * c.y + q2.a[k][1]);
+            s += fabsf(a.z * eb.a[k][2] - ea.a[k][2] * c.z + q2.a[k][2]);
+            s += fabsf(a.w * eb.a[k][3] - ea.a[k][3] * c.w + q2.a[k][3]);
+        }
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        return s;
+    };
+    for (int c0 = lo + wave; c0 < hi; c0 += NWV * 64) {
+        const int nc = min(64, (hi - c0 + NWV - 1) / NWV);
+        const int my = c0 + NWV * lane;
+        const int my_e = lane < nc ? pe[my] : 0, my_b = lane < nc ? pb[my] : 0;
+        float mine = 0.f;
+        if constexpr (DEPTH == 1) {
+            for (int j = 0; j < nc; ++j) {
+                Half ea, eb;
+                const int e = __builtin_amdgcn_readlane(my_e, j), b = __builtin_amdgcn_readlane(my_b, j);
+                load_half(ea, tab + (int64_t)e * 2000, lane, hb);
+                load_half(eb, tab + (int64_t)e * 2000 + 1000, lane, hb);
+                const float s = score(ea, eb, b);
+                if (lane == j) mine = s;
+            }
+        } else {
+            Half a0, b0, a1, b1;
+            int e = __builtin_amdgcn_readlane(my_e, 0);
+            load_half(a0, tab + (int64_t)e * 2000, lane, hb);
+            load_half(b0, tab + (int64_t)e * 2000 + 1000, lane, hb);
+            for (int j = 0; j < nc; j += 2) {
+                if (j + 1 < nc) {
+                    e = __builtin_amdgcn_readlane(my_e, j + 1);
+                    load_half(a1, tab + (int64_t)e * 2000, lane, hb);
+                    load_half(b1, tab + (int64_t)e * 2000 + 1000, lane, hb);
+                }
+                float s = score(a0, b0, __builtin_amdgcn_readlane(my_b, j));
+                if (lane == j) mine = s;
+                if (j + 1 < nc) {
+                    if (j + 2 < nc) {
+                        e = __builtin_amdgcn_readlane(my_e, j + 2);
+                        load_half(a0, tab + (int64_t)e * 2000, lane, hb);
+                        load_half(b0, tab + (int64_t)e * 2000 + 1000, lane, hb);
+                    }
+                    s = score(a1, b1, __builtin_amdgcn_readlane(my_b, j + 1));
+                    if (lane == j + 1) mine = s;
+                }
+            }
+        }
+        if (lane < nc) out[my] = mine;
+    }
+}
+
 struct Lists {
     std::vector<int> off, ids, wl;
 };
@@ -369,6 +447,56 @@ int main() {
                    halves == 1 ? "entity-major + 12 KB query/pair, 8 slices" : "entity-major + query, 2 halves x 4 slices",
                    ms * 1e3, bytes / (ms * 1e-3) / 1e9);
         }
+        // row-group tiles (tile_pairs): R rows per block, pairs of slice x sorted by entity
+        auto tiles = [&](auto kern, int R, int nwv, const char* nm) {
+            const int ngrp = (int)(B / R), nblk = ngrp * 8;
+            std::vector<std::vector<std::pair<int, int>>> per(nblk);
+            for (int64_t i = 0; i < B * N; ++i) {
+                const int e = neg[i], b = (int)(i / N);
+                per[(b / R) * 8 + (int)(e / slice)].push_back({e, b % R});
+            }
+            std::vector<int> off{0}, pe, pb;
+            for (auto& v : per) {
+                std::sort(v.begin(), v.end());
+                for (auto& pr : v) {
+                    pe.push_back(pr.first);
+                    pb.push_back(pr.second);
+                }
+                off.push_back((int)pe.size());
+            }
+            int *doff, *dpe, *dpb;
+            CHECK(hipMalloc(&doff, off.size() * 4));
+            CHECK(hipMalloc(&dpe, pe.size() * 4));
+            CHECK(hipMalloc(&dpb, pb.size() * 4));
+            CHECK(hipMemcpy(doff, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+            CHECK(hipMemcpy(dpe, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+            CHECK(hipMemcpy(dpb, pb.data(), pb.size() * 4, hipMemcpyHostToDevice));
+            hipEvent_t a, bb;
+            CHECK(hipEventCreate(&a));
+            CHECK(hipEventCreate(&bb));
+            for (int i = 0; i < 3; ++i)
+                hipLaunchKernelGGL(kern, dim3(nblk), dim3(nwv * 64), 0, 0, tab, qbuf, rel, doff, dpe, dpb, out);
+            CHECK(hipGetLastError());
+            CHECK(hipEventRecord(a));
+            for (int i = 0; i < 20; ++i)
+                hipLaunchKernelGGL(kern, dim3(nblk), dim3(nwv * 64), 0, 0, tab, qbuf, rel, doff, dpe, dpb, out);
+            CHECK(hipEventRecord(bb));
+            CHECK(hipEventSynchronize(bb));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, a, bb));
+            ms /= 20;
+            printf("%-44s %8.1f us  %7.0f GB/s (gathered bytes)\n", nm, ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+            CHECK(hipFree(doff));
+            CHECK(hipFree(dpe));
+            CHECK(hipFree(dpb));
+        };
+        tiles(tile_pairs<16, 16, 1>, 16, 16, "tiles R=16, 16 waves, depth 1");
+        tiles(tile_pairs<16, 16, 2>, 16, 16, "tiles R=16, 16 waves, depth 2");
+        tiles(tile_pairs<16, 8, 2>, 16, 8, "tiles R=16, 8 waves, depth 2");
+        tiles(tile_pairs<8, 8, 1>, 8, 8, "tiles R=8, 8 waves, depth 1");
+        tiles(tile_pairs<8, 8, 2>, 8, 8, "tiles R=8, 8 waves, depth 2");
+        tiles(tile_pairs<8, 16, 1>, 8, 16, "tiles R=8, 16 waves, depth 1");
+        tiles(tile_pairs<4, 8, 2>, 4, 8, "tiles R=4, 8 waves, depth 2");
     }
     return 0;
 }

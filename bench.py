@@ -991,8 +991,9 @@ def main(argv=None):
 
     neg_bytes, pos_bytes = algorithmic_bytes(w)
     step_bytes = neg_bytes + pos_bytes  # the fused kernel moves both calls' bytes
-    xcd = bool(kge.load().kge_step_forward_order(w["nentity"], N))
-    step_kernels = ["step_fwd_xcd_kernel", "neg_rows_kernel"] if xcd else ["step_fwd_kernel"]
+    order = int(kge.load().kge_step_forward_order(w["nentity"], N))  # 0 row-major, 1 XCD-sliced, 2 tiles
+    step_kernels = {0: ["step_fwd_kernel"], 1: ["step_fwd_xcd_kernel", "neg_rows_kernel"],
+                    2: ["step_fwd_tile_kernel", "neg_rows_kernel"]}[order]
     traffic, traffic_src = pmc_traffic(a.workload, step_kernels)
     kern_avg_s = statistics.mean(kern_ms) / 1e3
     # head and tail reported separately (steps alternate head, tail, ...)
@@ -1020,9 +1021,12 @@ def main(argv=None):
                    "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": roofline_hbm(
             step_bytes, traffic, traffic_src, kern_avg_s,
-            kernel=("step_fwd_xcd_kernel + neg_rows_kernel (the step's two launches: negatives and positives "
-                    "gathered in XCD-sliced ascending-id order, then the row reductions)" if xcd
-                    else "step_fwd_kernel (negatives + positives + row reductions, one launch)"),
+            kernel={0: "step_fwd_kernel (negatives + positives + row reductions, one launch)",
+                    1: "step_fwd_xcd_kernel + neg_rows_kernel (the step's two launches: negatives and positives "
+                       "gathered in XCD-sliced ascending-id order, then the row reductions)",
+                    2: "step_fwd_tile_kernel + neg_rows_kernel (the step's two launches: negatives and positives "
+                       "in row-group x XCD-slice tiles, queries in LDS, each block's candidates swept in entity "
+                       "order; then the row reductions)"}[order],
             kernel_avg_us_head_batch=head_ms[0] * 1e3, kernel_avg_us_tail_batch=tail_ms[0] * 1e3,
             unique_row_bytes_per_step=uniq * ent_dim_ * 4, row_reuse=(B * N + 2 * B) / max(1, uniq)),
         "build": kge.build_id(),

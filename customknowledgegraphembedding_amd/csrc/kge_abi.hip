@@ -467,7 +467,7 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
         waves = p.B * kWavesPerBlock;  // one block per slot / batch row
     } else if (kind == KIND_STEP_FWD_TILE || kind == KIND_SCORE_TILE) {
         if (p.tile_rows < 1 || p.tile_lds > kTileLdsMax) return fail(KGE_EINVAL, "tile plan missing");
-        // one block of kTileWaves waves per (group of tile_rows batch rows, entity slice): run_score's
+        // one block of tile_waves waves per (group of tile_rows batch rows, entity slice): run_score's
         // block count is waves / kWavesPerBlock
         waves = (p.B + p.tile_rows - 1) / p.tile_rows * 8 * kWavesPerBlock;
     } else if (kind == KIND_STEP_FWD_XCD || kind == KIND_SCORE_SHARD_XCD || kind == KIND_SHARD_BUCKET) {
@@ -615,14 +615,38 @@ int tile_plan(int fn, ScoreParams& p) {
     int V = 1, G = 1;
     if (pick_vg(p, V, G)) return 0;
     if (G > kFwdGradMaxG || p.N + 1 > 65536 || p.c_rows <= 0) return 0;
-    const int64_t qrow = (int64_t)tile_nq(fn) * G * kWave * V * 4 + 8, lrow = (p.N + 1) * 4;
+    const int64_t opb = (int64_t)G * kWave * V * 4;  // bytes of one query operand image
+    // InterHT: batch rows sorted by relation (B <= kTileSortMaxB), relation thirds in LDS slots
+    int64_t P2 = 0;
+    if (fn == KGE_INTERHT && p.B <= kTileSortMaxB) {
+        P2 = kWave;
+        while (P2 < p.B) P2 <<= 1;
+    }
+    const int64_t qrow = tile_nq(fn) * opb + 8 + 8 + 4, lrow = (p.N + 1) * 4;
     const int64_t fixed = kTileBuckets * 4 + 16;
-    int64_t R = std::min<int64_t>(kTileMaxRows, (kTileLdsMax - fixed) / (qrow + lrow));
+    auto lds = [&](int64_t R, int64_t QS) { return R * qrow + QS * opb + fixed + std::max(R * lrow, P2 * 4); };
+    int64_t R = kTileMaxRows;
     const char* env = getenv("KGE_TILE_ROWS");
     if (env && atoi(env) > 0) R = std::min<int64_t>(R, atoi(env));
+    while (R >= 1 && lds(R, 0) > kTileLdsMax) --R;
     if (R < 1) return 0;
+    int64_t QS = 0;
+    if (fn == KGE_INTERHT)
+        while (QS < R && lds(R, QS + 1) <= kTileLdsMax) ++QS;
+    const char* qenv = getenv("KGE_TILE_Q2SLOTS");
+    if (qenv) QS = std::min<int64_t>(QS, std::max(0, atoi(qenv)));
+    // waves per block: candidate rows of 4 KB or more keep 2 x 8 rows in flight per CU at 8 waves (two
+    // rows deep each); smaller rows need 16 waves for the same bytes in flight. KGE_TILE_WAVES overrides.
+    const int64_t row_bytes = (int64_t)p.D * 4 * (is_split(fn) ? 2 : 1);
+    p.tile_waves = row_bytes >= 4096 ? 8 : 16;
+    const char* wenv = getenv("KGE_TILE_WAVES");
+    if (wenv && (atoi(wenv) == 8 || atoi(wenv) == 16)) p.tile_waves = atoi(wenv);
+    p.tile_dry = getenv("KGE_TILE_DRY") ? std::max(1, atoi(getenv("KGE_TILE_DRY"))) : 0;
+    if (getenv("KGE_TILE_NOSORT")) P2 = 0;
     p.tile_rows = (int)R;
-    p.tile_lds = (int)(R * (qrow + lrow) + fixed);
+    p.tile_q2slots = (int)QS;
+    p.tile_sort = (int)P2;
+    p.tile_lds = (int)lds(R, QS);
     return 1;
 }
 

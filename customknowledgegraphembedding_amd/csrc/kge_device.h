@@ -882,7 +882,8 @@ step_fwd_xcd_kernel(ScoreParams p) {
 //   2. the rows' candidates that fall in slice x (slice 0 also takes the out-of-range ids, which score
 //      against a zero row), plus, with tile_pos, each row's positive whose tail falls there, are counting-
 //      sorted into kTileBuckets entity buckets in LDS (order inside a bucket: arbitrary);
-//   3. the block's kTileWaves waves take the sorted list round-robin, one candidate row in registers each.
+//   3. the block's NWV waves (8 for candidate rows of 4 KB or more, else 16) take the sorted list round-robin,
+//      two candidate rows in flight per wave.
 // The block sweeps its slice in ONE ascending front, and the ~32 blocks of an XCD sweep the same slice
 // together, so the ~3.4 gathers of an entity row (C2) are issued by one XCD close in time and the repeats
 // hit its L2. Against step_fwd_xcd_kernel (one wave per (row, slice, phase), which rebuilds its row's query
@@ -899,33 +900,84 @@ struct TileQueryIH {  // InterHT: q0, q1 from LDS, the relation third in registe
     vecf<V> q2[G];
 };
 
-template <int FN, bool CH, int V, int G>
-__global__ __launch_bounds__(kTileWaves * kWave) void step_fwd_tile_kernel(ScoreParams p) {
+template <int FN, bool CH, int V, int G, int NWV>
+__global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char tile_smem[];
     constexpr int NQ = tile_nq(FN);
     constexpr int W = G * kWave;
-    constexpr int NT = kTileWaves * kWave;
-    const int R = p.tile_rows;
+    constexpr int NT = NWV * kWave;
+    const int R = p.tile_rows, QS = p.tile_q2slots;
     vecf<V>* qimg = reinterpret_cast<vecf<V>*>(tile_smem);  // [R][NQ][W]
-    int64_t* rrow = reinterpret_cast<int64_t*>(qimg + (size_t)R * NQ * W);
-    int* hist = reinterpret_cast<int*>(rrow + R);
+    vecf<V>* q2img = qimg + (size_t)R * NQ * W;               // [QS][W] InterHT relation thirds
+    int64_t* rrow = reinterpret_cast<int64_t*>(q2img + (size_t)QS * W);
+    int64_t* brow = rrow + R;
+    int* q2slot = reinterpret_cast<int*>(brow + R);
+    int* hist = q2slot + R;
     int* cntp = hist + kTileBuckets;
-    int* list = cntp + 4;
+    int* list = cntp + 4;  // also the relation sort's keys before the list is built
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int x = (int)(blockIdx.x & 7);
-    const int64_t b0 = (int64_t)(blockIdx.x >> 3) * R;
-    const int nr = (int)min<int64_t>(R, p.B - b0);
+    const int64_t g0 = (int64_t)(blockIdx.x >> 3) * R;
+    const int nr = (int)min<int64_t>(R, p.B - g0);
     if (nr <= 0) return;  // block-uniform
     const int64_t S = (p.c_rows + 7) / 8;
     const int64_t e_lo = min((int64_t)x * S, p.c_rows), e_hi = min(p.c_rows, e_lo + S);
     const int64_t Np = p.tile_pos ? p.N + 1 : p.N;  // column N: the row's positive (its tail)
 
+    // 0. the block's batch rows: ranks [g0, g0 + nr) of the batch in (relation, row) order (p.tile_sort: InterHT,
+    //    so that a block's rows share few relations and their relation thirds fit QS LDS slots), else rows g0 + r.
+    //    Bitonic sort of (relation << 20 | row) keys held in registers, element i = u NT + t: strides below 64
+    //    within the wave (shuffles), larger ones through LDS.
+    if (p.tile_sort) {
+        const int P2 = p.tile_sort;  // power of two >= max(B, 64), <= kTileSortMaxB
+        constexpr int MU = (kTileSortMaxB + NT - 1) / NT;
+        int key[MU];
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            const int i = u * NT + t;
+            key[u] = INT32_MAX;
+            if (i < p.B) {
+                const int64_t rr = p.r_idx ? p.r_idx[i * p.r_stride] : i;
+                const int bk = (rr >= 0 && rr < p.r_rows) ? (int)min<int64_t>(rr, kTileSortRel - 2) : kTileSortRel - 1;
+                key[u] = (bk << 20) | i;
+            }
+        }
+        for (int k = 2; k <= P2; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                if (j >= kWave) {
+#pragma unroll
+                    for (int u = 0; u < MU; ++u)
+                        if (u * NT + t < P2) list[u * NT + t] = key[u];
+                    __syncthreads();
+                }
+#pragma unroll
+                for (int u = 0; u < MU; ++u) {
+                    const int i = u * NT + t;
+                    if (u * NT < P2) {  // block-uniform
+                        const int o = j >= kWave ? (i < P2 ? list[i ^ j] : INT32_MAX) : __shfl_xor(key[u], j, kWave);
+                        const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+                        key[u] = keep_min ? min(key[u], o) : max(key[u], o);
+                    }
+                }
+                if (j >= kWave) __syncthreads();
+            }
+#pragma unroll
+        for (int u = 0; u < MU; ++u)
+            if (u * NT + t < P2) list[u * NT + t] = key[u];
+        __syncthreads();
+        if (t < nr) brow[t] = list[g0 + t] & 0xFFFFF;
+    } else if (t < nr) {
+        brow[t] = g0 + t;
+    }
+    __syncthreads();
+    if (p.tile_dry == 1) return;  // A/B knob KGE_TILE_DRY=<level>: the setup up to this point alone
+
     // 1. the rows' query operands
-    for (int r = w; r < nr; r += kTileWaves) {
+    for (int r = w; r < nr; r += NWV) {
         Query<FN, CH, V, G> q;
         int64_t qi, ri;
         bool qok, rok;
-        build_query_for<FN, CH, V, G>(p, b0 + r, lane, q, qi, ri, qok, rok);
+        build_query_for<FN, CH, V, G>(p, brow[r], lane, q, qi, ri, qok, rok);
         vecf<V>* qr = qimg + (size_t)r * NQ * W;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
@@ -936,25 +988,78 @@ __global__ __launch_bounds__(kTileWaves * kWave) void step_fwd_tile_kernel(Score
     }
     for (int i = t; i < kTileBuckets; i += NT) hist[i] = 0;
     __syncthreads();
+    if constexpr (FN == KGE_INTERHT) {
+        // relation slots: one per run of equal relations among the block's rows (first QS runs; the rows of
+        // later runs read their relation third from the table per candidate)
+        if (t == 0) {
+            int sl = -1;
+            int64_t prev = INT64_MIN;
+            for (int r = 0; r < nr; ++r) {
+                if (rrow[r] != prev) {
+                    ++sl;
+                    prev = rrow[r];
+                }
+                q2slot[r] = sl < QS ? sl : -1;
+            }
+        }
+        __syncthreads();
+        for (int r = w; r < nr; r += NWV) {
+            const int sl = q2slot[r];
+            if (sl < 0 || (r > 0 && q2slot[r - 1] == sl)) continue;  // wave-uniform: the run's first row fills
+            const int64_t ri = rrow[r];
+            const rsrc_t sr = make_rsrc(p.rel + (ri >= 0 ? ri : 0) * p.r_ld + p.r_off, ri >= 0 ? (uint32_t)p.D * 4u : 0u);
+#pragma unroll
+            for (int k = 0; k < G; ++k) q2img[(size_t)sl * W + lane + k * kWave] = bload<V>(sr, goff<V>(lane, k));
+        }
+        __syncthreads();
+    }
 
+    if (p.tile_dry == 2) return;
     // 2. counting sort of the block's items of slice x by entity bucket
     const int64_t nf = (int64_t)nr * Np;
-    auto item = [&](int64_t f, int& bucket, int& code) -> bool {
-        const int r = (int)(f / Np);
-        const int64_t n = f - (int64_t)r * Np, b = b0 + r;
+    // no 64-bit divisions in the walk (an emulated int64 divide is ~100 instructions): the item's row by a
+    // float reciprocal corrected to the exact quotient (f < R (N + 1) < 2^21), the entity bucket by a float
+    // scale (any monotone map of the slice onto the buckets orders the sweep)
+    const int Np32 = (int)Np;
+    const float inv_np = 1.f / (float)Np32, bscale = (float)kTileBuckets / (float)S;
+    auto item = [&](int64_t f64, int& bucket, int& code) -> bool {
+        const int f = (int)f64;
+        int r = (int)((float)f * inv_np);
+        if (r * Np32 > f) --r;
+        if ((r + 1) * Np32 <= f) ++r;
+        const int n = f - r * Np32;
+        const int64_t b = brow[r];
         const int64_t id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
         const int64_t row = id - p.c_base;
         const bool valid = row >= 0 && row < p.c_rows;
         if (valid ? (row < e_lo || row >= e_hi) : x != 0) return false;
-        bucket = valid ? (int)((row - e_lo) * kTileBuckets / S) : 0;
-        code = (r << 16) | (int)n;
+        bucket = valid ? min(kTileBuckets - 1, (int)((float)(int)(row - e_lo) * bscale)) : 0;
+        code = (r << 16) | n;
         return true;
     };
-    for (int64_t f = t; f < nf; f += NT) {
-        int bk, code;
-        if (item(f, bk, code)) atomicAdd(&hist[bk], 1);
+    // the ids are loaded once, all in flight together, when the block's walk fits TPI per thread (C2: 4 112
+    // items over 512 threads); otherwise the walk is made twice (count, then scatter)
+    constexpr int TPI = 16;
+    int wbk[TPI], wcd[TPI];
+    const bool in_regs = nf <= (int64_t)TPI * NT;  // block-uniform
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < TPI; ++u) {
+            const int64_t f = (int64_t)u * NT + t;
+            wbk[u] = -1;
+            if (f < nf && !item(f, wbk[u], wcd[u])) wbk[u] = -1;
+        }
+#pragma unroll
+        for (int u = 0; u < TPI; ++u)
+            if (wbk[u] >= 0) atomicAdd(&hist[wbk[u]], 1);
+    } else {
+        for (int64_t f = t; f < nf; f += NT) {
+            int bk, code;
+            if (item(f, bk, code)) atomicAdd(&hist[bk], 1);
+        }
     }
     __syncthreads();
+    if (p.tile_dry == 3) return;
     if (w == 0) {  // exclusive scan of the bucket counts (4 per lane)
         constexpr int PL = kTileBuckets / kWave;
         int v[PL], s = 0;
@@ -978,13 +1083,20 @@ __global__ __launch_bounds__(kTileWaves * kWave) void step_fwd_tile_kernel(Score
         if (lane == kWave - 1) cntp[0] = incl;
     }
     __syncthreads();
-    for (int64_t f = t; f < nf; f += NT) {
-        int bk, code;
-        if (item(f, bk, code)) list[atomicAdd(&hist[bk], 1)] = code;
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < TPI; ++u)
+            if (wbk[u] >= 0) list[atomicAdd(&hist[wbk[u]], 1)] = wcd[u];
+    } else {
+        for (int64_t f = t; f < nf; f += NT) {
+            int bk, code;
+            if (item(f, bk, code)) list[atomicAdd(&hist[bk], 1)] = code;
+        }
     }
     __syncthreads();
     const int cnt = cntp[0];
 
+    if (p.tile_dry) return;
     // 3. the sweep: wave w takes items w, w + NWV, w + 2 NWV, ...; with KGE_TILE_DEPTH = 2 the next item's
     // candidate row (and InterHT's relation third) is in flight while this one is scored
     struct Item {
@@ -992,24 +1104,31 @@ __global__ __launch_bounds__(kTileWaves * kWave) void step_fwd_tile_kernel(Score
         vecf<V> q2[FN == KGE_INTERHT ? G : 1];
     };
     for (int c0 = w; c0 < cnt; c0 += NT) {
-        const int nc = min(kWave, (cnt - c0 + kTileWaves - 1) / kTileWaves);
+        const int nc = min(kWave, (cnt - c0 + NWV - 1) / NWV);
         int code = 0;
         int64_t my_id = 0;
         if (lane < nc) {
-            code = list[c0 + kTileWaves * lane];
+            code = list[c0 + NWV * lane];
             const int r = code >> 16, n = code & 0xFFFF;
-            const int64_t b = b0 + r;
+            const int64_t b = brow[r];
             my_id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
         }
         auto load = [&](Item& it, int j) {
             bool ok;
             it.c.load(cand_row(p, readlane64(my_id, j), ok), ok, p.D, lane);
             if constexpr (FN == KGE_INTERHT) {
-                const int64_t ri = rrow[__builtin_amdgcn_readlane(code, j) >> 16];
-                const rsrc_t sr = make_rsrc(p.rel + (ri >= 0 ? ri : 0) * p.r_ld + p.r_off,
-                                            ri >= 0 ? (uint32_t)p.D * 4u : 0u);
+                const int r = __builtin_amdgcn_readlane(code, j) >> 16;
+                const int sl = q2slot[r];
+                if (sl >= 0) {  // wave-uniform
 #pragma unroll
-                for (int k = 0; k < G; ++k) it.q2[k] = bload<V>(sr, goff<V>(lane, k));
+                    for (int k = 0; k < G; ++k) it.q2[k] = q2img[(size_t)sl * W + lane + k * kWave];
+                } else {
+                    const int64_t ri = rrow[r];
+                    const rsrc_t sr = make_rsrc(p.rel + (ri >= 0 ? ri : 0) * p.r_ld + p.r_off,
+                                                ri >= 0 ? (uint32_t)p.D * 4u : 0u);
+#pragma unroll
+                    for (int k = 0; k < G; ++k) it.q2[k] = bload<V>(sr, goff<V>(lane, k));
+                }
             }
         };
         auto score = [&](const Item& it, int j) -> float {
@@ -1019,7 +1138,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void step_fwd_tile_kernel(Score
             if (CH && n == p.N) {
                 // head-batch positive: the single-mode (h, r) query, tail formula (model.py:127-146)
                 Query<FN, false, V, G> qp;
-                const int64_t b = b0 + r;
+                const int64_t b = brow[r];
                 const int64_t hi = p.pos_base[b * 3], rj = p.pos_base[b * 3 + 1];
                 const bool hok = hi >= 0 && hi < p.q_rows, rjok = rj >= 0 && rj < p.r_rows;
                 qp.build(p.qent + (hok ? hi : 0) * p.q_ld, hok, p.rel + (rjok ? rj : 0) * p.r_ld + p.r_off, rjok, p.D,
@@ -1059,7 +1178,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void step_fwd_tile_kernel(Score
         }
         if (lane < nc) {
             const int r = code >> 16, n = code & 0xFFFF;
-            const int64_t b = b0 + r;
+            const int64_t b = brow[r];
             if (n < p.N) {
                 p.out[b * p.out_ld + n] = my_score;
             } else {
@@ -3110,6 +3229,15 @@ namespace kge_impl {
 // ---------------------------------------------------------------------------------------------
 // dispatch over (kind, candidate side, vector width, groups per lane) for one score function
 // ---------------------------------------------------------------------------------------------
+template <int FN, bool CH, int V, int G, int NWV>
+void launch_tile(const ScoreParams& p, hipStream_t st, int blocks) {
+    // up to the whole 160 KB of a CU's LDS per block (set once per instantiation)
+    static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G, NWV>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kTileLdsMax) == hipSuccess;
+    (void)lds_ok;
+    hipLaunchKernelGGL((step_fwd_tile_kernel<FN, CH, V, G, NWV>), dim3(blocks), dim3(NWV * kWave), p.tile_lds, st, p);
+}
+
 template <int FN, bool CH, int V, int G>
 void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
     if (kind == KIND_SHARD_FWD_GRAD || kind == KIND_SHARD_POS || kind == KIND_SHARD_EPILOGUE)
@@ -3138,13 +3266,10 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         hipLaunchKernelGGL((step_fwd_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_STEP_FWD_TILE || kind == KIND_SCORE_TILE) {
         if constexpr (G <= kFwdGradMaxG) {
-            // up to the whole 160 KB of a CU's LDS per block (set once per instantiation)
-            static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G>),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                           kTileLdsMax) == hipSuccess;
-            (void)lds_ok;
-            hipLaunchKernelGGL((step_fwd_tile_kernel<FN, CH, V, G>), dim3(blocks), dim3(kTileWaves * kWave),
-                               p.tile_lds, st, p);
+            if (p.tile_waves == 16)
+                launch_tile<FN, CH, V, G, 16>(p, st, blocks);
+            else
+                launch_tile<FN, CH, V, G, 8>(p, st, blocks);
         }
     }
     else if (kind == KIND_SCORE_SHARD_XCD)

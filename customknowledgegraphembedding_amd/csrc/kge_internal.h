@@ -38,16 +38,14 @@ enum Kind {
                                // entity-sorted sweep per block (queries in LDS)
     KIND_SCORE_TILE = 20,      // kge_score_indexed in the same order (no positives)
 };
-#ifndef KGE_TILE_WAVES
-#define KGE_TILE_WAVES 8
-#endif
 #ifndef KGE_TILE_DEPTH
 #define KGE_TILE_DEPTH 2
 #endif
-constexpr int kTileWaves = KGE_TILE_WAVES;  // waves per row-group tile block
 constexpr int kTileBuckets = 256;  // entity buckets of a slice (the block's counting sort)
 constexpr int kTileMaxRows = 16;
 constexpr int kTileLdsMax = 160 * 1024;
+constexpr int kTileSortRel = 2048;   // relation buckets of the tile kernel's row sort (larger ids share one)
+constexpr int kTileSortMaxB = 2048;  // batch rows the tile kernel sorts by relation in LDS
 // LDS query operands per batch row of the tile kernel (InterHT's third, the relation, is read per candidate)
 constexpr int tile_nq(int fn) { return (fn == KGE_COMPLEX || fn == KGE_ROTATE || fn == KGE_INTERHT) ? 2 : 1; }
 // query operands a score function's gradient has (q0 always; q1 for the complex / split forms; q2 InterHT)
@@ -87,6 +85,10 @@ struct ScoreParams {
     int tile_rows;        // step_fwd_tile_kernel: batch rows per block (their queries staged in LDS)
     int tile_lds;         // step_fwd_tile_kernel: dynamic LDS bytes of one block
     int tile_pos;         // step_fwd_tile_kernel: also score the rows' positives (kge_step_forward)
+    int tile_q2slots;     // step_fwd_tile_kernel (InterHT): LDS slots of relation thirds
+    int tile_sort;        // step_fwd_tile_kernel: 0, or the power of two >= B of the (relation, row) sort
+    int tile_waves;       // step_fwd_tile_kernel: waves per block (8 or 16)
+    int tile_dry;         // step_fwd_tile_kernel: setup only, no scoring (A/B knob KGE_TILE_DRY)
     float* out;
     int64_t out_ld;
     int64_t B, N;

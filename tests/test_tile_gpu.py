@@ -103,6 +103,23 @@ def test_tile_skewed_ids_one_slice_and_tiny_shapes(mode):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
+def test_tile_interht_relation_slots(mode):
+    """InterHT's relation thirds: rows sorted by relation (B <= 2048) with the first runs' thirds in LDS slots and
+    the rest read per candidate; many relations (slot overflow), no slots at all, out-of-range relations, and a
+    batch too large for the in-block sort (B > 2048, rows in batch order)."""
+    g = torch.Generator().manual_seed(11)
+    for E, R, B, N, slots in ((2500, 300, 40, 140, None), (2500, 5, 40, 140, 0), (2500, 7, 1500, 128, None),
+                              (2500, 3, 2100, 130, None)):
+        m = _model("InterHT", E, R, 32)
+        pos = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(-1, R + 1, (B,), generator=g),
+                           torch.randint(0, E, (B,), generator=g)], 1).to(DEV)
+        neg = torch.randint(0, E, (B, N), generator=g).to(DEV)
+        want = _run(m, mode, pos, neg, "row")
+        with _env(KGE_TILE_Q2SLOTS=slots):
+            assert _same(_run(m, mode, pos, neg, "tile"), want), (R, B, slots)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
 def test_tile_c2_full_size_bitwise(mode):
     """C2: WN18RR InterHT d=1000 -de -tr, B=512, N=256: tile == XCD-sliced == row-major, bitwise."""
     name, E, R, d, B, N = "InterHT", 40943, 11, 1000, 512, 256

@@ -182,12 +182,13 @@ __global__ __launch_bounds__(256) void gather_pairs(const float* __restrict__ ta
 // round-robin to its NWV waves, so the block sweeps its slice in one ascending front and the slice's 32 blocks
 // on one XCD sweep it together. Per pair: the candidate row from global (8 KB), the query from LDS (8 KB), the
 // relation third from a small global table (L2-resident).
-template <int R, int NWV, int DEPTH>
+template <int R, int NWV, int DEPTH, bool Q2LDS = false>
 __global__ __launch_bounds__(NWV * 64) void tile_pairs(const float* __restrict__ tab, const float* __restrict__ qbuf,
                                                        const float* __restrict__ rel, const int* __restrict__ off,
                                                        const int* __restrict__ pe, const int* __restrict__ pb,
                                                        float* __restrict__ out) {
     __shared__ float4 q[R][2][64 * GH];
+    __shared__ float4 q2s[Q2LDS ? 3 : 1][64 * GH];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int blk = blockIdx.x, grp = blk / 8;
     for (int i = t; i < R * 2 * 64 * GH; i += NWV * 64) {
@@ -195,12 +196,28 @@ __global__ __launch_bounds__(NWV * 64) void tile_pairs(const float* __restrict__
         q[r][hf][k] = k < 250 ? reinterpret_cast<const float4*>(qbuf)[(int64_t)(grp * R + r) * 500 + hf * 250 + k]
                               : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    if constexpr (Q2LDS)
+        for (int i = t; i < 3 * 64 * GH; i += NWV * 64) {
+            const int sl = i / (64 * GH), k = i % (64 * GH);
+            q2s[sl][k] = k < 250 ? reinterpret_cast<const float4*>(rel)[sl * 250 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     __syncthreads();
     const int lo = off[blk], hi = off[blk + 1];
     const uint32_t hb = 1000 * 4;
     auto score = [&](const Half& ea, const Half& eb, int b) {
         Half q2;
-        load_half(q2, rel + (int64_t)((grp * R + b) % 11) * 1000, lane, hb);
+        if constexpr (Q2LDS) {
+#pragma unroll
+            for (int k = 0; k < GH; ++k) {
+                const float4 v = q2s[b % 3][lane + 64 * k];
+                q2.a[k][0] = v.x;
+                q2.a[k][1] = v.y;
+                q2.a[k][2] = v.z;
+                q2.a[k][3] = v.w;
+            }
+        } else {
+            load_half(q2, rel + (int64_t)((grp * R + b) % 11) * 1000, lane, hb);
+        }
         float s = 0.f;
 #pragma unroll
         for (int k = 0; k < GH; ++k) {
@@ -252,6 +269,91 @@ __global__ __launch_bounds__(NWV * 64) void tile_pairs(const float* __restrict__
             }
         }
         if (lane < nc) out[my] = mine;
+    }
+}
+
+// tile_pairs with the XCD's waves paced together: the block's sorted pairs are cut into NG entity groups
+// (group g: entities [g S / NG, (g + 1) S / NG) of the slice); a wave starts group g only when every wave of
+// its XCD has finished group g - L - 1 (per-(XCD, group) counters, agent-scope atomics; the wait is bounded,
+// so pacing never deadlocks, it only bounds the spread of the fronts to L + 1 groups). Counters accumulate
+// over launches: launch `epoch` (0-based) waits for nwx * (epoch + 1).
+template <int R, int NWV, int NG, int L>
+__global__ __launch_bounds__(NWV * 64) void tile_pairs_sync(const float* __restrict__ tab,
+                                                            const float* __restrict__ qbuf,
+                                                            const float* __restrict__ rel, const int* __restrict__ goff,
+                                                            const int* __restrict__ pe, const int* __restrict__ pb,
+                                                            float* __restrict__ out, int* sync, int nwx, int epoch) {
+    __shared__ float4 q[R][2][64 * GH];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int blk = blockIdx.x, grp = blk / 8, x = blk % 8;
+    for (int i = t; i < R * 2 * 64 * GH; i += NWV * 64) {
+        const int r = i / (2 * 64 * GH), j = i % (2 * 64 * GH), hf = j / (64 * GH), k = j % (64 * GH);
+        q[r][hf][k] = k < 250 ? reinterpret_cast<const float4*>(qbuf)[(int64_t)(grp * R + r) * 500 + hf * 250 + k]
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const uint32_t hb = 1000 * 4;
+    auto score = [&](const Half& ea, const Half& eb, int b) {
+        Half q2;
+        load_half(q2, rel + (int64_t)((grp * R + b) % 11) * 1000, lane, hb);
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < GH; ++k) {
+            const float4 a = q[b][0][lane + 64 * k], c = q[b][1][lane + 64 * k];
+            s += fabsf(a.x * eb.a[k][0] - ea.a[k][0] * c.x + q2.a[k][0]);
+            s += fabsf(a.y * eb.a[k][1] - ea.a[k][1] * c.y + q2.a[k][1]);
+            s += fabsf(a.z * eb.a[k][2] - ea.a[k][2] * c.z + q2.a[k][2]);
+            s += fabsf(a.w * eb.a[k][3] - ea.a[k][3] * c.w + q2.a[k][3]);
+        }
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        return s;
+    };
+    for (int g = 0; g < NG; ++g) {
+        if (g > L) {
+            int* c = sync + x * NG + (g - L - 1);
+            const int want = nwx * (epoch + 1);
+            int polls = 0;
+            int v = 0;
+            if (lane == 0) v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = __shfl(v, 0);
+            while (v < want && polls < 4000) {
+                __builtin_amdgcn_s_sleep(4);
+                ++polls;
+                if (lane == 0) v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v = __shfl(v, 0);
+            }
+        }
+        const int lo = goff[blk * (NG + 1) + g], hi = goff[blk * (NG + 1) + g + 1];
+        for (int c0 = lo + wave; c0 < hi; c0 += NWV * 64) {
+            const int nc = min(64, (hi - c0 + NWV - 1) / NWV);
+            const int my = c0 + NWV * lane;
+            const int my_e = lane < nc ? pe[my] : 0, my_b = lane < nc ? pb[my] : 0;
+            float mine = 0.f;
+            Half a0, b0, a1, b1;
+            int e = __builtin_amdgcn_readlane(my_e, 0);
+            load_half(a0, tab + (int64_t)e * 2000, lane, hb);
+            load_half(b0, tab + (int64_t)e * 2000 + 1000, lane, hb);
+            for (int j = 0; j < nc; j += 2) {
+                if (j + 1 < nc) {
+                    e = __builtin_amdgcn_readlane(my_e, j + 1);
+                    load_half(a1, tab + (int64_t)e * 2000, lane, hb);
+                    load_half(b1, tab + (int64_t)e * 2000 + 1000, lane, hb);
+                }
+                float s = score(a0, b0, __builtin_amdgcn_readlane(my_b, j));
+                if (lane == j) mine = s;
+                if (j + 1 < nc) {
+                    if (j + 2 < nc) {
+                        e = __builtin_amdgcn_readlane(my_e, j + 2);
+                        load_half(a0, tab + (int64_t)e * 2000, lane, hb);
+                        load_half(b0, tab + (int64_t)e * 2000 + 1000, lane, hb);
+                    }
+                    s = score(a1, b1, __builtin_amdgcn_readlane(my_b, j + 1));
+                    if (lane == j + 1) mine = s;
+                }
+            }
+            if (lane < nc) out[my] = mine;
+        }
+        if (lane == 0) __hip_atomic_fetch_add(sync + x * NG + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -497,6 +599,67 @@ int main() {
         tiles(tile_pairs<8, 8, 2>, 8, 8, "tiles R=8, 8 waves, depth 2");
         tiles(tile_pairs<8, 16, 1>, 8, 16, "tiles R=8, 16 waves, depth 1");
         tiles(tile_pairs<4, 8, 2>, 4, 8, "tiles R=4, 8 waves, depth 2");
+        tiles(tile_pairs<16, 8, 2, true>, 16, 8, "tiles R=16, 8 waves, depth 2, q2 in LDS");
+        tiles(tile_pairs<16, 16, 1, true>, 16, 16, "tiles R=16, 16 waves, depth 1, q2 in LDS");
+        tiles(tile_pairs<16, 16, 2, true>, 16, 16, "tiles R=16, 16 waves, depth 2, q2 in LDS");
+        // paced tiles (tile_pairs_sync): R = 16 rows, 8 waves, NG entity groups, lookahead L
+        int* sync;
+        CHECK(hipMalloc(&sync, 8 * 64 * 4));
+        auto paced = [&](auto kern, int NG, const char* nm) {
+            const int R = 16, nwv = 8, ngrp = (int)(B / R), nblk = ngrp * 8;
+            std::vector<std::vector<std::pair<int, int>>> per(nblk);
+            for (int64_t i = 0; i < B * N; ++i) {
+                const int e = neg[i], b = (int)(i / N);
+                per[(b / R) * 8 + (int)(e / slice)].push_back({e, b % R});
+            }
+            std::vector<int> goff, pe, pb;
+            for (int blk = 0; blk < nblk; ++blk) {
+                auto& v = per[blk];
+                std::sort(v.begin(), v.end());
+                const int x = blk % 8;
+                size_t k = 0;
+                for (int g = 0; g < NG; ++g) {
+                    goff.push_back((int)pe.size());
+                    const int64_t ehi = x * slice + (slice * (g + 1)) / NG;
+                    while (k < v.size() && v[k].first < ehi) {
+                        pe.push_back(v[k].first);
+                        pb.push_back(v[k].second);
+                        ++k;
+                    }
+                }
+                goff.push_back((int)pe.size());
+            }
+            int *dgo, *dpe, *dpb;
+            CHECK(hipMalloc(&dgo, goff.size() * 4));
+            CHECK(hipMalloc(&dpe, pe.size() * 4));
+            CHECK(hipMalloc(&dpb, pb.size() * 4));
+            CHECK(hipMemcpy(dgo, goff.data(), goff.size() * 4, hipMemcpyHostToDevice));
+            CHECK(hipMemcpy(dpe, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+            CHECK(hipMemcpy(dpb, pb.data(), pb.size() * 4, hipMemcpyHostToDevice));
+            CHECK(hipMemset(sync, 0, 8 * 64 * 4));
+            const int nwx = ngrp * nwv;  // waves per XCD
+            hipEvent_t a, bb;
+            CHECK(hipEventCreate(&a));
+            CHECK(hipEventCreate(&bb));
+            int ep = 0;
+            for (int i = 0; i < 3; ++i, ++ep)
+                hipLaunchKernelGGL(kern, dim3(nblk), dim3(nwv * 64), 0, 0, tab, qbuf, rel, dgo, dpe, dpb, out, sync, nwx, ep);
+            CHECK(hipGetLastError());
+            CHECK(hipEventRecord(a));
+            for (int i = 0; i < 20; ++i, ++ep)
+                hipLaunchKernelGGL(kern, dim3(nblk), dim3(nwv * 64), 0, 0, tab, qbuf, rel, dgo, dpe, dpb, out, sync, nwx, ep);
+            CHECK(hipEventRecord(bb));
+            CHECK(hipEventSynchronize(bb));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, a, bb));
+            ms /= 20;
+            printf("%-44s %8.1f us  %7.0f GB/s (gathered bytes)\n", nm, ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+            CHECK(hipFree(dgo));
+            CHECK(hipFree(dpe));
+            CHECK(hipFree(dpb));
+        };
+        (void)paced;  // paced tiles (every XCD-group barrier a bounded spin): 6-17x slower, same fetched bytes
+
     }
     return 0;
 }

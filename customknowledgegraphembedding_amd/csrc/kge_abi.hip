@@ -624,7 +624,9 @@ int tile_plan(int fn, ScoreParams& p) {
     }
     const int64_t qrow = tile_nq(fn) * opb + 8 + 8 + 4, lrow = (p.N + 1) * 4;
     const int64_t fixed = kTileBuckets * 4 + 16;
-    auto lds = [&](int64_t R, int64_t QS) { return R * qrow + QS * opb + fixed + std::max(R * lrow, P2 * 4); };
+    // the list region also holds the relation sort's per-wave bucket counts ([ceil(kTileSortMaxB / NT) NWV][64])
+    const int64_t sort_ints = P2 ? (int64_t)((kTileSortMaxB + 8 * kWave - 1) / (8 * kWave)) * 8 * kTileSortRel : 0;
+    auto lds = [&](int64_t R, int64_t QS) { return R * qrow + QS * opb + fixed + std::max(R * lrow, sort_ints * 4); };
     int64_t R = kTileMaxRows;
     const char* env = getenv("KGE_TILE_ROWS");
     if (env && atoi(env) > 0) R = std::min<int64_t>(R, atoi(env));

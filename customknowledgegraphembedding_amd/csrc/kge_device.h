@@ -926,58 +926,69 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
 
     // 0. the block's batch rows: ranks [g0, g0 + nr) of the batch in (relation, row) order (p.tile_sort: InterHT,
     //    so that a block's rows share few relations and their relation thirds fit QS LDS slots), else rows g0 + r.
-    //    Bitonic sort of (relation << 20 | row) keys held in registers, element i = u NT + t: strides below 64
-    //    within the wave (shuffles), larger ones through LDS.
+    //    A stable counting sort over kTileSortRel relation buckets: row i = (u NWV + w) 64 + lane is ranked inside
+    //    its wave by ballots (one per distinct bucket of the wave), then by the bucket counts of the earlier waves.
     if (p.tile_sort) {
-        const int P2 = p.tile_sort;  // power of two >= max(B, 64), <= kTileSortMaxB
-        constexpr int MU = (kTileSortMaxB + NT - 1) / NT;
-        int key[MU];
+        constexpr int MU = (kTileSortMaxB + NT - 1) / NT, NB = kTileSortRel;
+        int* wc = list;  // [MU NWV][NB] per-wave bucket counts, then their exclusive prefixes
+        int bk[MU], wr[MU];
 #pragma unroll
         for (int u = 0; u < MU; ++u) {
             const int i = u * NT + t;
-            key[u] = INT32_MAX;
+            bk[u] = NB;
             if (i < p.B) {
                 const int64_t rr = p.r_idx ? p.r_idx[i * p.r_stride] : i;
-                const int bk = (rr >= 0 && rr < p.r_rows) ? (int)min<int64_t>(rr, kTileSortRel - 2) : kTileSortRel - 1;
-                key[u] = (bk << 20) | i;
+                bk[u] = (rr >= 0 && rr < p.r_rows) ? (int)min<int64_t>(rr, NB - 2) : NB - 1;
             }
         }
-        for (int k = 2; k <= P2; k <<= 1)
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                if (j >= kWave) {
-#pragma unroll
-                    for (int u = 0; u < MU; ++u)
-                        if (u * NT + t < P2) list[u * NT + t] = key[u];
-                    __syncthreads();
-                }
-#pragma unroll
-                for (int u = 0; u < MU; ++u) {
-                    const int i = u * NT + t;
-                    if (u * NT < P2) {  // block-uniform
-                        const int o = j >= kWave ? (i < P2 ? list[i ^ j] : INT32_MAX) : __shfl_xor(key[u], j, kWave);
-                        const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
-                        key[u] = keep_min ? min(key[u], o) : max(key[u], o);
-                    }
-                }
-                if (j >= kWave) __syncthreads();
-            }
-#pragma unroll
-        for (int u = 0; u < MU; ++u)
-            if (u * NT + t < P2) list[u * NT + t] = key[u];
+        for (int i = t; i < MU * NWV * NB; i += NT) wc[i] = 0;
         __syncthreads();
-        if (t < nr) brow[t] = list[g0 + t] & 0xFFFFF;
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            wr[u] = 0;
+            if (u * NT >= p.B) continue;  // block-uniform
+            uint64_t todo = __ballot(bk[u] < NB);
+            while (todo) {  // wave-uniform: one round per distinct bucket of the wave
+                const int v = __builtin_amdgcn_readlane(bk[u], __builtin_ctzll(todo));
+                const uint64_t m = __ballot(bk[u] == v);
+                if (bk[u] == v) wr[u] = lanes_below(m);
+                if (lane == 0) wc[(u * NWV + w) * NB + v] = __popcll(m);
+                todo &= ~m;
+            }
+        }
+        __syncthreads();
+        if (w == 0) {  // bucket v = lane: prefix over the waves in row order, then over the buckets
+            int run = 0;
+            for (int c = 0; c < MU * NWV; ++c) {
+                const int y = wc[c * NB + lane];
+                wc[c * NB + lane] = run;
+                run += y;
+            }
+            int incl = run;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const int y = __shfl_up(incl, o, kWave);
+                if (lane >= o) incl += y;
+            }
+            const int base = incl - run;
+            for (int c = 0; c < MU * NWV; ++c) wc[c * NB + lane] += base;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            if (bk[u] >= NB) continue;
+            const int64_t rank = wc[(u * NWV + w) * NB + bk[u]] + wr[u];
+            if (rank >= g0 && rank < g0 + nr) brow[rank - g0] = u * NT + t;
+        }
     } else if (t < nr) {
         brow[t] = g0 + t;
     }
     __syncthreads();
     if (p.tile_dry == 1) return;  // A/B knob KGE_TILE_DRY=<level>: the setup up to this point alone
 
-    // 1. the rows' query operands
-    for (int r = w; r < nr; r += NWV) {
-        Query<FN, CH, V, G> q;
-        int64_t qi, ri;
-        bool qok, rok;
-        build_query_for<FN, CH, V, G>(p, brow[r], lane, q, qi, ri, qok, rok);
+    // 1. the rows' query operands; with fewer waves than rows, two rows per wave built side by side (branch-free:
+    //    both rows' loads in flight together)
+    auto put = [&](int r, const Query<FN, CH, V, G>& q, int64_t ri, bool rok) {
         vecf<V>* qr = qimg + (size_t)r * NQ * W;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
@@ -985,6 +996,26 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             if constexpr (NQ > 1) qr[W + lane + k * kWave] = q.q1[k];
         }
         if (lane == 0) rrow[r] = rok ? ri : -1;
+    };
+    if constexpr (2 * NWV <= kTileMaxRows) {
+        for (int r = w; r < nr; r += 2 * NWV) {
+            const int r2 = r + NWV < nr ? r + NWV : r;
+            Query<FN, CH, V, G> qa, qb;
+            int64_t qi, ri, qi2, ri2;
+            bool qok, rok, qok2, rok2;
+            build_query_for<FN, CH, V, G>(p, brow[r], lane, qa, qi, ri, qok, rok);
+            build_query_for<FN, CH, V, G>(p, brow[r2], lane, qb, qi2, ri2, qok2, rok2);
+            put(r, qa, ri, rok);
+            if (r2 != r) put(r2, qb, ri2, rok2);
+        }
+    } else {
+        for (int r = w; r < nr; r += NWV) {
+            Query<FN, CH, V, G> q;
+            int64_t qi, ri;
+            bool qok, rok;
+            build_query_for<FN, CH, V, G>(p, brow[r], lane, q, qi, ri, qok, rok);
+            put(r, q, ri, rok);
+        }
     }
     for (int i = t; i < kTileBuckets; i += NT) hist[i] = 0;
     __syncthreads();
@@ -1084,9 +1115,12 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     }
     __syncthreads();
     if (in_regs) {
+        int at[TPI];
+#pragma unroll
+        for (int u = 0; u < TPI; ++u) at[u] = wbk[u] >= 0 ? atomicAdd(&hist[wbk[u]], 1) : -1;
 #pragma unroll
         for (int u = 0; u < TPI; ++u)
-            if (wbk[u] >= 0) list[atomicAdd(&hist[wbk[u]], 1)] = wcd[u];
+            if (at[u] >= 0) list[at[u]] = wcd[u];
     } else {
         for (int64_t f = t; f < nf; f += NT) {
             int bk, code;

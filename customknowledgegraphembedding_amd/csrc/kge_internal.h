@@ -44,7 +44,7 @@ enum Kind {
 constexpr int kTileBuckets = 256;  // entity buckets of a slice (the block's counting sort)
 constexpr int kTileMaxRows = 16;
 constexpr int kTileLdsMax = 160 * 1024;
-constexpr int kTileSortRel = 2048;   // relation buckets of the tile kernel's row sort (larger ids share one)
+constexpr int kTileSortRel = 64;     // relation buckets of the tile kernel's row sort (ids >= 62 share one)
 constexpr int kTileSortMaxB = 2048;  // batch rows the tile kernel sorts by relation in LDS
 // LDS query operands per batch row of the tile kernel (InterHT's third, the relation, is read per candidate)
 constexpr int tile_nq(int fn) { return (fn == KGE_COMPLEX || fn == KGE_ROTATE || fn == KGE_INTERHT) ? 2 : 1; }

@@ -691,8 +691,11 @@ int kge_score_indexed(int fn, int mode, const float* ent, int64_t nentity, int64
                  emb_range, modulus);
     p.out = scores;
     p.out_ld = scores_ld;
-    if (mode != KGE_SINGLE && nentity < ((int64_t)1 << 31) && use_xcd_order(nentity, N))
+    if (mode != KGE_SINGLE && nentity < ((int64_t)1 << 31) && use_xcd_order(nentity, N)) {
+        if (step_order(nentity, N) == 2 && tile_plan(fn, p))
+            return run_score(fn, mode, p, KIND_SCORE_TILE, stream);  // row-group x XCD-slice tiles (§3.0)
         return run_score(fn, mode, p, KIND_SCORE_SHARD_XCD, stream);  // XCD-sliced gather order (§3.0)
+    }
     return run_score(fn, mode, p, KIND_FWD, stream);
 }
 

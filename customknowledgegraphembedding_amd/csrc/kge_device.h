@@ -986,6 +986,43 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     __syncthreads();
     if (p.tile_dry == 1) return;  // A/B knob KGE_TILE_DRY=<level>: the setup up to this point alone
 
+    // 2. counting sort of the block's items of slice x by entity bucket
+    const int64_t nf = (int64_t)nr * Np;
+    // no 64-bit divisions in the walk (an emulated int64 divide is ~100 instructions): the item's row by a
+    // float reciprocal corrected to the exact quotient (f < R (N + 1) < 2^21), the entity bucket by a float
+    // scale (any monotone map of the slice onto the buckets orders the sweep)
+    const int Np32 = (int)Np;
+    const float inv_np = 1.f / (float)Np32, bscale = (float)kTileBuckets / (float)S;
+    auto item = [&](int64_t f64, int& bucket, int& code) -> bool {
+        const int f = (int)f64;
+        int r = (int)((float)f * inv_np);
+        if (r * Np32 > f) --r;
+        if ((r + 1) * Np32 <= f) ++r;
+        const int n = f - r * Np32;
+        const int64_t b = brow[r];
+        const int64_t id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
+        const int64_t row = id - p.c_base;
+        const bool valid = row >= 0 && row < p.c_rows;
+        if (valid ? (row < e_lo || row >= e_hi) : x != 0) return false;
+        bucket = valid ? min(kTileBuckets - 1, (int)((float)(int)(row - e_lo) * bscale)) : 0;
+        code = (r << 16) | n;
+        return true;
+    };
+    // the ids are loaded once, all in flight together, when the block's walk fits TPI per thread (C2: 4 112
+    // items over 512 threads); otherwise the walk is made twice (count, then scatter)
+    constexpr int TPI = 16;
+    int wbk[TPI], wcd[TPI];
+    const bool in_regs = nf <= (int64_t)TPI * NT;  // block-uniform
+    // (their loads are issued here, before the query build, so both latencies overlap)
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < TPI; ++u) {
+            const int64_t f = (int64_t)u * NT + t;
+            wbk[u] = -1;
+            if (f < nf && !item(f, wbk[u], wcd[u])) wbk[u] = -1;
+        }
+    }
+
     // 1. the rows' query operands; with fewer waves than rows, two rows per wave built side by side (branch-free:
     //    both rows' loads in flight together)
     auto put = [&](int r, const Query<FN, CH, V, G>& q, int64_t ri, bool rok) {
@@ -1019,6 +1056,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     }
     for (int i = t; i < kTileBuckets; i += NT) hist[i] = 0;
     __syncthreads();
+    if (p.tile_dry == 2) return;
     if constexpr (FN == KGE_INTERHT) {
         // relation slots: one per run of equal relations among the block's rows (first QS runs; the rows of
         // later runs read their relation third from the table per candidate)
@@ -1033,53 +1071,8 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
                 q2slot[r] = sl < QS ? sl : -1;
             }
         }
-        __syncthreads();
-        for (int r = w; r < nr; r += NWV) {
-            const int sl = q2slot[r];
-            if (sl < 0 || (r > 0 && q2slot[r - 1] == sl)) continue;  // wave-uniform: the run's first row fills
-            const int64_t ri = rrow[r];
-            const rsrc_t sr = make_rsrc(p.rel + (ri >= 0 ? ri : 0) * p.r_ld + p.r_off, ri >= 0 ? (uint32_t)p.D * 4u : 0u);
-#pragma unroll
-            for (int k = 0; k < G; ++k) q2img[(size_t)sl * W + lane + k * kWave] = bload<V>(sr, goff<V>(lane, k));
-        }
-        __syncthreads();
     }
-
-    if (p.tile_dry == 2) return;
-    // 2. counting sort of the block's items of slice x by entity bucket
-    const int64_t nf = (int64_t)nr * Np;
-    // no 64-bit divisions in the walk (an emulated int64 divide is ~100 instructions): the item's row by a
-    // float reciprocal corrected to the exact quotient (f < R (N + 1) < 2^21), the entity bucket by a float
-    // scale (any monotone map of the slice onto the buckets orders the sweep)
-    const int Np32 = (int)Np;
-    const float inv_np = 1.f / (float)Np32, bscale = (float)kTileBuckets / (float)S;
-    auto item = [&](int64_t f64, int& bucket, int& code) -> bool {
-        const int f = (int)f64;
-        int r = (int)((float)f * inv_np);
-        if (r * Np32 > f) --r;
-        if ((r + 1) * Np32 <= f) ++r;
-        const int n = f - r * Np32;
-        const int64_t b = brow[r];
-        const int64_t id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
-        const int64_t row = id - p.c_base;
-        const bool valid = row >= 0 && row < p.c_rows;
-        if (valid ? (row < e_lo || row >= e_hi) : x != 0) return false;
-        bucket = valid ? min(kTileBuckets - 1, (int)((float)(int)(row - e_lo) * bscale)) : 0;
-        code = (r << 16) | n;
-        return true;
-    };
-    // the ids are loaded once, all in flight together, when the block's walk fits TPI per thread (C2: 4 112
-    // items over 512 threads); otherwise the walk is made twice (count, then scatter)
-    constexpr int TPI = 16;
-    int wbk[TPI], wcd[TPI];
-    const bool in_regs = nf <= (int64_t)TPI * NT;  // block-uniform
     if (in_regs) {
-#pragma unroll
-        for (int u = 0; u < TPI; ++u) {
-            const int64_t f = (int64_t)u * NT + t;
-            wbk[u] = -1;
-            if (f < nf && !item(f, wbk[u], wcd[u])) wbk[u] = -1;
-        }
 #pragma unroll
         for (int u = 0; u < TPI; ++u)
             if (wbk[u] >= 0) atomicAdd(&hist[wbk[u]], 1);
@@ -1091,6 +1084,16 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     }
     __syncthreads();
     if (p.tile_dry == 3) return;
+    if constexpr (FN == KGE_INTERHT) {
+        for (int r = w; r < nr; r += NWV) {
+            const int sl = q2slot[r];
+            if (sl < 0 || (r > 0 && q2slot[r - 1] == sl)) continue;  // wave-uniform: the run's first row fills
+            const int64_t ri = rrow[r];
+            const rsrc_t sr = make_rsrc(p.rel + (ri >= 0 ? ri : 0) * p.r_ld + p.r_off, ri >= 0 ? (uint32_t)p.D * 4u : 0u);
+#pragma unroll
+            for (int k = 0; k < G; ++k) q2img[(size_t)sl * W + lane + k * kWave] = bload<V>(sr, goff<V>(lane, k));
+        }
+    }
     if (w == 0) {  // exclusive scan of the bucket counts (4 per lane)
         constexpr int PL = kTileBuckets / kWave;
         int v[PL], s = 0;

@@ -87,6 +87,30 @@ def test_tile_bitwise_equals_row_and_xcd(name, mode):
         assert _same(_run(m, mode, pos, neg, "tile", rows), want), rows
 
 
+@pytest.mark.parametrize("name", FNS)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_score_indexed_tile_bitwise(name, mode):
+    """kge_score_indexed (model(((pos, neg), mode)), model.py:114-205) in the tile order (no positives) equals the
+    batch-row-major scorer bitwise, out-of-range ids included."""
+    E, R, d, B, N = 2999, 6, 64, 35, 150
+    m = _model(name, E, R, d, seed=2)
+    g = torch.Generator().manual_seed(13)
+    pos = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(0, R, (B,), generator=g),
+                       torch.randint(0, E, (B,), generator=g)], 1)
+    neg = torch.randint(0, E, (B, N), generator=g)
+    neg[2, :3] = torch.tensor([-5, E, E + 1])
+    pos, neg = pos.to(DEV), neg.to(DEV)
+    mod = float(m.modulus.detach().reshape(-1)[0]) if name == "pRotatE" else 0.0
+    outs = []
+    for order in ("row", "tile", "xcd"):
+        with _env(KGE_STEP_ORDER=order):
+            outs.append(ops.score_indexed_raw(FN_IDS[name], mode, m.entity_embedding.detach(),
+                                              m.relation_embedding.detach(), m._rel_off, pos, neg, m._D, m._gamma_f,
+                                              m._range_f, mod))
+        torch.cuda.synchronize()
+    assert _same([outs[1]], [outs[0]]) and _same([outs[2]], [outs[0]])
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_tile_skewed_ids_one_slice_and_tiny_shapes(mode):
     """Every candidate in slice 0 (one block of each row group holds all R (N + 1) items), duplicates of

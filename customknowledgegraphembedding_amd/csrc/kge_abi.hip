@@ -637,12 +637,14 @@ int tile_plan(int fn, ScoreParams& p) {
         while (QS < R && lds(R, QS + 1) <= kTileLdsMax) ++QS;
     const char* qenv = getenv("KGE_TILE_Q2SLOTS");
     if (qenv) QS = std::min<int64_t>(QS, std::max(0, atoi(qenv)));
-    // waves per block: candidate rows of 4 KB or more keep 2 x 8 rows in flight per CU at 8 waves (two
-    // rows deep each); smaller rows need 16 waves for the same bytes in flight. KGE_TILE_WAVES overrides.
+    // waves per block (each two candidate rows deep): 12 for candidate rows of 4 KB or more (3 waves per SIMD
+    // at <= 168 VGPRs; C2 InterHT 105 -> 95 us and C3 RotatE 124-131 -> 115-120 us against 8 waves, whose
+    // 2 waves per SIMD leave the score's VALU exposed; 16 spills), 16 for smaller rows (C4 DistMult: 2 KB rows
+    // need the waves for bytes in flight). KGE_TILE_WAVES overrides (8, 12, 16).
     const int64_t row_bytes = (int64_t)p.D * 4 * (is_split(fn) ? 2 : 1);
-    p.tile_waves = row_bytes >= 4096 ? 8 : 16;
+    p.tile_waves = row_bytes >= 4096 ? 12 : 16;
     const char* wenv = getenv("KGE_TILE_WAVES");
-    if (wenv && (atoi(wenv) == 8 || atoi(wenv) == 16)) p.tile_waves = atoi(wenv);
+    if (wenv && (atoi(wenv) == 8 || atoi(wenv) == 12 || atoi(wenv) == 16)) p.tile_waves = atoi(wenv);
     p.tile_dry = getenv("KGE_TILE_DRY") ? std::max(1, atoi(getenv("KGE_TILE_DRY"))) : 0;
     if (getenv("KGE_TILE_NOSORT")) P2 = 0;
     p.tile_rows = (int)R;

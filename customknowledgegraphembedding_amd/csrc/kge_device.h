@@ -882,8 +882,8 @@ step_fwd_xcd_kernel(ScoreParams p) {
 //   2. the rows' candidates that fall in slice x (slice 0 also takes the out-of-range ids, which score
 //      against a zero row), plus, with tile_pos, each row's positive whose tail falls there, are counting-
 //      sorted into kTileBuckets entity buckets in LDS (order inside a bucket: arbitrary);
-//   3. the block's NWV waves (8 for candidate rows of 4 KB or more, else 16) take the sorted list round-robin,
-//      two candidate rows in flight per wave.
+//   3. the block's NWV waves (12 for candidate rows of 4 KB or more, else 16) take the sorted list round-robin,
+//      two candidate rows in flight per wave; head-batch positives (their own (h, r) query) after the sweep.
 // The block sweeps its slice in ONE ascending front, and the ~32 blocks of an XCD sweep the same slice
 // together, so the ~3.4 gathers of an entity row (C2) are issued by one XCD close in time and the repeats
 // hit its L2. Against step_fwd_xcd_kernel (one wave per (row, slice, phase), which rebuilds its row's query
@@ -922,7 +922,9 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     if (nr <= 0) return;  // block-uniform
     const int64_t S = (p.c_rows + 7) / 8;
     const int64_t e_lo = min((int64_t)x * S, p.c_rows), e_hi = min(p.c_rows, e_lo + S);
-    const int64_t Np = p.tile_pos ? p.N + 1 : p.N;  // column N: the row's positive (its tail)
+    // column N: the row's positive (its tail) in tail-batch mode, where it shares the negatives' query; head-batch
+    // positives need their own (h, r) query and are scored after the sweep
+    const int64_t Np = (p.tile_pos && !CH) ? p.N + 1 : p.N;
 
     // 0. the block's batch rows: ranks [g0, g0 + nr) of the batch in (relation, row) order (p.tile_sort: InterHT,
     //    so that a block's rows share few relations and their relation thirds fit QS LDS slots), else rows g0 + r.
@@ -1172,16 +1174,8 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             const int cj = __builtin_amdgcn_readlane(code, j);
             const int r = cj >> 16, n = cj & 0xFFFF;
             const vecf<V>* qr = qimg + (size_t)r * NQ * W;
-            if (CH && n == p.N) {
-                // head-batch positive: the single-mode (h, r) query, tail formula (model.py:127-146)
-                Query<FN, false, V, G> qp;
-                const int64_t b = brow[r];
-                const int64_t hi = p.pos_base[b * 3], rj = p.pos_base[b * 3 + 1];
-                const bool hok = hi >= 0 && hi < p.q_rows, rjok = rj >= 0 && rj < p.r_rows;
-                qp.build(p.qent + (hok ? hi : 0) * p.q_ld, hok, p.rel + (rjok ? rj : 0) * p.r_ld + p.r_off, rjok, p.D,
-                         lane, p);
-                return cand_score<FN, false, V, G>(it.c, qp, p);
-            } else if constexpr (FN == KGE_INTERHT) {
+            (void)n;
+            if constexpr (FN == KGE_INTERHT) {
                 TileQueryIH<V, G> q{{qr, lane}, {qr + W, lane}, {}};
 #pragma unroll
                 for (int k = 0; k < G; ++k) q.q2[k] = it.q2[k];
@@ -1221,6 +1215,30 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             } else {
                 if (p.out_pos_raw) p.out_pos_raw[b] = my_score;
                 p.out_pos_ls[b] = log_sigmoid(my_score);
+            }
+        }
+    }
+    if constexpr (CH) {
+        if (!p.tile_pos) return;
+        // head-batch positives whose tail falls in this slice: the single-mode (h, r) query, tail formula
+        // (model.py:127-146), one wave per row
+        for (int r = w; r < nr; r += NWV) {
+            const int64_t b = brow[r];
+            const int64_t tt = p.pos_base[b * 3 + 2], row = tt - p.c_base;
+            const bool valid = row >= 0 && row < p.c_rows;
+            if (valid ? (row < e_lo || row >= e_hi) : x != 0) continue;  // wave-uniform
+            Query<FN, false, V, G> qp;
+            const int64_t hi = p.pos_base[b * 3], rj = p.pos_base[b * 3 + 1];
+            const bool hok = hi >= 0 && hi < p.q_rows, rjok = rj >= 0 && rj < p.r_rows;
+            qp.build(p.qent + (hok ? hi : 0) * p.q_ld, hok, p.rel + (rjok ? rj : 0) * p.r_ld + p.r_off, rjok, p.D,
+                     lane, p);
+            bool ok;
+            Cand<FN, V, G> c;
+            c.load(cand_row(p, tt, ok), ok, p.D, lane);
+            const float s = cand_score<FN, false, V, G>(c, qp, p);
+            if (lane == 0) {
+                if (p.out_pos_raw) p.out_pos_raw[b] = s;
+                p.out_pos_ls[b] = log_sigmoid(s);
             }
         }
     }
@@ -3305,6 +3323,8 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         if constexpr (G <= kFwdGradMaxG) {
             if (p.tile_waves == 16)
                 launch_tile<FN, CH, V, G, 16>(p, st, blocks);
+            else if (p.tile_waves == 12)
+                launch_tile<FN, CH, V, G, 12>(p, st, blocks);
             else
                 launch_tile<FN, CH, V, G, 8>(p, st, blocks);
         }

@@ -119,6 +119,28 @@ def pmc_traffic(workload, kernel_prefixes):
     return total, os.path.relpath(path, ROOT)
 
 
+def pmc_l2_requests(workload, kernel_prefixes):
+    """Bytes the kernels request from L2 per step: (TCC_HIT_sum + TCC_MISS_sum) x 128 B lines, from the same
+    PMC summary as pmc_traffic (None when it is missing or stale)."""
+    path = os.path.join(os.environ.get("KGE_PMC_DIR") or os.path.join(ROOT, "profiles"), f"pmc_{workload}.json")
+    try:
+        with open(path) as f:
+            summ = json.load(f)
+        rows = summ["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    if summ.get("source_hash") != loaded_source_hash():
+        return None
+    total = 0.0
+    for pre in kernel_prefixes:
+        got = [(r["TCC_HIT_sum"] + r["TCC_MISS_sum"]) * 128.0 for r in rows
+               if (r.get("kernel", "").startswith(pre + "<") or r.get("kernel", "") == pre) and "TCC_HIT_sum" in r]
+        if not got:
+            return None
+        total += sum(got) / len(got)
+    return total
+
+
 def roofline_hbm(step_bytes, traffic, traffic_src, kern_avg_s, **extra):
     """The HBM roofline object of a gather-bound step. `frac` is on the COUNTER bytes (the PMC passes'
     FETCH_SIZE x 2 + WRITE_SIZE of the same kernels, per launch) whenever a summary of this build
@@ -137,6 +159,22 @@ def roofline_hbm(step_bytes, traffic, traffic_src, kern_avg_s, **extra):
                   "of this build)", "frac_counter": None})
     r.update(extra)
     return r
+
+
+# the L2-served gather rate of MI355X_MICROARCH.md §"Indexed rows: gather into LDS" (rows shared by every
+# workgroup, served by the XCD's L2: 16.8-18.8 TB/s chip-wide), the ceiling of a kernel whose repeat gathers hit L2
+L2_GATHER_PEAK_GBS = 18800.0
+
+
+def l2_gather_roofline(l2_bytes, kern_avg_s):
+    """Second roofline for a gather kernel that no longer reaches HBM for most rows: bytes requested from L2
+    (PMC TCC_HIT + TCC_MISS lines) per step over the L2-served gather ceiling."""
+    if not l2_bytes:
+        return None
+    ach = l2_bytes / kern_avg_s / 1e9
+    return {"achieved": ach, "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s", "frac": ach / L2_GATHER_PEAK_GBS,
+            "l2_request_bytes_per_step": l2_bytes,
+            "peak_source": "MI355X_MICROARCH.md, indexed rows gathered from the XCD's L2: 16.8-18.8 TB/s chip-wide"}
 
 
 def dims(w):
@@ -1021,6 +1059,7 @@ def main(argv=None):
                    "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": roofline_hbm(
             step_bytes, traffic, traffic_src, kern_avg_s,
+            l2_gather=l2_gather_roofline(pmc_l2_requests(a.workload, step_kernels), kern_avg_s),
             kernel={0: "step_fwd_kernel (negatives + positives + row reductions, one launch)",
                     1: "step_fwd_xcd_kernel + neg_rows_kernel (the step's two launches: negatives and positives "
                        "gathered in XCD-sliced ascending-id order, then the row reductions)",

@@ -77,6 +77,8 @@ def test_c2_xcd_phases_bitwise():
     ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
     fn = FN_IDS[name]
     old = os.environ.get("KGE_XCD_PHASES")
+    old_order = os.environ.get("KGE_STEP_ORDER")
+    os.environ["KGE_STEP_ORDER"] = "xcd"  # the phases belong to the XCD-sliced form (the default is the tile form)
     try:
         for mode in (0, 1):
             outs = []
@@ -94,6 +96,10 @@ def test_c2_xcd_phases_bitwise():
             os.environ.pop("KGE_XCD_PHASES", None)
         else:
             os.environ["KGE_XCD_PHASES"] = old
+        if old_order is None:
+            os.environ.pop("KGE_STEP_ORDER", None)
+        else:
+            os.environ["KGE_STEP_ORDER"] = old_order
 
 
 def test_c3_fb15k237_rotate_full_size():

@@ -859,6 +859,30 @@ def dry_run(a, world, rank):
         tdist.destroy_process_group()
 
 
+SHARDED_TIMEOUT_S = float(os.environ.get("KGE_BENCH_SHARDED_TIMEOUT", "240"))
+
+
+def sharded_watchdog(line, rank, timeout_s):
+    """A timer on every rank around the row-sharded side section: if it has not finished after timeout_s
+    (a collective that never completes), rank 0 prints the headline line it already holds, with the section
+    marked as timed out, and every rank leaves with status 0 (all ranks' timers start together, after the
+    headline's barrier-bracketed measurement). Cancelled when the section returns."""
+    import threading
+
+    def fire():
+        if rank == 0:
+            line["yago3_10_rowshard_error"] = f"timeout after {timeout_s:.0f} s (collective hang); headline kept"
+            print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    t = threading.Timer(timeout_s, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def sharded_lines(line, a, world, rank, device, dist):
     """c4s beside the headline: ShardedKGE.step_forward and .train_step at this world size, and at one GPU
     the simulated 8-rank step (shard_sim_bench)."""
@@ -1076,12 +1100,18 @@ def main(argv=None):
         # the north star's YAGO3-10 row-sharded configuration at this world size (weak scaling: bz=512 per
         # rank), measured beside the headline replica metric; a failure there is recorded in the line and
         # does not cost the headline
+        # across processes the section's collectives are its first RCCL use: a hang there must not cost the
+        # headline line either (sharded_watchdog)
+        dog = sharded_watchdog(line, rank, SHARDED_TIMEOUT_S) if dist else None
         try:
             sharded_lines(line, a, world, rank, device, dist)
         except Exception as e:  # noqa: BLE001
             import traceback
             traceback.print_exc()
             line["yago3_10_rowshard_error"] = repr(e)
+        finally:
+            if dog is not None:
+                dog.cancel()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w, a.cpu_budget)
     if rank == 0:

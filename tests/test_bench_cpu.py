@@ -118,3 +118,16 @@ def test_cpu_baseline_runs_on_the_gpu_lines_inputs():
     assert np.array_equal(pos.numpy(), p0[:64]) and np.array_equal(neg.numpy(), n0[:64])
     assert "wn18rr_ids.npz" in src
     assert np.array_equal(n0, np.random.RandomState(2).randint(w["nentity"], size=(512, 256)))
+
+
+def test_sharded_watchdog_prints_the_headline_and_exits_zero():
+    """A hung row-sharded side section (its first RCCL use at N > 1) must not cost the headline: the watchdog
+    prints rank 0's line, marked, and leaves with status 0."""
+    import subprocess
+    import sys
+    code = ("import bench, time; line = {'metric': 'm', 'value': 1.0}; "
+            "bench.sharded_watchdog(line, 0, 0.5); time.sleep(30)")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["value"] == 1.0 and "timeout" in out["yago3_10_rowshard_error"]

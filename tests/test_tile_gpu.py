@@ -156,3 +156,35 @@ def test_tile_c2_full_size_bitwise(mode):
     want = _run(m, mode, pos, neg, "xcd")
     assert _same(_run(m, mode, pos, neg, "tile"), want)
     assert _same(_run(m, mode, pos, neg, "row"), want)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_tile_step_forward_graph_capture_replays_bitwise(mode):
+    """The boundary's contract (stream-async, no host sync, graph-capturable): kge_step_forward in the tile
+    form and kge_score_indexed captured into a HIP graph replay to the eager outputs bitwise."""
+    name, E, R, d, B, N = "InterHT", 3000, 7, 64, 40, 200
+    m = _model(name, E, R, d, seed=4)
+    g = torch.Generator().manual_seed(21)
+    pos = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(0, R, (B,), generator=g),
+                       torch.randint(0, E, (B,), generator=g)], 1).to(DEV)
+    neg = torch.randint(0, E, (B, N), generator=g).to(DEV)
+    ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
+
+    def call():
+        fwd = ops.step_forward_raw(FN_IDS[name], mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
+        sc = ops.score_indexed_raw(FN_IDS[name], mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
+        return list(fwd) + [sc]
+
+    with _env(KGE_STEP_ORDER="tile"):
+        want = call()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            call()  # warm-up on a side stream before capture, as torch.cuda.graph expects
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            got = call()
+        graph.replay()
+        torch.cuda.synchronize()
+    assert _same(got, want)

@@ -385,6 +385,61 @@ def rank0_step_parts(ranks, pos, neg, mode, chunks=None):
             "finish": lambda: HK.shard_finish(r0, plan, recv, pos, neg, 1.0, True)}
 
 
+class _PrefilledComm:
+    """One rank's communicator stand-in for measuring its host cost: every collective returns at once and
+    its output buffers keep what they hold (the scores computed from them are garbage; only the host time
+    is read). No other rank exists, so no other thread contends for the GIL."""
+
+    def __init__(self, world, rank):
+        self.world, self.rank = world, rank
+
+    def all_to_all(self, out, inp, out_splits, in_splits, async_op=False):
+        from customknowledgegraphembedding_amd.distributed import _Done
+        return _Done()
+
+
+def rank_host_cost(tables, world, device, steps=20):
+    """CPU time one rank's thread spends issuing ShardedKGE.step_forward at `world` ranks (full C4 size): one
+    real rank (rank 0) with a prefilled-buffer communicator, the device held behind a sleep kernel so that no
+    host call waits for the GPU. Returns per-step microseconds of the plan made a step ahead (plan) and of
+    the step given that plan (step), and whether the device was still held when the host finished (if not,
+    the host waited and the figure is an upper bound)."""
+    from customknowledgegraphembedding_amd.distributed import ShardedKGE
+    w = WORKLOADS["c4s"]
+    sk = ShardedKGE("DistMult", w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"], device=device,
+                    world=world, rank=0, comm=_PrefilledComm(world, 0), full_tables=tables)
+    batches = _global_batches(w, world, 4, device)
+    side = torch.cuda.Stream(device)
+    plans = [sk.plan(batches[i % 4][0], batches[i % 4][1], i % 2) for i in range(steps)]
+    for p in plans:
+        p.summary()  # resolved before the timed region: step_forward then never waits for the device
+    for i in range(3):
+        sk.step_forward(batches[i % 4][0], batches[i % 4][1], i % 2, plan=plans[i])
+        sk.plan(batches[i % 4][0], batches[i % 4][1], i % 2, stream=side)
+    torch.cuda.synchronize()
+
+    def held(f):
+        torch.cuda._sleep(200_000_000)  # hold the device queue (far longer than the host loop)
+        t0 = time.perf_counter()
+        f()
+        el = time.perf_counter() - t0
+        probe = torch.cuda.Event()
+        probe.record()
+        still = not probe.query()
+        torch.cuda.synchronize()
+        return el / steps * 1e6, still
+
+    plan_us, held_p = held(lambda: [sk.plan(batches[i % 4][0], batches[i % 4][1], i % 2, stream=side)
+                                    for i in range(steps)])
+    step_us, held_s = held(lambda: [sk.step_forward(batches[i % 4][0], batches[i % 4][1], i % 2, plan=plans[i])
+                                    for i in range(steps)])
+    return {"plan": plan_us, "step": step_us, "total": plan_us + step_us, "device_held_throughout": held_p and held_s,
+            "steps": steps,
+            "what": "host time of one rank's ShardedKGE.plan (next step, side stream) + step_forward(plan=...) at "
+                    f"W={world}, C4 full size; collectives stubbed (return at once), device queue held behind a "
+                    "sleep kernel: the Python + ctypes + launch cost per rank-step that an RCCL run adds to"}
+
+
 def shard_sim_bench(device, world=8, reps=10, v1=None):
     """Single-GPU evidence for the row-sharded scaling at the full C4 size (YAGO3-10
     DistMult d=500, E=123182, N=1024, global batch of world x 512 rows):
@@ -450,6 +505,7 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
            "step_wall_us_all_ranks_one_gpu": sim_wall_us,
            "rank_step_kernels_us": {"plan_side_stream": t_plan, "query_gather": t_gather, "compact_scoring": t_score,
                                     "finish": t_finish, "critical_path": rank_us},
+           "host_us_per_rank_step": rank_host_cost(tables, world, device),
            "unsharded_global_kernel_us": unsharded_us,
            "unsharded_global_step_us": step_us,
            "rank_scoring_over_unsharded": t_score / unsharded_us,
@@ -862,20 +918,28 @@ def dry_run(a, world, rank):
 SHARDED_TIMEOUT_S = float(os.environ.get("KGE_BENCH_SHARDED_TIMEOUT", "240"))
 
 
+SHARDED_TIMEOUT_STATUS = 3  # exit status of a run whose row-sharded side section hung (headline printed)
+
+
 def sharded_watchdog(line, rank, timeout_s):
     """A timer on every rank around the row-sharded side section: if it has not finished after timeout_s
     (a collective that never completes), rank 0 prints the headline line it already holds, with the section
-    marked as timed out, and every rank leaves with status 0 (all ranks' timers start together, after the
-    headline's barrier-bracketed measurement). Cancelled when the section returns."""
+    marked as timed out, and every rank leaves with status SHARDED_TIMEOUT_STATUS, so the harness can tell
+    the hang from a clean run (all ranks' timers start together, after the headline's barrier-bracketed
+    measurement). The printed text is serialised HERE, before the section starts writing into `line`, so
+    the timer thread never iterates a dict the main thread is changing. Cancelled when the section returns."""
     import threading
+
+    marked = dict(line)
+    marked["yago3_10_rowshard_error"] = f"timeout after {timeout_s:.0f} s (collective hang); headline kept"
+    text = json.dumps(marked)
 
     def fire():
         if rank == 0:
-            line["yago3_10_rowshard_error"] = f"timeout after {timeout_s:.0f} s (collective hang); headline kept"
-            print(json.dumps(line), flush=True)
+            print(text, flush=True)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(SHARDED_TIMEOUT_STATUS)
 
     t = threading.Timer(timeout_s, fire)
     t.daemon = True
@@ -1031,13 +1095,15 @@ def main(argv=None):
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [evs[g][0].elapsed_time(evs[g][1]) / ev_group for g in sorted(evs)]
-    # SURVEY §8d per-mode kernel times, after the timed region: one event pair around ev_group
-    # consecutive launches of the same mode
+    # SURVEY §8d per-mode kernel times, after the timed region, timed like kern_ms: a group of ev_group
+    # same-mode steps is queued first (untimed, it keeps the device busy), then one event pair brackets the
+    # next ev_group, so the first launch's host latency does not land inside the pair
     per_mode = {}
     for mode in (0, 1):
         e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        e[0].record()
-        for i in range(ev_group):
+        for i in range(2 * ev_group):
+            if i == ev_group:
+                e[0].record()
             pos, neg = batches[i % len(batches)]
             run_step(m, pos, neg, mode, fn)
         e[1].record()

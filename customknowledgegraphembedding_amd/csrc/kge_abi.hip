@@ -622,10 +622,20 @@ int tile_plan(int fn, ScoreParams& p) {
         P2 = kWave;
         while (P2 < p.B) P2 <<= 1;
     }
+    // waves per block (each two candidate rows deep): 12 for candidate rows of 4 KB or more (3 waves per SIMD
+    // at <= 168 VGPRs; C2 InterHT 105 -> 95 us and C3 RotatE 124-131 -> 115-120 us against 8 waves, whose
+    // 2 waves per SIMD leave the score's VALU exposed; 16 spills), 16 for smaller rows (C4 DistMult: 2 KB rows
+    // need the waves for bytes in flight). KGE_TILE_WAVES overrides (8, 12, 16).
+    const int64_t row_bytes = (int64_t)p.D * 4 * (is_split(fn) ? 2 : 1);
+    p.tile_waves = row_bytes >= 4096 ? 12 : 16;
+    const char* wenv = getenv("KGE_TILE_WAVES");
+    if (wenv && (atoi(wenv) == 8 || atoi(wenv) == 12 || atoi(wenv) == 16)) p.tile_waves = atoi(wenv);
+    const int64_t NT = (int64_t)p.tile_waves * kWave;
     const int64_t qrow = tile_nq(fn) * opb + 8 + 8 + 4, lrow = (p.N + 1) * 4;
     const int64_t fixed = kTileBuckets * 4 + 16;
-    // the list region also holds the relation sort's per-wave bucket counts ([ceil(kTileSortMaxB / NT) NWV][64])
-    const int64_t sort_ints = P2 ? (int64_t)((kTileSortMaxB + 8 * kWave - 1) / (8 * kWave)) * 8 * kTileSortRel : 0;
+    // the list region also holds the relation sort's per-wave bucket counts ([ceil(kTileSortMaxB / NT) NWV][64],
+    // step_fwd_tile_kernel step 0), sized for the block's actual wave count
+    const int64_t sort_ints = P2 ? (kTileSortMaxB + NT - 1) / NT * p.tile_waves * kTileSortRel : 0;
     auto lds = [&](int64_t R, int64_t QS) { return R * qrow + QS * opb + fixed + std::max(R * lrow, sort_ints * 4); };
     int64_t R = kTileMaxRows;
     const char* env = getenv("KGE_TILE_ROWS");
@@ -637,16 +647,12 @@ int tile_plan(int fn, ScoreParams& p) {
         while (QS < R && lds(R, QS + 1) <= kTileLdsMax) ++QS;
     const char* qenv = getenv("KGE_TILE_Q2SLOTS");
     if (qenv) QS = std::min<int64_t>(QS, std::max(0, atoi(qenv)));
-    // waves per block (each two candidate rows deep): 12 for candidate rows of 4 KB or more (3 waves per SIMD
-    // at <= 168 VGPRs; C2 InterHT 105 -> 95 us and C3 RotatE 124-131 -> 115-120 us against 8 waves, whose
-    // 2 waves per SIMD leave the score's VALU exposed; 16 spills), 16 for smaller rows (C4 DistMult: 2 KB rows
-    // need the waves for bytes in flight). KGE_TILE_WAVES overrides (8, 12, 16).
-    const int64_t row_bytes = (int64_t)p.D * 4 * (is_split(fn) ? 2 : 1);
-    p.tile_waves = row_bytes >= 4096 ? 12 : 16;
-    const char* wenv = getenv("KGE_TILE_WAVES");
-    if (wenv && (atoi(wenv) == 8 || atoi(wenv) == 12 || atoi(wenv) == 16)) p.tile_waves = atoi(wenv);
+#ifdef KGE_PROFILING_KNOBS
+    // profiling-only A/B knobs (a build with -DKGE_PROFILING_KNOBS): KGE_TILE_DRY=<level> runs the setup alone and
+    // writes no scores; KGE_TILE_NOSORT keeps the batch-row order
     p.tile_dry = getenv("KGE_TILE_DRY") ? std::max(1, atoi(getenv("KGE_TILE_DRY"))) : 0;
     if (getenv("KGE_TILE_NOSORT")) P2 = 0;
+#endif
     p.tile_rows = (int)R;
     p.tile_q2slots = (int)QS;
     p.tile_sort = (int)P2;

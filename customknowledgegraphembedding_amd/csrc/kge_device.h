@@ -473,6 +473,23 @@ __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Q& q,
                 if (nsg) nsg[k].a[i] = -sgnf(x);  // the Jacobian's sign (0 past D: x = 0 there)
             }
         // groups past D: candidate zero-loaded and query zero -> x = 0
+    } else if constexpr (FN == KGE_ROTATE && V % 2 == 0) {
+        // per-element modulus |q - c| on packed fp32 pairs and the hardware v_sqrt_f32 (1 ulp): the IEEE
+        // sqrtf expansion (denormal scaling + two Newton corrections, ~15 instructions per element) made the
+        // C3 tile kernel issue-bound (SQ_WAIT_ANY 30 % of the wave cycles, slower than C2 on the same bytes)
+        typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const vecf<V> q0 = q.q0[k], q1 = q.q1[k];
+#pragma unroll
+            for (int i = 0; i < V; i += 2) {
+                const f2 xr = f2{q0.a[i], q0.a[i + 1]} - f2{c.ca[k].a[i], c.ca[k].a[i + 1]};
+                const f2 xi = f2{q1.a[i], q1.a[i + 1]} - f2{c.cb[k].a[i], c.cb[k].a[i + 1]};
+                const f2 s2 = xr * xr + xi * xi;
+                acc += __builtin_amdgcn_sqrtf(s2.x);
+                acc += __builtin_amdgcn_sqrtf(s2.y);
+            }
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < G; ++k)
@@ -489,7 +506,7 @@ __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Q& q,
                 } else if constexpr (FN == KGE_ROTATE) {
                     const float y = c.cb[k].a[i];
                     const float xr = q.q0[k].a[i] - x, xi = q.q1[k].a[i] - y;
-                    acc += sqrtf(xr * xr + xi * xi);
+                    acc += __builtin_amdgcn_sqrtf(xr * xr + xi * xi);  // hardware sqrt, as the packed form
                 } else if constexpr (FN == KGE_PROTATE) {
                     const float pc = x / p.phase_div;
                     acc += fabsf(sinf(CH ? (pc + q.q0[k].a[i]) : (q.q0[k].a[i] - pc)));

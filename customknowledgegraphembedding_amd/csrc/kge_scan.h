@@ -83,7 +83,8 @@ constexpr int kScanK = 8;  // tiles in flight per super-tile
 typedef int scan_i4 __attribute__((ext_vector_type(4)));
 typedef unsigned scan_u4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(kScanTile) void scan_block_kernel(int* __restrict__ count, int64_t E, int* __restrict__ off,
+// (unused attribute: kge_transparse.hip includes this header for launch_exclusive_scan only)
+__global__ __launch_bounds__(kScanTile) __attribute__((unused)) void scan_block_kernel(int* __restrict__ count, int64_t E, int* __restrict__ off,
                                                                int* __restrict__ cursor, int zero, int cap) {
     constexpr int NW = kScanTile / kWave;  // 16 waves
     __shared__ int wtot[kScanK][NW];
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(kScanTile) void scan_block_kernel(int* __restrict__
 // it to each cursor it draws, and it rewrites off to the global offsets for phase 2. All tiles run at once
 // (one launch, no cross-block wait), instead of one block walking every tile.
 constexpr int kTile4k = 4 * kScanTile;
-__global__ __launch_bounds__(kScanTile) void scan_tiles4k_kernel(const int* __restrict__ count, int64_t E,
+__global__ __launch_bounds__(kScanTile) __attribute__((unused)) void scan_tiles4k_kernel(const int* __restrict__ count, int64_t E,
                                                                  int* __restrict__ off, int* __restrict__ cursor,
                                                                  int* __restrict__ tile_sum) {
     constexpr int NW = kScanTile / kWave;

@@ -479,6 +479,9 @@ class ShardedKGE:
         if isinstance(comm, ThreadComm):
             comm = comm.view(self.rank)
         self.comm = comm if comm is not None else (TorchComm(group) if self.world > 1 else None)
+        # the exchange runs through self.comm (W > 1). At W = 1 the steps skip it (it is the identity) unless a
+        # communicator was given and `exchange` is set: tests run the whole collective path under RCCL on one GPU
+        self.exchange = self.world > 1
         self.kernels = kernels or HipShardKernels()
         self.model_name = model_name
         self.fn = FN_IDS[model_name]
@@ -514,7 +517,9 @@ class ShardedKGE:
         is the model's (updated identically on every rank). Rows outside the shard go stale during
         training until `sync_entity_table` re-broadcasts every rank's block. With a ThreadComm (W
         simulated ranks of one process) each rank gets its own copy of the relation table: W in-place
-        relation updates of one shared tensor would compound."""
+        relation updates of one shared tensor would compound. Training through such a view therefore
+        leaves `model.relation_embedding` unchanged: call `sync_relation_table(model.relation_embedding)`
+        (from any one rank) to copy the replicas' table back."""
         ent = model.entity_embedding.data
         rel = model.relation_embedding.data
         if isinstance(comm, (ThreadComm, _ThreadCommRank)):
@@ -534,6 +539,13 @@ class ShardedKGE:
             if r == self.rank and blk.data_ptr() != self.shard.data_ptr():
                 blk.copy_(self.shard)
             self.comm.broadcast_(blk, r)
+        return table
+
+    def sync_relation_table(self, table):
+        """This rank's relation table -> `table` (the replicas' tables are identical after every step). With
+        a ThreadComm, from_model gave each simulated rank a copy; this writes the trained one back."""
+        if table.data_ptr() != self.relation_embedding.data_ptr():
+            table.copy_(self.relation_embedding)
         return table
 
     def configure_optimizer(self, lr=5e-5, betas=(0.9, 0.999), eps=None, semantics="keras"):
@@ -578,11 +590,13 @@ class ShardedKGE:
             raise ValueError("global batch must split evenly over ranks")
         K = default_chunks(self.world, chunks)
         if stream is None:
-            return self.kernels.plan(self, pos_g, neg_g, mode, K, flags)
-        stream.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(stream):
             p = self.kernels.plan(self, pos_g, neg_g, mode, K, flags)
-        p.stream = stream
+        else:
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(stream):
+                p = self.kernels.plan(self, pos_g, neg_g, mode, K, flags)
+            p.stream = stream
+        p.ids = (pos_g.data_ptr(), neg_g.data_ptr())  # step_forward(plan=...) checks it is this batch's plan
         return p
 
     def _exchange_queries(self, plan, pos_g):
@@ -615,7 +629,7 @@ class ShardedKGE:
         owned scores, both through self.comm. At W = 1 the exchange is the identity and the step is the
         unsharded fused forward (kge_step_forward; the same scores bitwise)."""
         W, me = self.world, self.rank
-        if W == 1:
+        if not self.exchange:
             m = ops.mode_id(mode)
             if m not in (HEAD_BATCH, TAIL_BATCH):
                 raise ValueError("step_forward needs a negative mode (0 or 1)")
@@ -626,6 +640,12 @@ class ShardedKGE:
             plan = self.plan(pos_g, neg_g, mode, chunks)
         if plan.rank != me:
             raise ValueError("the plan was made by another rank (its bucket is that rank's)")
+        if plan.mode != ops.mode_id(mode) or (plan.Bg, plan.N) != tuple(neg_g.shape):
+            raise ValueError(f"the plan was made for mode {plan.mode}, batch {plan.Bg} x {plan.N}; this step is mode "
+                             f"{ops.mode_id(mode)}, batch {tuple(neg_g.shape)}")
+        ids = getattr(plan, "ids", None)
+        if ids is not None and ids != (pos_g.data_ptr(), neg_g.data_ptr()):
+            raise ValueError("the plan was made for other pos/neg tensors than this step's")
         if getattr(plan, "stream", None) is not None:  # made on a side stream
             plan.use_on(torch.cuda.current_stream(self.device))
         K = plan.chunks
@@ -668,7 +688,7 @@ class ShardedKGE:
         Bg = pos_g.shape[0]
         rows = torch.empty((2 if ops.mode_id(mode) == HEAD_BATCH else 1, Bg, self.entity_dim), dtype=torch.float32,
                            device=self.device)
-        if self.world == 1:
+        if not self.exchange:
             for i, c in enumerate(query_cols(ops.mode_id(mode), KGE_SHARD_TWO_COLUMNS)):
                 self.kernels.gather_rows(self.shard, self.lo, pos_g[:, c:], 3, Bg, rows[i])
             return rows[0], rows[-1]
@@ -705,7 +725,7 @@ class ShardedKGE:
         k.train_forward(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w)
         stats_all = self._gather_cat(bufs["stats"])
         k.train_combine(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w, stats_all)
-        if self.world > 1:
+        if self.exchange:
             self.comm.all_reduce_sum_(bufs["dq"])
         loss = k.train_backward(self, bufs, mode, qent, qent_pos, pos_g, neg_g, w, self.step + 1, self.loss_sum)
         self.step += 1
@@ -713,7 +733,7 @@ class ShardedKGE:
         return loss[self.rank]
 
     def _gather_cat(self, t):
-        return t.unsqueeze(0) if self.world == 1 else self.comm.all_gather_cat(t)
+        return self.comm.all_gather_cat(t) if self.exchange else t.unsqueeze(0)
 
     def step_forward_gather(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True):
         """Same contract and results as step_forward (bitwise: the same rows reach the same kernel

@@ -255,3 +255,22 @@ def test_sharded_owner_computes_more_ranks_gloo(world, chunks):
     assert len(results) == world
     for r in range(world):
         assert results[r] < 1e-5, (r, results[r])
+
+
+def test_step_forward_rejects_a_plan_of_another_batch_or_mode():
+    """step_forward(plan=...) checks the plan's mode, shape and tensors against the step's (a plan made for
+    another step would give wrong scores with no error): ValueError before any collective."""
+    from shard_oracle_backend import OracleShardKernels
+    E, R, d, Bg, N = 40, 3, 8, 4, 6
+    sk = ShardedKGE("DistMult", E, R, d, 24.0, device="cpu", seed=0, world=2, rank=0, comm=object(),
+                    kernels=OracleShardKernels())
+    g = np.random.RandomState(0)
+    pos = torch.from_numpy(np.stack([g.randint(E, size=Bg), g.randint(R, size=Bg), g.randint(E, size=Bg)], 1))
+    neg = torch.from_numpy(g.randint(E, size=(Bg, N)))
+    plan = sk.plan(pos, neg, 1, chunks=1)
+    with pytest.raises(ValueError, match="mode"):
+        sk.step_forward(pos, neg, 0, plan=plan)
+    with pytest.raises(ValueError, match="other pos/neg"):
+        sk.step_forward(pos.clone(), neg.clone(), 1, plan=plan)
+    with pytest.raises(ValueError, match="batch"):
+        sk.step_forward(pos, neg[:, :N - 1].contiguous(), 1, plan=plan)

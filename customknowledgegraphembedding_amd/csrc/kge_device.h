@@ -1155,9 +1155,13 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     if (p.tile_dry) return;
     // 3. the sweep: wave w takes items w, w + NWV, w + 2 NWV, ...; with KGE_TILE_DEPTH = 2 the next item's
     // candidate row (and InterHT's relation third) is in flight while this one is scored
+    // KGE_TILE_Q2LDS: InterHT's relation third is read from its LDS slot inside the score (like q0, q1), not
+    // staged per item in registers; rows without a slot load it from the table at score time (rare: the rows
+    // are relation-sorted). Two candidate rows in flight then hold 32 fewer VGPRs.
+    constexpr bool Q2R = FN == KGE_INTERHT && !KGE_TILE_Q2LDS;
     struct Item {
         Cand<FN, V, G> c;
-        vecf<V> q2[FN == KGE_INTERHT ? G : 1];
+        vecf<V> q2[Q2R ? G : 1];
     };
     for (int c0 = w; c0 < cnt; c0 += NT) {
         const int nc = min(kWave, (cnt - c0 + NWV - 1) / NWV);
@@ -1172,7 +1176,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         auto load = [&](Item& it, int j) {
             bool ok;
             it.c.load(cand_row(p, readlane64(my_id, j), ok), ok, p.D, lane);
-            if constexpr (FN == KGE_INTERHT) {
+            if constexpr (Q2R) {
                 const int r = __builtin_amdgcn_readlane(code, j) >> 16;
                 const int sl = q2slot[r];
                 if (sl >= 0) {  // wave-uniform
@@ -1192,10 +1196,22 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             const int r = cj >> 16, n = cj & 0xFFFF;
             const vecf<V>* qr = qimg + (size_t)r * NQ * W;
             (void)n;
-            if constexpr (FN == KGE_INTERHT) {
+            if constexpr (Q2R) {
                 TileQueryIH<V, G> q{{qr, lane}, {qr + W, lane}, {}};
 #pragma unroll
                 for (int k = 0; k < G; ++k) q.q2[k] = it.q2[k];
+                return cand_score<FN, CH, V, G>(it.c, q, p);
+            } else if constexpr (FN == KGE_INTERHT) {
+                const int sl = q2slot[r];
+                if (sl >= 0) {  // wave-uniform
+                    const LdsQuery<V> q{{qr, lane}, {qr + W, lane}, {q2img + (size_t)sl * W, lane}};
+                    return cand_score<FN, CH, V, G>(it.c, q, p);
+                }
+                TileQueryIH<V, G> q{{qr, lane}, {qr + W, lane}, {}};
+                const int64_t ri = rrow[r];
+                const rsrc_t sr = make_rsrc(p.rel + (ri >= 0 ? ri : 0) * p.r_ld + p.r_off, ri >= 0 ? (uint32_t)p.D * 4u : 0u);
+#pragma unroll
+                for (int k = 0; k < G; ++k) q.q2[k] = bload<V>(sr, goff<V>(lane, k));
                 return cand_score<FN, CH, V, G>(it.c, q, p);
             } else {
                 const LdsQuery<V> q{{qr, lane}, {qr + (NQ > 1 ? W : 0), lane}, {qr, lane}};

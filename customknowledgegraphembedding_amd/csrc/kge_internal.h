@@ -41,6 +41,9 @@ enum Kind {
 #ifndef KGE_TILE_DEPTH
 #define KGE_TILE_DEPTH 2
 #endif
+#ifndef KGE_TILE_Q2LDS
+#define KGE_TILE_Q2LDS 0
+#endif
 constexpr int kTileBuckets = 256;  // entity buckets of a slice (the block's counting sort)
 constexpr int kTileMaxRows = 16;
 constexpr int kTileLdsMax = 160 * 1024;

@@ -279,6 +279,31 @@ class ShardPlan:
                 t.record_stream(stream)
         self.stream = stream
 
+    def layout(self, rank):
+        """This rank's split sizes of the forward's exchange, as Python ints (computed once per plan):
+        per chunk k, the query all-to-all (send offset and length into the all-chunk send block, received
+        rows, out / in splits in floats of ent_dim rows: set by ShardedKGE) and the score all-to-all (in
+        splits, send length, out splits, received length). The host path of step_forward reads only this."""
+        lay = self.__dict__.get("_layout")
+        if lay is not None and lay[0] == rank:
+            return lay[1]
+        tot, qtot = self.summary()
+        W, K = self.world, self.chunks
+        hpc = W // K
+        qper = qtot.sum(1).tolist()  # [K][W] query rows of chunk k owned by o
+        totl = tot.tolist()
+        k_home = rank // hpc
+        chunks = []
+        for k in range(K):
+            per = qper[k]
+            sin = [totl[h][rank] if k * hpc <= h < (k + 1) * hpc else 0 for h in range(W)]
+            sout = totl[rank] if k == k_home else [0] * W
+            chunks.append({"qper": per, "q_mine": per[rank], "q_rows": sum(per), "s_in": sin, "s_send": sum(sin),
+                           "s_out": sout, "s_recv": sum(sout)})
+        lay = {"chunks": chunks, "k_home": k_home, "q_send_rows": W * sum(c["q_mine"] for c in chunks)}
+        self._layout = (rank, lay)
+        return lay
+
     def summary(self):
         if self._parsed is None:
             if self._event is not None:
@@ -343,49 +368,52 @@ class HipShardKernels:
                          bstart)
 
     @staticmethod
-    def gather_queries(sk, plan, pos_g, k, send, qidx):
+    def gather_queries(sk, plan, pos_g, k, send, qidx, st=None):
         """Query rows this rank owns -> send (chunk k's block, or k = -1: every chunk's, back to back)."""
         rc = _lib.load().kge_shard_gather_queries(
             sk.shard.data_ptr(), sk.shard.shape[0], sk.shard.stride(0), sk.lo, pos_g.data_ptr(), plan.Bg,
             plan.chunks, k, sk.entity_dim, sk.world, sk.rank, plan.mode, plan.flags, plan.qown.data_ptr(),
             plan.qslot.data_ptr(), plan._dev.data_ptr(), send.data_ptr() if send.numel() else None, qidx.data_ptr(),
-            _st(sk.shard))
+            st if st is not None else _st(sk.shard))
         check(rc, "kge_shard_gather_queries")
 
     @staticmethod
-    def score_compact(sk, qblock, qidx, pos_g, neg_g, plan, row0, rows, send):
+    def score_compact(sk, qblock, qidx, pos_g, neg_g, plan, row0, rows, send, st=None):
         """Owned scores (negatives and positives) of rows [row0, row0 + rows) (whole homes) -> send,
-        compacted (kge_shard_score over the plan's bucket)."""
+        compacted (kge_shard_score over the plan's bucket). Row offsets into the plan's arrays are taken by
+        pointer arithmetic (no tensor slicing on the host path)."""
         if plan.rank != sk.rank or plan.bucket is None:
             raise ValueError("kge_shard_score needs a forward plan made by this rank (its bucket)")
         if send.numel() == 0:  # this rank owns none of these rows' candidates
             return
         hB = plan.Bg // sk.world
         rel = sk.relation_embedding
-        pos = pos_g[row0:row0 + rows]
+        me = sk.rank
+        bk, bs, hp, cn = plan.bucket, plan.bucket_start, plan.hpre, plan.cnt
         rc = _lib.load().kge_shard_score(
             sk.fn, plan.mode, qblock.data_ptr(), qblock.shape[0], qblock.stride(0), qidx.data_ptr(),
             rel.data_ptr(), rel.shape[0], rel.stride(0), sk.rel_off, sk.shard.data_ptr(), sk.shard.shape[0],
-            sk.shard.stride(0), sk.lo, pos.data_ptr(), rows, plan.N, sk.D, float(sk.gamma), float(sk.emb_range),
-            float(sk.modulus), plan.bucket[row0].data_ptr(), plan.bucket_start[row0].data_ptr(),
-            plan.hpre[sk.rank, row0:].data_ptr(), plan.cnt[sk.rank, row0:].data_ptr(), plan._dev.data_ptr(),
-            sk.world, sk.rank, hB, row0 // hB, send.data_ptr() if send.numel() else None, _st(sk.shard))
+            sk.shard.stride(0), sk.lo, pos_g.data_ptr() + row0 * pos_g.stride(0) * 8, rows, plan.N, sk.D,
+            float(sk.gamma), float(sk.emb_range), float(sk.modulus), bk.data_ptr() + row0 * bk.stride(0) * 4,
+            bs.data_ptr() + row0 * bs.stride(0) * 4, hp.data_ptr() + (me * hp.stride(0) + row0) * 4,
+            cn.data_ptr() + (me * cn.stride(0) + row0) * 4, plan._dev.data_ptr(), sk.world, me, hB, row0 // hB,
+            send.data_ptr(), st if st is not None else _st(sk.shard))
         check(rc, "kge_shard_score")
 
     @staticmethod
-    def shard_finish(sk, plan, recv, pos_g, neg_g, temperature, adversarial):
+    def shard_finish(sk, plan, recv, pos_g, neg_g, temperature, adversarial, st=None):
         W, r = sk.world, sk.rank
         B, N = plan.Bg // W, plan.N
-        f32 = dict(dtype=torch.float32, device=neg_g.device)
-        scores, out_neg = torch.empty((B, N), **f32), torch.empty(B, **f32)
-        pos_raw, out_pos = torch.empty(B, **f32), torch.empty(B, **f32)
+        # the four outputs in one allocation: scores [B, N], out_neg, pos_raw, out_pos [B]
+        out = torch.empty(B * (N + 3), dtype=torch.float32, device=neg_g.device)
+        base = out.data_ptr()
         rc = _lib.load().kge_shard_finish(
             recv.data_ptr() if recv.numel() else None, plan._dev.data_ptr(), plan.hpre.data_ptr(), pos_g.data_ptr(),
             neg_g.data_ptr(), neg_g.stride(0), plan.Bg, N, sk.nentity, W, r, plan.mode, float(temperature),
-            int(adversarial), scores.data_ptr(), scores.stride(0), out_neg.data_ptr(), pos_raw.data_ptr(),
-            out_pos.data_ptr(), _st(neg_g))
+            int(adversarial), base, N, base + B * N * 4, base + B * (N + 1) * 4, base + B * (N + 2) * 4,
+            st if st is not None else _st(neg_g))
         check(rc, "kge_shard_finish")
-        return out_neg, out_pos, scores
+        return out[B * N:B * (N + 1)], out[B * (N + 2):], out[:B * N].view(B, N)
 
     @staticmethod
     def step_forward(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus, temperature, adversarial):
@@ -508,6 +536,7 @@ class ShardedKGE:
         self.step = 0
         self.loss_sum = None  # optional 0-dim fp32 device tensor: the step adds W * sum(replica losses)
         self._bufs = {}
+        self._wsb = {}
         self._pin, self._pin_i = [], 0
 
     @classmethod
@@ -599,24 +628,31 @@ class ShardedKGE:
         p.ids = (pos_g.data_ptr(), neg_g.data_ptr())  # step_forward(plan=...) checks it is this batch's plan
         return p
 
-    def _exchange_queries(self, plan, pos_g):
+    def _ws(self, name, n, dtype=torch.float32):
+        """A view of n elements of this rank's persistent exchange buffer `name` (grown by 1.25x when too
+        small). Reuse across steps is stream-ordered: every collective that touches a buffer is waited for on
+        the current stream before the step returns, so the next step's kernels come after it."""
+        b = self._wsb.get(name)
+        if b is None or b.numel() < n or b.dtype != dtype:
+            b = torch.empty(max(int(n * 1.25), 1), dtype=dtype, device=self.device)
+            self._wsb[name] = b
+        return b[:n]
+
+    def _exchange_queries(self, plan, pos_g, st=None):
         """Every chunk's query rows: each owner's compacted rows sent to every rank (one gather launch for
         all chunks, then one async all-to-all per chunk). Returns [(block [rows, ent_dim], qidx [ncol,
         Bg/K] into it, handle)] per chunk and the send buffer to keep alive."""
-        W, me, K = self.world, self.rank, plan.chunks
-        _, qtot = plan.summary()
-        d = self.entity_dim
-        f32 = dict(dtype=torch.float32, device=self.device)
-        per = [[int(qtot[k, :, o].sum()) for o in range(W)] for k in range(K)]
-        send = torch.empty(sum(W * per[k][me] for k in range(K)) * d, **f32)
-        qidx = torch.empty((plan.ncol, plan.Bg), dtype=torch.int64, device=self.device)
-        self.kernels.gather_queries(self, plan, pos_g, -1, send, qidx)
+        W, K, d = self.world, plan.chunks, self.entity_dim
+        lay = plan.layout(self.rank)
+        send = self._ws("q_send", lay["q_send_rows"] * d)
+        qidx = self._ws("q_idx", plan.ncol * plan.Bg, torch.int64).view(plan.ncol, plan.Bg)
+        self.kernels.gather_queries(self, plan, pos_g, -1, send, qidx, st=st)
         Rk = plan.Bg // K
         out, at = [], 0
-        for k in range(K):
-            n = W * per[k][me] * d
-            block = torch.empty((sum(per[k]), d), **f32)
-            h = self.comm.all_to_all(block.view(-1), send[at:at + n], [p * d for p in per[k]], [per[k][me] * d] * W,
+        for k, c in enumerate(lay["chunks"]):
+            n = W * c["q_mine"] * d
+            block = self._ws(f"q_block{k}", c["q_rows"] * d).view(c["q_rows"], d)
+            h = self.comm.all_to_all(block.view(-1), send[at:at + n], [p * d for p in c["qper"]], [c["q_mine"] * d] * W,
                                      async_op=True)
             out.append((block, qidx[:, k * Rk:(k + 1) * Rk], h))
             at += n
@@ -627,7 +663,10 @@ class ShardedKGE:
         (out_neg [B], out_pos [B], scores [B, N]) for this rank's home rows [rank*B, (rank+1)*B).
         Collectives: per chunk one all-to-all of compacted query rows and one all-to-all of compacted
         owned scores, both through self.comm. At W = 1 the exchange is the identity and the step is the
-        unsharded fused forward (kge_step_forward; the same scores bitwise)."""
+        unsharded fused forward (kge_step_forward; the same scores bitwise).
+        Host path (it bounds the step at W = 8: bench rank_host_cost): the split sizes come from the plan's
+        cached layout, the exchange buffers are persistent (self._ws), the kernels get pointers and the
+        stream handle computed once."""
         W, me = self.world, self.rank
         if not self.exchange:
             m = ops.mode_id(mode)
@@ -646,32 +685,30 @@ class ShardedKGE:
         ids = getattr(plan, "ids", None)
         if ids is not None and ids != (pos_g.data_ptr(), neg_g.data_ptr()):
             raise ValueError("the plan was made for other pos/neg tensors than this step's")
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         if getattr(plan, "stream", None) is not None:  # made on a side stream
-            plan.use_on(torch.cuda.current_stream(self.device))
+            plan.use_on(cur)
+        st = cur.cuda_stream if cur is not None else None
         K = plan.chunks
-        Rk, hpc = plan.Bg // K, W // K
-        tot, _ = plan.summary()
-        k_home = me // hpc
+        Rk = plan.Bg // K
+        lay = plan.layout(me)
         # 1. every chunk's query exchange in flight before any scoring
-        qx, _qsend = self._exchange_queries(plan, pos_g)
+        qx, _qsend = self._exchange_queries(plan, pos_g, st)
         # 2. owner-computes scores per chunk, compacted per home; 3. all-to-all to the home ranks
         pending, recv = [], None
-        for k in range(K):
+        for k, c in enumerate(lay["chunks"]):
             block, qidx, h = qx[k]
             h.wait()
-            homes = range(k * hpc, (k + 1) * hpc)
-            in_splits = [int(tot[hh, me]) if hh in homes else 0 for hh in range(W)]
-            send = torch.empty(sum(in_splits), dtype=torch.float32, device=self.device)
-            self.kernels.score_compact(self, block, qidx[0], pos_g, neg_g, plan, k * Rk, Rk, send)
-            out_splits = [int(tot[me, o]) for o in range(W)] if k == k_home else [0] * W
-            out = torch.empty(sum(out_splits), dtype=torch.float32, device=self.device)
-            if k == k_home:
+            send = self._ws(f"s_send{k}", c["s_send"])
+            self.kernels.score_compact(self, block, qidx[0], pos_g, neg_g, plan, k * Rk, Rk, send, st=st)
+            out = self._ws("s_recv", c["s_recv"]) if k == lay["k_home"] else self._ws(f"s_none{k}", 0)
+            if k == lay["k_home"]:
                 recv = out
-            pending.append((self.comm.all_to_all(out, send, out_splits, in_splits, async_op=True), send, out))
-        for h, _, _ in pending:
+            pending.append(self.comm.all_to_all(out, send, c["s_out"], c["s_in"], async_op=True))
+        for h in pending:
             h.wait()
         # 4. scatter to the home rows, reductions
-        return self.kernels.shard_finish(self, plan, recv, pos_g, neg_g, temperature, adversarial)
+        return self.kernels.shard_finish(self, plan, recv, pos_g, neg_g, temperature, adversarial, st=st)
 
     def collective_bytes(self, plan):
         """Bytes this rank receives per step through the forward's collectives (payload only)."""

@@ -104,7 +104,7 @@ class OracleShardKernels:
         return bucket, start
 
     @staticmethod
-    def gather_queries(sk, plan, pos_g, k, send, qidx):
+    def gather_queries(sk, plan, pos_g, k, send, qidx, st=None):
         """send: this rank's rows [column 0 | column 1] in slot order, once per destination ([W, P, d] per
         chunk; k = -1: every chunk's block back to back); qidx [ncol, rows]: row index in the received
         block (owners' pieces in rank order)."""
@@ -133,7 +133,7 @@ class OracleShardKernels:
                             blk[dd, (int(qtot[kk, 0, me]) if c else 0) + s] = sk.shard[int(pos_g[g, col]) - sk.lo]
 
     @classmethod
-    def score_compact(cls, sk, block, qidx, pos_g, neg_g, plan, row0, rows, send):
+    def score_compact(cls, sk, block, qidx, pos_g, neg_g, plan, row0, rows, send, st=None):
         tot, _ = plan.summary()
         hB = plan.Bg // sk.world
         name = NAMES[sk.fn]
@@ -172,7 +172,7 @@ class OracleShardKernels:
                 k += 1
 
     @classmethod
-    def shard_finish(cls, sk, plan, recv, pos_g, neg_g, temperature, adversarial):
+    def shard_finish(cls, sk, plan, recv, pos_g, neg_g, temperature, adversarial, st=None):
         tot, _ = plan.summary()
         W, me, N = sk.world, sk.rank, plan.N
         B = plan.Bg // W

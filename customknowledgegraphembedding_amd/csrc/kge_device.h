@@ -20,6 +20,8 @@
 
 #include <type_traits>
 
+#include <hip/hip_cooperative_groups.h>
+
 #include "kge_internal.h"
 
 namespace kge_impl {
@@ -911,6 +913,8 @@ step_fwd_xcd_kernel(ScoreParams p) {
 // bucket counts / cursors [kTileBuckets], the item count, the sorted list [R (N + 1)] of (row << 16 | column)
 // (column N: the row's positive).
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float row_reduce_fast(const float* row, int64_t N, float T, int adversarial, int lane);
+
 template <int V, int G>
 struct TileQueryIH {  // InterHT: q0, q1 from LDS, the relation third in registers
     LdsOperand<V> q0, q1;
@@ -1252,10 +1256,9 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         }
     }
     if constexpr (CH) {
-        if (!p.tile_pos) return;
         // head-batch positives whose tail falls in this slice: the single-mode (h, r) query, tail formula
         // (model.py:127-146), one wave per row
-        for (int r = w; r < nr; r += NWV) {
+        for (int r = w; r < nr && p.tile_pos; r += NWV) {
             const int64_t b = brow[r];
             const int64_t tt = p.pos_base[b * 3 + 2], row = tt - p.c_base;
             const bool valid = row >= 0 && row < p.c_rows;
@@ -1273,6 +1276,17 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
                 if (p.out_pos_raw) p.out_pos_raw[b] = s;
                 p.out_pos_ls[b] = log_sigmoid(s);
             }
+        }
+    }
+    if (p.tile_gridsync) {
+        // cooperative launch (every block resident): after a grid barrier every row's scores are in memory, and
+        // the 8 slice blocks of a row group reduce its rows (row r by block x = r % 8, wave r / 8) in
+        // row_reduce's exact order: the neg_rows_kernel launch folded in
+        cooperative_groups::this_grid().sync();
+        for (int r = x + 8 * w; r < nr; r += 8 * NWV) {
+            const int64_t b = brow[r];
+            const float red = row_reduce_fast(p.out + b * p.out_ld, p.N, p.temperature, p.adversarial, lane);
+            if (lane == 0) p.out_neg[b] = red;
         }
     }
 }
@@ -3320,10 +3334,31 @@ namespace kge_impl {
 template <int FN, bool CH, int V, int G, int NWV>
 void launch_tile(const ScoreParams& p, hipStream_t st, int blocks) {
     // up to the whole 160 KB of a CU's LDS per block (set once per instantiation)
-    static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G, NWV>),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kTileLdsMax) == hipSuccess;
+    const void* k = reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G, NWV>);
+    static const bool lds_ok = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kTileLdsMax) == hipSuccess;
     (void)lds_ok;
+    if (p.tile_gridsync) {  // the caller checked co-residency (tile_gridsync_ok)
+        ScoreParams q = p;
+        void* args[] = {&q};
+        if (hipLaunchCooperativeKernel(k, dim3(blocks), dim3(NWV * kWave), args, (unsigned)p.tile_lds, st) != hipSuccess) {
+            (void)hipGetLastError();
+            const_cast<ScoreParams&>(p).tile_gridsync = -1;  // refused: the caller falls back to two launches
+        }
+        return;
+    }
     hipLaunchKernelGGL((step_fwd_tile_kernel<FN, CH, V, G, NWV>), dim3(blocks), dim3(NWV * kWave), p.tile_lds, st, p);
+}
+
+// blocks of step_fwd_tile_kernel<FN, CH, V, G, NWV> that can be resident at once on the current device (0 if unknown)
+template <int FN, bool CH, int V, int G, int NWV>
+int64_t tile_resident_blocks(int lds) {
+    const void* k = reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G, NWV>);
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kTileLdsMax);
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, NWV * kWave, (size_t)lds) != hipSuccess) return 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return (int64_t)per_cu * cus;
 }
 
 template <int FN, bool CH, int V, int G>
@@ -3352,6 +3387,15 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, false>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_STEP_FWD_XCD)
         hipLaunchKernelGGL((step_fwd_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
+    else if (kind == KIND_TILE_RESIDENT) {
+        // query only (no launch): p.tile_resident <- how many tile blocks of this shape fit the device at once
+        if constexpr (G <= kFwdGradMaxG) {
+            ScoreParams& q = const_cast<ScoreParams&>(p);
+            q.tile_resident = p.tile_waves == 16   ? tile_resident_blocks<FN, CH, V, G, 16>(p.tile_lds)
+                              : p.tile_waves == 12 ? tile_resident_blocks<FN, CH, V, G, 12>(p.tile_lds)
+                                                   : tile_resident_blocks<FN, CH, V, G, 8>(p.tile_lds);
+        }
+    }
     else if (kind == KIND_STEP_FWD_TILE || kind == KIND_SCORE_TILE) {
         if constexpr (G <= kFwdGradMaxG) {
             if (p.tile_waves == 16)

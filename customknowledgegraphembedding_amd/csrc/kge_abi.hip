@@ -4,9 +4,6 @@
 
 #include <algorithm>
 #include <cmath>
-#include <map>
-#include <mutex>
-#include <tuple>
 
 #include <string>
 
@@ -663,38 +660,6 @@ int tile_plan(int fn, ScoreParams& p) {
     return 1;
 }
 
-// Whether kge_step_forward's tile kernel runs as ONE cooperative launch with the row reductions after a grid
-// barrier (tile_gridsync) instead of tile kernel + neg_rows_kernel: every block of the grid must be resident at
-// once (C2: 256 blocks of 146 KB LDS, one per CU). KGE_TILE_GRIDSYNC=0 / 1 forces it off / on (A/B runs).
-bool tile_gridsync_ok(int fn, int mode, ScoreParams& p, int64_t blocks) {
-    const char* env = getenv("KGE_TILE_GRIDSYNC");
-    if (!env || atoi(env) == 0 || p.tile_dry) return false;  // every block must reach the barrier
-    int V = 1, G = 1;
-    if (pick_vg(p, V, G)) return false;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    // occupancy per (device, function, side, shape, waves, LDS), computed once
-    static std::mutex mu;
-    static std::map<std::tuple<int, int, int, int, int, int, int>, int64_t> cache;
-    const bool ch = mode == KGE_HEAD_BATCH;
-    const auto key = std::make_tuple(dev, fn, (int)ch, V, G, p.tile_waves, p.tile_lds);
-    int64_t fit = -1;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = cache.find(key);
-        if (it != cache.end()) fit = it->second;
-    }
-    if (fit < 0) {
-        ScoreParams q = p;
-        q.tile_resident = 0;
-        if (dispatch(fn, q, KIND_TILE_RESIDENT, nullptr, 0, ch, V, G)) return false;
-        fit = q.tile_resident;
-        std::lock_guard<std::mutex> lk(mu);
-        cache[key] = fit;
-    }
-    return fit > 0 && blocks <= fit;
-}
-
 }  // namespace
 
 int set_error(int code, const char* msg) { return fail(code, msg); }
@@ -795,13 +760,6 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
         // ascending-id order, then the rows' self-adversarial reductions
         if (order == 2 && tile_plan(fn, p)) {
             p.tile_pos = 1;
-            const int64_t tblocks = (B + p.tile_rows - 1) / p.tile_rows * 8;
-            if (tile_gridsync_ok(fn, mode, p, tblocks)) {
-                p.tile_gridsync = 1;  // one cooperative launch: the row reductions after a grid barrier
-                rc = run_score(fn, mode, p, KIND_STEP_FWD_TILE, stream);
-                if (rc || p.tile_gridsync == 1) return rc;
-                p.tile_gridsync = 0;  // the runtime refused the cooperative launch: two launches
-            }
             rc = run_score(fn, mode, p, KIND_STEP_FWD_TILE, stream);
         } else {
             p.xcd_phases = xcd_phases(nentity, ent_ld);

@@ -20,8 +20,6 @@
 
 #include <type_traits>
 
-#include <hip/hip_cooperative_groups.h>
-
 #include "kge_internal.h"
 
 namespace kge_impl {
@@ -913,8 +911,6 @@ step_fwd_xcd_kernel(ScoreParams p) {
 // bucket counts / cursors [kTileBuckets], the item count, the sorted list [R (N + 1)] of (row << 16 | column)
 // (column N: the row's positive).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float row_reduce_fast(const float* row, int64_t N, float T, int adversarial, int lane);
-
 template <int V, int G>
 struct TileQueryIH {  // InterHT: q0, q1 from LDS, the relation third in registers
     LdsOperand<V> q0, q1;
@@ -1159,13 +1155,9 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     if (p.tile_dry) return;
     // 3. the sweep: wave w takes items w, w + NWV, w + 2 NWV, ...; with KGE_TILE_DEPTH = 2 the next item's
     // candidate row (and InterHT's relation third) is in flight while this one is scored
-    // KGE_TILE_Q2LDS: InterHT's relation third is read from its LDS slot inside the score (like q0, q1), not
-    // staged per item in registers; rows without a slot load it from the table at score time (rare: the rows
-    // are relation-sorted). Two candidate rows in flight then hold 32 fewer VGPRs.
-    constexpr bool Q2R = FN == KGE_INTERHT && !KGE_TILE_Q2LDS;
     struct Item {
         Cand<FN, V, G> c;
-        vecf<V> q2[Q2R ? G : 1];
+        vecf<V> q2[FN == KGE_INTERHT ? G : 1];
     };
     for (int c0 = w; c0 < cnt; c0 += NT) {
         const int nc = min(kWave, (cnt - c0 + NWV - 1) / NWV);
@@ -1180,7 +1172,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         auto load = [&](Item& it, int j) {
             bool ok;
             it.c.load(cand_row(p, readlane64(my_id, j), ok), ok, p.D, lane);
-            if constexpr (Q2R) {
+            if constexpr (FN == KGE_INTERHT) {
                 const int r = __builtin_amdgcn_readlane(code, j) >> 16;
                 const int sl = q2slot[r];
                 if (sl >= 0) {  // wave-uniform
@@ -1200,22 +1192,10 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             const int r = cj >> 16, n = cj & 0xFFFF;
             const vecf<V>* qr = qimg + (size_t)r * NQ * W;
             (void)n;
-            if constexpr (Q2R) {
+            if constexpr (FN == KGE_INTERHT) {
                 TileQueryIH<V, G> q{{qr, lane}, {qr + W, lane}, {}};
 #pragma unroll
                 for (int k = 0; k < G; ++k) q.q2[k] = it.q2[k];
-                return cand_score<FN, CH, V, G>(it.c, q, p);
-            } else if constexpr (FN == KGE_INTERHT) {
-                const int sl = q2slot[r];
-                if (sl >= 0) {  // wave-uniform
-                    const LdsQuery<V> q{{qr, lane}, {qr + W, lane}, {q2img + (size_t)sl * W, lane}};
-                    return cand_score<FN, CH, V, G>(it.c, q, p);
-                }
-                TileQueryIH<V, G> q{{qr, lane}, {qr + W, lane}, {}};
-                const int64_t ri = rrow[r];
-                const rsrc_t sr = make_rsrc(p.rel + (ri >= 0 ? ri : 0) * p.r_ld + p.r_off, ri >= 0 ? (uint32_t)p.D * 4u : 0u);
-#pragma unroll
-                for (int k = 0; k < G; ++k) q.q2[k] = bload<V>(sr, goff<V>(lane, k));
                 return cand_score<FN, CH, V, G>(it.c, q, p);
             } else {
                 const LdsQuery<V> q{{qr, lane}, {qr + (NQ > 1 ? W : 0), lane}, {qr, lane}};
@@ -1256,9 +1236,10 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         }
     }
     if constexpr (CH) {
+        if (!p.tile_pos) return;
         // head-batch positives whose tail falls in this slice: the single-mode (h, r) query, tail formula
         // (model.py:127-146), one wave per row
-        for (int r = w; r < nr && p.tile_pos; r += NWV) {
+        for (int r = w; r < nr; r += NWV) {
             const int64_t b = brow[r];
             const int64_t tt = p.pos_base[b * 3 + 2], row = tt - p.c_base;
             const bool valid = row >= 0 && row < p.c_rows;
@@ -1276,17 +1257,6 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
                 if (p.out_pos_raw) p.out_pos_raw[b] = s;
                 p.out_pos_ls[b] = log_sigmoid(s);
             }
-        }
-    }
-    if (p.tile_gridsync) {
-        // cooperative launch (every block resident): after a grid barrier every row's scores are in memory, and
-        // the 8 slice blocks of a row group reduce its rows (row r by block x = r % 8, wave r / 8) in
-        // row_reduce's exact order: the neg_rows_kernel launch folded in
-        cooperative_groups::this_grid().sync();
-        for (int r = x + 8 * w; r < nr; r += 8 * NWV) {
-            const int64_t b = brow[r];
-            const float red = row_reduce_fast(p.out + b * p.out_ld, p.N, p.temperature, p.adversarial, lane);
-            if (lane == 0) p.out_neg[b] = red;
         }
     }
 }
@@ -3334,31 +3304,10 @@ namespace kge_impl {
 template <int FN, bool CH, int V, int G, int NWV>
 void launch_tile(const ScoreParams& p, hipStream_t st, int blocks) {
     // up to the whole 160 KB of a CU's LDS per block (set once per instantiation)
-    const void* k = reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G, NWV>);
-    static const bool lds_ok = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kTileLdsMax) == hipSuccess;
+    static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G, NWV>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kTileLdsMax) == hipSuccess;
     (void)lds_ok;
-    if (p.tile_gridsync) {  // the caller checked co-residency (tile_gridsync_ok)
-        ScoreParams q = p;
-        void* args[] = {&q};
-        if (hipLaunchCooperativeKernel(k, dim3(blocks), dim3(NWV * kWave), args, (unsigned)p.tile_lds, st) != hipSuccess) {
-            (void)hipGetLastError();
-            const_cast<ScoreParams&>(p).tile_gridsync = -1;  // refused: the caller falls back to two launches
-        }
-        return;
-    }
     hipLaunchKernelGGL((step_fwd_tile_kernel<FN, CH, V, G, NWV>), dim3(blocks), dim3(NWV * kWave), p.tile_lds, st, p);
-}
-
-// blocks of step_fwd_tile_kernel<FN, CH, V, G, NWV> that can be resident at once on the current device (0 if unknown)
-template <int FN, bool CH, int V, int G, int NWV>
-int64_t tile_resident_blocks(int lds) {
-    const void* k = reinterpret_cast<const void*>(step_fwd_tile_kernel<FN, CH, V, G, NWV>);
-    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kTileLdsMax);
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, NWV * kWave, (size_t)lds) != hipSuccess) return 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 0;
-    return (int64_t)per_cu * cus;
 }
 
 template <int FN, bool CH, int V, int G>
@@ -3387,15 +3336,6 @@ void launch_one(const ScoreParams& p, int kind, hipStream_t st, int blocks) {
         hipLaunchKernelGGL((step_fwd_kernel<FN, CH, V, G, false>), dim3(blocks), dim3(kBlock), 0, st, p);
     else if (kind == KIND_STEP_FWD_XCD)
         hipLaunchKernelGGL((step_fwd_xcd_kernel<FN, CH, V, G>), dim3(blocks), dim3(kBlock), 0, st, p);
-    else if (kind == KIND_TILE_RESIDENT) {
-        // query only (no launch): p.tile_resident <- how many tile blocks of this shape fit the device at once
-        if constexpr (G <= kFwdGradMaxG) {
-            ScoreParams& q = const_cast<ScoreParams&>(p);
-            q.tile_resident = p.tile_waves == 16   ? tile_resident_blocks<FN, CH, V, G, 16>(p.tile_lds)
-                              : p.tile_waves == 12 ? tile_resident_blocks<FN, CH, V, G, 12>(p.tile_lds)
-                                                   : tile_resident_blocks<FN, CH, V, G, 8>(p.tile_lds);
-        }
-    }
     else if (kind == KIND_STEP_FWD_TILE || kind == KIND_SCORE_TILE) {
         if constexpr (G <= kFwdGradMaxG) {
             if (p.tile_waves == 16)

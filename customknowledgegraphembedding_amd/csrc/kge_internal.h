@@ -37,13 +37,9 @@ enum Kind {
     KIND_STEP_FWD_TILE = 19,   // kge_step_forward's negatives + positives: row-group x XCD-slice tiles, one
                                // entity-sorted sweep per block (queries in LDS)
     KIND_SCORE_TILE = 20,      // kge_score_indexed in the same order (no positives)
-    KIND_TILE_RESIDENT = 21,   // no launch: how many step_fwd_tile_kernel blocks of this shape fit at once
 };
 #ifndef KGE_TILE_DEPTH
 #define KGE_TILE_DEPTH 2
-#endif
-#ifndef KGE_TILE_Q2LDS
-#define KGE_TILE_Q2LDS 0
 #endif
 constexpr int kTileBuckets = 256;  // entity buckets of a slice (the block's counting sort)
 constexpr int kTileMaxRows = 16;
@@ -93,8 +89,6 @@ struct ScoreParams {
     int tile_sort;        // step_fwd_tile_kernel: 0, or the power of two >= B of the (relation, row) sort
     int tile_waves;       // step_fwd_tile_kernel: waves per block (8 or 16)
     int tile_dry;         // step_fwd_tile_kernel: setup only, no scoring (A/B knob KGE_TILE_DRY)
-    int tile_gridsync;    // step_fwd_tile_kernel: cooperative launch, the row reductions after a grid barrier
-    int64_t tile_resident;  // KIND_TILE_RESIDENT's answer
     float* out;
     int64_t out_ld;
     int64_t B, N;

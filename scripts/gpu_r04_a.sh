@@ -33,8 +33,5 @@ AB="--steps 100 --warmup 10 --train-steps 0 --sharded-steps 0 --no-cpu-baseline"
 run ab_base 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_base -o run -- python3 bench.py $AB
 run ab_q2 300 env KGE_HIP_LIB=$R/abtmp/q2lds/libkge_hip.so rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_q2 -o run -- python3 bench.py $AB
 run ab_q2w16 300 env KGE_HIP_LIB=$R/abtmp/q2lds/libkge_hip.so KGE_TILE_WAVES=16 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_q2w16 -o run -- python3 bench.py $AB
-run pytest_gs 600 env KGE_TILE_GRIDSYNC=1 python3 -u -m pytest tests/test_tile_gpu.py tests/test_configs_gpu.py tests/test_parity_gpu.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread
-tail -n 1 $O/pytest_gs.log
-run ab_gs 300 env KGE_TILE_GRIDSYNC=1 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_gs -o run -- python3 bench.py $AB
 run ab_base2 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ab_base2 -o run -- python3 bench.py $AB
 echo r04a done

@@ -98,7 +98,7 @@ def test_filtered_ranks_match_oracle(name):
     test = true[:29]
     ent = m.entity_embedding.detach().cpu().double()
     rel = m.relation_embedding.detach().cpu().double()
-    mod = float(m.modulus.reshape(-1)[0]) if name == "pRotatE" else None
+    mod = float(m.modulus.detach().reshape(-1)[0]) if name == "pRotatE" else None
     for mode in ("head-batch", "tail-batch"):
         ptr, ids = evaluate.build_filter(test, mode, true)
         pos = torch.from_numpy(test).to(DEV)

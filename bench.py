@@ -307,11 +307,21 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
     elif w.get("scheme") == "gather":
         def step(b, i):
             return sk.step_forward_gather(b[0], b[1], i % 2)
+    elif sk.world > 1 and dist_on and os.environ.get("KGE_SHARD_NATIVE", "1") != "0":
+        # the native executor (one C call per rank-step, RCCL issued from C++ through its own communicator):
+        # each step also plans the next batch, on the executor's plan stream, overlapping this step
+        from customknowledgegraphembedding_amd.distributed import NativeComm
+        sk.use_native(NativeComm(device=device))
+
+        def step(b, i):
+            nb = batches[(i + 1) % 4]
+            return sk.step_forward(b[0], b[1], i % 2, nxt=(nb[0], nb[1], (i + 1) % 2))
     else:
         # the exchange plan of step i + 1 (kge_shard_plan: ownership counts and ranks from the ids, its
         # split sizes copied to the host asynchronously) is issued before step i's work, so the host
         # never waits for it; it is device work inside the timed region like the rest of the step, on a
         # side stream (KGE_PLAN_STREAM=main: the step's own stream) where it overlaps step i's scoring
+        # (the Python host path: KGE_SHARD_NATIVE=0)
         plans = {}
         side = torch.cuda.Stream(device) if os.environ.get("KGE_PLAN_STREAM", "side") == "side" else None
 
@@ -433,11 +443,56 @@ def rank_host_cost(tables, world, device, steps=20):
                                     for i in range(steps)])
     step_us, held_s = held(lambda: [sk.step_forward(batches[i % 4][0], batches[i % 4][1], i % 2, plan=plans[i])
                                     for i in range(steps)])
-    return {"plan": plan_us, "step": step_us, "total": plan_us + step_us, "device_held_throughout": held_p and held_s,
-            "steps": steps,
-            "what": "host time of one rank's ShardedKGE.plan (next step, side stream) + step_forward(plan=...) at "
-                    f"W={world}, C4 full size; collectives stubbed (return at once), device queue held behind a "
-                    "sleep kernel: the Python + ctypes + launch cost per rank-step that an RCCL run adds to"}
+    out = {"python_path": {"plan": plan_us, "step": step_us, "total": plan_us + step_us,
+                           "device_held_throughout": held_p and held_s, "steps": steps,
+                           "what": "host time of one rank's ShardedKGE.plan (next step, side stream) + "
+                                   f"step_forward(plan=...) at W={world}, C4 full size; collectives stubbed (return "
+                                   "at once), device queue held behind a sleep kernel: the Python + ctypes + launch "
+                                   "cost per rank-step, before any torch.distributed call"}}
+    out["native"] = native_host_cost(tables, world, device, batches, 4 * steps)
+    out["per_rank_step_us"] = out["native"]["step_us"]
+    return out
+
+
+def native_host_cost(tables, world, device, batches, steps):
+    """Host time of one rank's native row-sharded step (ShardedKGE.use_native: ONE C call that issues the
+    query gather, per chunk the query all-to-all, the owner-computes scoring and the score all-to-all, the
+    finish, and the NEXT batch's plan) at `world` ranks, C4 full size, collectives skipped (KGE_EXEC_PROBE;
+    an RCCL ncclAllToAllv call's own host cost is measured beside it in scripts/shard_host_probe.py). The
+    device runs the steps back to back; the host time the calls spent blocked on the plans' summaries (the
+    device pacing the host) is subtracted."""
+    from customknowledgegraphembedding_amd.distributed import ShardedKGE
+    w = WORKLOADS["c4s"]
+    sk = ShardedKGE("DistMult", w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"], device=device,
+                    world=world, rank=0, comm=_PrefilledComm(world, 0), full_tables=tables).use_native(probe=True)
+    nb = len(batches)
+
+    def run(n):
+        for i in range(n):
+            p, q, _ = batches[i % nb]
+            np_, nq, _ = batches[(i + 1) % nb]
+            sk.step_forward(p, q, i % 2, nxt=(np_, nq, (i + 1) % 2))
+
+    run(6)
+    torch.cuda.synchronize()
+    ex = next(iter(sk._native.values()))
+    lib = kge.load()
+    lib.kge_shard_exec_host_wait_us(ex.handle, 1)
+    t0 = time.perf_counter()
+    run(steps)
+    el = time.perf_counter() - t0
+    blocked = lib.kge_shard_exec_host_wait_us(ex.handle, 1)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    dev_us = (time.perf_counter() - t1) / steps * 1e6
+    ex.close()
+    return {"step_us": (el * 1e6 - blocked) / steps, "blocked_us_per_step": blocked / steps,
+            "wall_us_per_step": dev_us, "steps": steps, "chunks": ex.K,
+            "what": f"host time per rank-step of the native executor at W={world} (one ctypes call: gather, "
+                    f"{ex.K} x (query all-to-all, scoring, score all-to-all), finish, next plan), C4 full size, "
+                    "collectives skipped; wall_us_per_step: the same steps with the device pacing them"}
 
 
 def shard_sim_bench(device, world=8, reps=10, v1=None):

@@ -75,6 +75,25 @@ SIGNATURES = {
     "kge_shard_finish": (
         _c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_f, _c_i, _c_p,
                _c_i64, _c_p, _c_p, _c_p, _c_p]),
+    "kge_comm_unique_id": (_c_i, [_c_p]),
+    "kge_comm_loopback_group": (_c_p, [_c_i]),
+    "kge_comm_loopback_group_destroy": (_c_i, [_c_p]),
+    "kge_comm_loopback_init": (_c_i, [_c_p, _c_p, _c_i]),
+    "kge_comm_init": (_c_i, [_c_p, _c_p, _c_i, _c_i]),
+    "kge_comm_destroy": (_c_i, [_c_p]),
+    "kge_comm_all_to_allv": (_c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "kge_comm_all_reduce_sum": (_c_i, [_c_p, _c_p, _c_i64, _c_p]),
+    "kge_shard_exec_workspace_size": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_i, _c_i]),
+    "kge_shard_exec_host_ints": (_c_i64, [_c_i, _c_i]),
+    "kge_shard_exec_create": (
+        _c_i, [_c_p, _c_p, _c_i, _c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i, _c_i, _c_i, _c_p, _c_i64,
+               _c_p, _c_i64]),
+    "kge_shard_exec_destroy": (_c_i, [_c_p]),
+    "kge_shard_exec_host_wait_us": (ctypes.c_double, [_c_p, _c_i]),
+    "kge_shard_exec_plan": (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_p]),
+    "kge_shard_exec_step": (
+        _c_i, [_c_p, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i, _c_f, _c_f, _c_f,
+               _c_f, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p]),
     "kge_eval_query": (
         _c_i, [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
     "kge_gemm_nt": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p]),

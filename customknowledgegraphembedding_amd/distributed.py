@@ -151,6 +151,137 @@ class TorchComm:
         return out
 
 
+class NativeComm:
+    """The RCCL communicator of libkge_hip.so (kge_comm_*, csrc/kge_comm.hip): the row-sharded step's
+    collectives issued from C++ by the native executor (ShardedKGE.use_native), with no torch.distributed
+    call on the per-step path. Made collectively, one per process: rank 0's 128-byte RCCL id reaches every
+    rank through torch.distributed (`group`, any backend)."""
+
+    def __init__(self, group=None, device=None):
+        import ctypes
+        lib = _lib.load()
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        buf = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            check(lib.kge_comm_unique_id(ctypes.addressof(buf)), "kge_comm_unique_id")
+        on_dev = dist.get_backend(group) == "nccl"
+        idt = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+        if on_dev:
+            idt = idt.to(device if device is not None else torch.device("cuda", torch.cuda.current_device()))
+        dist.broadcast(idt, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        buf = ctypes.create_string_buffer(bytes(idt.cpu().tolist()), 128)
+        h = ctypes.c_void_p()
+        check(lib.kge_comm_init(ctypes.addressof(h), ctypes.addressof(buf), self.world, self.rank), "kge_comm_init")
+        self.handle = h.value
+
+    def all_to_all(self, out, inp, out_splits, in_splits, async_op=False):
+        """TorchComm.all_to_all's contract (float tensors) through ncclAllToAllv on torch's current stream."""
+        import ctypes
+        W = self.world
+        sc, rc = (ctypes.c_int64 * W)(*[int(x) for x in in_splits]), (ctypes.c_int64 * W)(*[int(x) for x in out_splits])
+        check(_lib.load().kge_comm_all_to_allv(self.handle, inp.data_ptr(), ctypes.addressof(sc), out.data_ptr(),
+                                               ctypes.addressof(rc), _st(inp)), "kge_comm_all_to_allv")
+        return _Done()
+
+    def all_reduce_sum_(self, t, async_op=False):
+        check(_lib.load().kge_comm_all_reduce_sum(self.handle, t.data_ptr(), t.numel(), _st(t)), "kge_comm_all_reduce_sum")
+        return _Done() if async_op else t
+
+    def close(self):
+        if getattr(self, "handle", None):
+            check(_lib.load().kge_comm_destroy(self.handle), "kge_comm_destroy")
+            self.handle = None
+
+
+class _NativeHandle:
+    def __init__(self, handle, world, rank):
+        self.handle, self.world, self.rank = handle, world, rank
+
+
+class LoopbackGroup:
+    """W native communicators of ONE process (kge_comm_loopback_*): the native executor's W-rank step on
+    one GPU, one host thread per rank (run_threads) and one compute stream per rank (ranks sharing a stream
+    would wait on each other's queued work), as ThreadComm runs the Python path. comm(r) -> rank r's."""
+
+    def __init__(self, world):
+        import ctypes
+        lib = _lib.load()
+        self.world = world
+        self._g = lib.kge_comm_loopback_group(world)
+        if not self._g:
+            check(-22, "kge_comm_loopback_group")
+        self._comms = []
+        for r in range(world):
+            h = ctypes.c_void_p()
+            check(lib.kge_comm_loopback_init(ctypes.addressof(h), self._g, r), "kge_comm_loopback_init")
+            self._comms.append(_NativeHandle(h.value, world, r))
+
+    def comm(self, rank):
+        return self._comms[rank]
+
+    def close(self):
+        lib = _lib.load()
+        for c in self._comms:
+            check(lib.kge_comm_destroy(c.handle), "kge_comm_destroy")
+        self._comms = []
+        if self._g:
+            check(lib.kge_comm_loopback_group_destroy(self._g), "kge_comm_loopback_group_destroy")
+            self._g = None
+
+
+class NativeShardExec:
+    """One rank's row-sharded forward step as ONE C call (kge_shard_exec_*, csrc/kge_comm.hip): the plan of
+    the next batch, the query exchange, owner-computes scoring, the score exchange and the finish, with the
+    collectives on the executor's communication stream (RCCL through `comm`, a NativeComm) and the step's
+    kernels on torch's current stream. comm None: world 1 (the pieces are device copies), or `probe` at any
+    world (collectives skipped, outputs meaningless: the host-cost probe). The workspace and the pinned
+    summary buffers are torch allocations owned here."""
+
+    def __init__(self, sk, Bg, N, comm=None, probe=False, chunks=None):
+        import ctypes
+        lib = _lib.load()
+        W, K = sk.world, default_chunks(sk.world, chunks)
+        self.lib, self.Bg, self.N, self.B, self.K = lib, Bg, N, Bg // W, K
+        nbytes = lib.kge_shard_exec_workspace_size(Bg, N, sk.entity_dim, W, K)
+        check(int(nbytes) if nbytes < 0 else 0, "kge_shard_exec_workspace_size")
+        self.ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=sk.device)
+        ws = (self.ws.data_ptr() + 255) & ~255
+        hi = lib.kge_shard_exec_host_ints(W, K)
+        self.host = torch.empty(hi, dtype=torch.int32, pin_memory=True)
+        h = ctypes.c_void_p()
+        check(lib.kge_shard_exec_create(ctypes.addressof(h), None if comm is None else comm.handle, 1 if probe else 0,
+                                        sk.fn, sk.nentity, sk.shard.shape[0], sk.entity_dim, sk.D, Bg, N, W, sk.rank,
+                                        K, ws, nbytes, self.host.data_ptr(), hi), "kge_shard_exec_create")
+        self.handle = h.value
+        self.sk = sk
+        self.comm = comm
+
+    def plan(self, pos_g, neg_g, mode):
+        check(self.lib.kge_shard_exec_plan(self.handle, pos_g.data_ptr(), neg_g.data_ptr(), neg_g.stride(0), mode,
+                                           _st(neg_g)), "kge_shard_exec_plan")
+
+    def step(self, pos_g, neg_g, mode, temperature, adversarial, nxt=None):
+        sk, B, N = self.sk, self.B, self.N
+        out = torch.empty(B * (N + 3), dtype=torch.float32, device=sk.device)
+        base = out.data_ptr()
+        sh, rel = sk.shard, sk.relation_embedding
+        npos, nneg, nmode = (nxt[0].data_ptr(), nxt[1].data_ptr(), nxt[2]) if nxt is not None else (None, None, 0)
+        check(self.lib.kge_shard_exec_step(
+            self.handle, sh.data_ptr(), sh.stride(0), sk.lo, rel.data_ptr(), rel.shape[0], rel.stride(0), sk.rel_off,
+            pos_g.data_ptr(), neg_g.data_ptr(), neg_g.stride(0), mode, sk.gamma, sk.emb_range, sk.modulus,
+            temperature, int(adversarial), npos, nneg, nmode, base, N, base + B * N * 4, base + B * (N + 1) * 4,
+            base + B * (N + 2) * 4, _st(sh)), "kge_shard_exec_step")
+        return out[B * N:B * (N + 1)], out[B * (N + 2):], out[:B * N].view(B, N)
+
+    def close(self):
+        """Destroys the executor (its streams and events); its buffers go with this object. Not done at
+        garbage collection: an executor left open at exit is reclaimed with the process."""
+        if getattr(self, "handle", None):
+            torch.cuda.synchronize(self.sk.device)
+            check(self.lib.kge_shard_exec_destroy(self.handle), "kge_shard_exec_destroy")
+            self.handle = None
+
+
 class ThreadComm:
     """The same collectives between W threads of ONE process (one Python thread per simulated rank,
     all on one device and stream): used to run the W-rank sharded steps on a single GPU. Sums are
@@ -537,6 +668,7 @@ class ShardedKGE:
         self.loss_sum = None  # optional 0-dim fp32 device tensor: the step adds W * sum(replica losses)
         self._bufs = {}
         self._wsb = {}
+        self._native_cfg, self._native = None, {}
         self._pin, self._pin_i = [], 0
 
     @classmethod
@@ -658,7 +790,38 @@ class ShardedKGE:
             at += n
         return out, send
 
-    def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None, plan=None):
+    def use_native(self, comm=None, probe=False):
+        """Run step_forward through the native executor (NativeShardExec: one C call per rank-step, RCCL
+        issued from C++): `comm` a NativeComm (W > 1, or W = 1 through RCCL), None at W = 1 (device copies),
+        or `probe` (collectives skipped: host-cost measurement only). One executor per batch shape."""
+        if comm is None and self.world > 1 and not probe:
+            raise ValueError("the native executor needs a NativeComm at world > 1")
+        self._native_cfg = (comm, bool(probe))
+        self._native = {}
+        return self
+
+    def _native_step(self, pos_g, neg_g, mode, temperature, adversarial, chunks, nxt):
+        m = ops.mode_id(mode)
+        if m not in (HEAD_BATCH, TAIL_BATCH):
+            raise ValueError("the sharded step needs a negative mode (0 or 1)")
+        Bg, N = neg_g.shape
+        if Bg % self.world:
+            raise ValueError("global batch must split evenly over ranks")
+        if pos_g.stride() != (3, 1) or neg_g.stride(1) != 1:
+            raise ValueError("the native step needs contiguous pos [Bg, 3] and row-major neg [Bg, N]")
+        key = (Bg, N, default_chunks(self.world, chunks))
+        ex = self._native.get(key)
+        if ex is None:
+            comm, probe = self._native_cfg
+            ex = self._native[key] = NativeShardExec(self, Bg, N, comm=comm, probe=probe, chunks=chunks)
+        if nxt is not None:
+            nm = ops.mode_id(nxt[2])
+            if tuple(nxt[1].shape) != (Bg, N) or nxt[0].stride() != (3, 1) or nxt[1].stride(1) != 1:
+                raise ValueError("the next batch must have this batch's shape and layout")
+            nxt = (nxt[0], nxt[1], nm)
+        return ex.step(pos_g, neg_g, m, temperature, adversarial, nxt)
+
+    def step_forward(self, pos_g, neg_g, mode, temperature=1.0, adversarial=True, chunks=None, plan=None, nxt=None):
         """pos_g [W*B, 3], neg_g [W*B, N] (the global batch, identical on every rank) ->
         (out_neg [B], out_pos [B], scores [B, N]) for this rank's home rows [rank*B, (rank+1)*B).
         Collectives: per chunk one all-to-all of compacted query rows and one all-to-all of compacted
@@ -666,8 +829,12 @@ class ShardedKGE:
         unsharded fused forward (kge_step_forward; the same scores bitwise).
         Host path (it bounds the step at W = 8: bench rank_host_cost): the split sizes come from the plan's
         cached layout, the exchange buffers are persistent (self._ws), the kernels get pointers and the
-        stream handle computed once."""
+        stream handle computed once.
+        After use_native(...) the whole step is one C call (NativeShardExec; `plan` must then be None):
+        `nxt` = (pos, neg, mode) of the next batch, whose plan that call makes on the side (plan-ahead)."""
         W, me = self.world, self.rank
+        if self._native_cfg is not None and plan is None:
+            return self._native_step(pos_g, neg_g, mode, temperature, adversarial, chunks, nxt)
         if not self.exchange:
             m = ops.mode_id(mode)
             if m not in (HEAD_BATCH, TAIL_BATCH):

@@ -21,7 +21,7 @@ def main():
     from customknowledgegraphembedding_amd import ops
     from customknowledgegraphembedding_amd._lib import FN_IDS
     from customknowledgegraphembedding_amd.model import TFKGEModel
-    bench.ops, bench.FN_IDS = ops, FN_IDS
+    bench.ops, bench.FN_IDS, bench.kge = ops, FN_IDS, customknowledgegraphembedding_amd
     device = torch.device("cuda", 0)
     w = bench.WORKLOADS["c4s"]
     full = TFKGEModel("DistMult", w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"], device=device, seed=0)
@@ -65,6 +65,29 @@ def main():
     torch.cuda.synchronize()
     print(json.dumps({"rccl_all_to_all_host_us_per_call": (t1 - t0) / n * 1e6,
                       "rccl_wait_host_us_per_call": (t2 - t1) / n * 1e6, "device_held": held}), flush=True)
+    # the same all-to-all through the native communicator (kge_comm_all_to_allv: ncclAllToAllv from C++)
+    from customknowledgegraphembedding_amd.distributed import NativeComm
+    nc = NativeComm(device=device)
+    for _ in range(5):
+        nc.all_to_all(y, x, [x.numel()], [x.numel()])
+    torch.cuda.synchronize()
+    lib = customknowledgegraphembedding_amd.load()
+    import ctypes
+    sc = (ctypes.c_int64 * 1)(x.numel())
+    st = torch.cuda.current_stream().cuda_stream
+    torch.cuda._sleep(200_000_000)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        lib.kge_comm_all_to_allv(nc.handle, x.data_ptr(), ctypes.addressof(sc), y.data_ptr(), ctypes.addressof(sc), st)
+    t1 = time.perf_counter()
+    ev = torch.cuda.Event()
+    ev.record()
+    held = not ev.query()
+    torch.cuda.synchronize()
+    print(json.dumps({"native_rccl_all_to_allv_host_us_per_call": (t1 - t0) / n * 1e6, "device_held": held,
+                      "what": "ncclAllToAllv at world 1 (one piece) issued by kge_comm_all_to_allv from a ctypes "
+                              "call, device held behind a sleep kernel"}), flush=True)
+    nc.close()
     dist.destroy_process_group()
 
 

@@ -121,3 +121,39 @@ def test_sharded_train_step_through_rccl_equals_world1(rccl, name):
     assert l0 == l1
     assert torch.equal(e0, e1) and torch.equal(r0, r1)
     assert all(np.isfinite(l0))
+
+
+def test_native_comm_and_executor_through_rccl(rccl):
+    """The native communicator (kge_comm_*: its own RCCL communicator, id broadcast through the nccl process
+    group) and the native executor over it: ncclAllToAllv self-pieces (including empty ones), the float
+    all-reduce, then a chain of row-sharded steps (each planning the next batch) equal the unsharded fused
+    forward bitwise."""
+    from customknowledgegraphembedding_amd.distributed import NativeComm
+    dev = torch.device("cuda", 0)
+    nc = NativeComm(device=dev)
+    try:
+        assert nc.world == 1 and nc.rank == 0
+        x = torch.arange(41, dtype=torch.float32, device=dev)
+        out = torch.full_like(x, -1.0)
+        nc.all_to_all(out, x, [41], [41])
+        empty = torch.empty(0, dtype=torch.float32, device=dev)
+        nc.all_to_all(empty, empty, [0], [0])
+        y = x.clone()
+        nc.all_reduce_sum_(y)
+        torch.cuda.synchronize()
+        assert torch.equal(out, x) and torch.equal(y, x)
+        E, R, d, B, N = 1500, 7, 64, 32, 200
+        ref = ShardedKGE("DistMult", E, R, d, 24.0, device="cuda", seed=0)
+        sk = ShardedKGE("DistMult", E, R, d, 24.0, device="cuda", seed=0).use_native(nc)
+        batches = [(*_batch(E, R, B, N, 20 + i)[:2], i % 2) for i in range(3)]
+        got = [sk.step_forward(p, n, m, nxt=batches[i + 1] if i + 1 < 3 else None)
+               for i, (p, n, m) in enumerate(batches)]
+        want = [ref.step_forward(p, n, m) for p, n, m in batches]
+        torch.cuda.synchronize()
+        for a, b in zip(got, want):
+            for u, v in zip(a, b):
+                assert torch.equal(u, v)
+        for ex in sk._native.values():
+            ex.close()
+    finally:
+        nc.close()

@@ -312,10 +312,12 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
         # each step also plans the next batch, on the executor's plan stream, overlapping this step
         from customknowledgegraphembedding_amd.distributed import NativeComm
         sk.use_native(NativeComm(device=device))
+        sk.plan_native(batches[0][0], batches[0][1], 0)  # two batches planned ahead, then each step plans the
+        sk.plan_native(batches[1][0], batches[1][1], 1)  # batch two steps later
 
         def step(b, i):
-            nb = batches[(i + 1) % 4]
-            return sk.step_forward(b[0], b[1], i % 2, nxt=(nb[0], nb[1], (i + 1) % 2))
+            nb = batches[(i + 2) % 4]
+            return sk.step_forward(b[0], b[1], i % 2, nxt=(nb[0], nb[1], i % 2))
     else:
         # the exchange plan of step i + 1 (kge_shard_plan: ownership counts and ranks from the ids, its
         # split sizes copied to the host asynchronously) is issued before step i's work, so the host
@@ -466,12 +468,16 @@ def native_host_cost(tables, world, device, batches, steps):
     sk = ShardedKGE("DistMult", w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"], device=device,
                     world=world, rank=0, comm=_PrefilledComm(world, 0), full_tables=tables).use_native(probe=True)
     nb = len(batches)
+    at = [0]  # the plan-ahead chain continues across the calls: step i plans batch i + 2
+    for i in range(2):
+        sk.plan_native(batches[i][0], batches[i][1], i % 2)
 
     def run(n):
-        for i in range(n):
+        for i in range(at[0], at[0] + n):
             p, q, _ = batches[i % nb]
-            np_, nq, _ = batches[(i + 1) % nb]
-            sk.step_forward(p, q, i % 2, nxt=(np_, nq, (i + 1) % 2))
+            np_, nq, _ = batches[(i + 2) % nb]
+            sk.step_forward(p, q, i % 2, nxt=(np_, nq, i % 2))
+        at[0] += n
 
     run(6)
     torch.cuda.synchronize()
@@ -1046,6 +1052,8 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS) + ["pipeline"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="A/B: issue consecutive steps on this many streams in turn (1: torch's current stream)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--train-steps", type=int, default=50, help="train-step side measurement (0 = skip)")
     ap.add_argument("--event-group", type=int, default=5,
@@ -1134,11 +1142,18 @@ def main(argv=None):
     # (a bracket around every single launch adds ~3 us to each step)
     ev_group = max(1, a.event_group)
     evs = {}
+    # --streams S > 1 (A/B): consecutive steps (independent batches) on S streams in turn, so one step's
+    # setup can overlap the previous step's tail; no event groups then (the wall clock times the steps)
+    side = [torch.cuda.Stream(device) for _ in range(a.streams)] if a.streams > 1 else None
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
         pos, neg = batches[i % len(batches)]
+        if side is not None:
+            with torch.cuda.stream(side[i % len(side)]):
+                run_step(m, pos, neg, i % 2, fn)
+            continue
         g, r = divmod(i, ev_group)
         if g % 2 == 0 and r == 0 and i + ev_group <= a.steps:
             evs[g] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -1201,7 +1216,8 @@ def main(argv=None):
         "data": "synthetic U(-(gamma+2)/d,(gamma+2)/d) tables (seed 0); positives: " + m.positives_source +
                 "; negatives RandomState(2).randint(E); 8 distinct batches resident in HBM, mode alternating head/tail",
         "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N, "hidden_dim": w["hidden_dim"],
-                   "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
+                   "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single",
+                   **({"streams": a.streams} if a.streams > 1 else {})},
         "roofline": roofline_hbm(
             step_bytes, traffic, traffic_src, kern_avg_s,
             l2_gather=l2_gather_roofline(pmc_l2_requests(a.workload, step_kernels), kern_avg_s),

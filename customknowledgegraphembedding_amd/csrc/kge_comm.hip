@@ -136,6 +136,9 @@ int hip_fail(const char* what, hipError_t e) {
 
 constexpr int kMaxWorld = 64;
 constexpr int kMaxChunks = 8;
+// plan slots: the step being issued and up to two batches planned ahead, so the host can run two steps
+// ahead of the device without ever waiting for a summary that is still being computed
+constexpr int kSlots = 3;
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -165,7 +168,7 @@ Layout layout_for(int64_t Bg, int64_t N, int64_t ent_dim, int world, int chunks)
     L.bucket = take((size_t)Bg * (N + 1) * 8);
     L.bstart = take((size_t)Bg * 9 * 4);
     L.slot = o;
-    o = 2 * L.slot;  // two plan slots: the current batch's and the next one's
+    o = kSlots * L.slot;  // the current batch's plan slot and the ones planned ahead
     // query rows: each chunk's block of this rank's rows, W copies (the all-to-all's input), at most Rk rows;
     // the received blocks hold at most Rk rows each
     L.q_send = take((size_t)W * Bg * ent_dim * 4);
@@ -189,7 +192,7 @@ struct kge_shard_exec {
     int64_t nentity = 0, shard_rows = 0, ent_dim = 0, D = 0, Bg = 0, N = 0;
     Layout L{};
     char* ws = nullptr;
-    int* host = nullptr;  // [2][summ_ints] pinned
+    int* host = nullptr;  // [kSlots][summ_ints] pinned
     struct Slot {
         bool planned = false;
         int mode = 0;
@@ -198,8 +201,9 @@ struct kge_shard_exec {
         int64_t neg_ld = 0;
         hipEvent_t ready = nullptr;  // the summary's copy to the host has landed
         hipEvent_t freed = nullptr;  // the last step that read the slot's device arrays is done
-    } slot[2];
-    int cur = 0;  // the slot the next step consumes
+    } slot[kSlots];
+    int cur = 0;       // the slot the next step consumes (the oldest plan)
+    int nplanned = 0;  // plans waiting, in slots cur, cur + 1, ... (mod kSlots)
     hipStream_t comm_st = nullptr, plan_st = nullptr;
     hipEvent_t ev_start = nullptr, ev_gather = nullptr, ev_q[kMaxChunks] = {}, ev_s[kMaxChunks] = {},
                ev_x = nullptr;
@@ -403,7 +407,7 @@ int64_t kge_shard_exec_workspace_size(int64_t Bg, int64_t N, int64_t ent_dim, in
 int64_t kge_shard_exec_host_ints(int world, int chunks) {
     if (world < 1 || world > kMaxWorld || chunks < 1 || chunks > kMaxChunks)
         return set_error(KGE_EINVAL, "kge_shard_exec_host_ints: bad world/chunks");
-    return 2 * ((int64_t)world * world + (int64_t)chunks * world);
+    return kSlots * ((int64_t)world * world + (int64_t)chunks * world);
 }
 
 int kge_shard_exec_create(kge_shard_exec** out, kge_comm* comm, int flags, int fn, int64_t nentity, int64_t shard_rows,
@@ -461,8 +465,7 @@ int kge_shard_exec_create(kge_shard_exec** out, kge_comm* comm, int flags, int f
     }
     if (e == hipSuccess) {
         // the slots start free: their `freed` events complete at once
-        e = hipEventRecord(x->slot[0].freed, x->plan_st);
-        if (e == hipSuccess) e = hipEventRecord(x->slot[1].freed, x->plan_st);
+        for (int i = 0; i < kSlots && e == hipSuccess; ++i) e = hipEventRecord(x->slot[i].freed, x->plan_st);
     }
     if (e != hipSuccess) {
         kge_shard_exec_destroy(x);
@@ -508,12 +511,13 @@ int kge_shard_exec_plan(kge_shard_exec* x, const int64_t* pos, const int64_t* ne
     if (!x || !pos || !neg) return set_error(KGE_EINVAL, "kge_shard_exec_plan: null pointer");
     if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH)
         return set_error(KGE_EINVAL, "kge_shard_exec_plan: mode must be 0 or 1");
-    // the slot after the ones already planned (at most two plans are outstanding)
-    int s = x->cur;
-    if (x->slot[s].planned) s ^= 1;
-    if (x->slot[s].planned) return set_error(KGE_EINVAL, "kge_shard_exec_plan: two plans are already waiting");
+    // the slot after the ones already planned
+    if (x->nplanned >= kSlots) return set_error(KGE_EINVAL, "kge_shard_exec_plan: every plan slot is waiting");
+    const int s = (x->cur + x->nplanned) % kSlots;
     KGE_HIP_TRY("kge_shard_exec_plan", hipEventRecord(x->ev_start, (hipStream_t)stream));
-    return make_plan(x, s, pos, neg, neg_ld, mode, x->ev_start);
+    const int rc = make_plan(x, s, pos, neg, neg_ld, mode, x->ev_start);
+    if (!rc) ++x->nplanned;
+    return rc;
 }
 
 int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld, int64_t shard_lo, const float* rel,
@@ -529,9 +533,10 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
     kge_shard_exec::Slot* sl = &x->slot[s];
     // the work queued so far (the next batch's ids included) ends here: the next plan waits for no more
     KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(x->ev_start, st));
-    if (!sl->planned) {  // no plan made ahead: plan now (the host then waits for the split sizes)
+    if (x->nplanned == 0) {  // no plan made ahead: plan now (the host then waits for the split sizes)
         int rc = make_plan(x, s, pos, neg, neg_ld, mode, x->ev_start);
         if (rc) return rc;
+        x->nplanned = 1;
     } else if (sl->pos != pos || sl->neg != neg || sl->neg_ld != neg_ld || sl->mode != mode) {
         return set_error(KGE_EINVAL, "kge_shard_exec_step: the waiting plan was made for another batch or mode");
     }
@@ -625,14 +630,18 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
     if (rc) return rc;
     KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(sl->freed, st));
     sl->planned = false;
-    x->cur = s ^ 1;
-    // the next batch's plan, made now so that its split sizes are on the host before the next step; its
-    // stream waits only for the work queued before this step (ev_start), so it overlaps this step
-    if (next_pos && next_neg && !x->slot[x->cur].planned) {
+    x->cur = (s + 1) % kSlots;
+    --x->nplanned;
+    // the batch after the planned ones, planned now (into the slot a step before this one freed) so that
+    // its split sizes are on the host long before its step; its stream waits only for the work queued
+    // before this step (ev_start), so it overlaps this step
+    if (next_pos && next_neg) {
         if (next_mode != KGE_HEAD_BATCH && next_mode != KGE_TAIL_BATCH)
             return set_error(KGE_EINVAL, "kge_shard_exec_step: next_mode must be 0 or 1");
-        rc = make_plan(x, x->cur, next_pos, next_neg, neg_ld, next_mode, x->ev_start);
+        if (x->nplanned >= kSlots) return set_error(KGE_EINVAL, "kge_shard_exec_step: every plan slot is waiting");
+        rc = make_plan(x, (x->cur + x->nplanned) % kSlots, next_pos, next_neg, neg_ld, next_mode, x->ev_start);
         if (rc) return rc;
+        ++x->nplanned;
     }
     return set_error(0, "");
 }

@@ -841,6 +841,258 @@ ts_fwd_x3_kernel(TsParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Head-batch forward with the operands split ONCE (ts_fwd_x3s_kernel): ts_fwd_x3_kernel's block tile,
+// products and accumulation order (so bitwise its scores), restaged so that the MFMA loop does no VALU work:
+//   * K in chunks of 16 (one 32x32x16 k-step). The staging threads load a chunk of the rows (A: 256 x 16)
+//     and of M_r (B: 16 x 256) with raw buffer loads whose hardware range check zero-fills everything past
+//     d and every invalid row (no branches, no waits inside the loop), split each fp32 value ONCE into its
+//     three bf16 terms (split3_bf16's arithmetic) and store three bf16 planes per operand; ts_fwd_x3_kernel
+//     split every fragment in the MFMA loop, A twice and B four times over, and its branchy loads compiled
+//     to a vmcnt(0) wait per chunk plus 32 spilled VGPRs;
+//   * planes [row or column][16 k] bf16 (32-B rows) with the 16-B halves swapped on every other group of
+//     8 rows: the MFMA operand reads (ds_read_b128, one per fragment and plane) and the staging stores are
+//     bank-conflict-free (B's transposing 4-B stores 2-way, which costs a ds_write_b32 nothing);
+//   * two LDS stages (96 KB) and two register sets: chunk g + 2 is loaded while chunk g is multiplied and
+//     chunk g + 1 stored, one barrier per chunk.
+// The 48 MFMAs of a chunk per wave read 18 ds_read_b128 (2 A fragments x 3 planes, 4 B fragments x 3).
+// ---------------------------------------------------------------------------------------------
+constexpr int kXsPlane = XBR * 16 * 2;  // bytes of one bf16 plane chunk (256 rows x 16 k)
+constexpr int kXsStage = 6 * kXsPlane;  // A planes then B planes
+constexpr int kXsMaxDim = 1024;         // u - 1 image beside the two stages
+constexpr uint32_t kXsOOB = 0xFFFFFFF0u;
+
+__device__ __forceinline__ int xs_off(int row, int h) { return row * 32 + ((h ^ ((row >> 3) & 1)) << 4); }
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// split3_bf16's arithmetic on 4 and 2 values (elementwise the same operations: the same three terms)
+__device__ __forceinline__ void split3_x4(f32x4_t v, bf16x4_t& a0, bf16x4_t& a1, bf16x4_t& a2) {
+    a0 = __builtin_convertvector(v, bf16x4_t);
+    const f32x4_t r1 = v - __builtin_convertvector(a0, f32x4_t);
+    a1 = __builtin_convertvector(r1, bf16x4_t);
+    a2 = __builtin_convertvector(r1 - __builtin_convertvector(a1, f32x4_t), bf16x4_t);
+}
+
+struct XsRegs {
+    float4 a[2], b[2], m[2];
+};
+
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(2))) void
+ts_fwd_x3s_kernel(TsParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char xs_smem[];  // 2 stages, then u - 1 (d floats)
+    __shared__ int rowid[XBR];
+    __shared__ float2 red[2][XBR];
+    __shared__ float wsum[kXWaves];
+    __shared__ int wcnt[kXWaves];
+    __shared__ int hist[kTsSortMaxRel + 1];
+    __shared__ int sel[3];
+    float* cs = reinterpret_cast<float*>(xs_smem + 2 * kXsStage);
+
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int half = lane >> 5, col = lane & 31;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int d = p.d;
+    const int64_t blk = blockIdx.x;
+    int64_t b = blk / p.nchunk;
+    int ch = (int)(blk % p.nchunk);
+    if (p.nrel <= kTsSortMaxRel && p.B <= kTsSortMaxB) {  // ts_fwd_x3_kernel's relation-sorted order
+        const int64_t nblk = p.B * p.nchunk, q8 = nblk / 8, r8 = nblk % 8, x = blk % 8;
+        const int64_t rank = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blk / 8;
+        ch = (int)(rank % p.nchunk);
+        b = ts_sorted_row_nt<kXThreads>(p, rank / p.nchunk, hist, wcnt, sel);
+    }
+    const int64_t r = p.pos[b * 3 + 1];
+    const bool rok = r >= 0 && r < p.nrel;
+    const int64_t n0 = (int64_t)ch * XBR;
+    const int nrows = (int)min<int64_t>(XBR, p.N - n0);
+    if (t < XBR) {
+        int id = -1;
+        if (t < nrows) {
+            const int64_t e = p.neg[b * p.neg_ld + n0 + t];
+            if (e >= 0 && e < p.nent) id = (int)e;
+        }
+        rowid[t] = id;
+        red[0][t] = red[1][t] = make_float2(0.f, 0.f);
+    }
+    {  // u - 1 for the relation row (ts_fwd_x3_kernel's arithmetic)
+        float ss = 0.f;
+        for (int j = t; j < d; j += kXThreads) {
+            const float v = rok ? p.rel[r * p.rel_ld + j] : 0.f;
+            cs[j] = v;
+            ss += v * v;
+        }
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, kWave);
+        if (lane == 0) wsum[wave] = ss;
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < kXWaves; ++w) tot += wsum[w];
+        const float rnorm = sqrtf(tot);
+        for (int j = t; j < d; j += kXThreads) cs[j] = cs[j] / rnorm - 1.f;
+    }
+    __syncthreads();
+    // buffer descriptors: the entity table (rows by per-lane offset) and the relation's d x d matrix
+    const rsrc_t ra = make_rsrc(p.ent, (uint32_t)(p.nent * p.ent_ld * 4));
+    const float* Wr = rok ? (p.Mpre ? p.Mpre : p.W) + r * (int64_t)d * d : p.W;
+    const uint32_t mbytes = rok ? (uint32_t)((int64_t)d * d * 4) : 0u;
+    const rsrc_t rw = make_rsrc(Wr, mbytes);
+    const bool fuse_mask = !p.Mpre;
+    const rsrc_t rm = make_rsrc(fuse_mask && rok ? p.mask + r * (int64_t)d * d : p.W, fuse_mask ? mbytes : 0u);
+    // this thread's staging slots: A rows (t >> 2) + 128 u, k quad t & 3; B k pair t & 7 (+u), columns 4 (t >> 3)
+    int aid[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) aid[u] = rowid[(t >> 2) + 128 * u];
+    const int aq = t & 3, bkp = t & 7, bjq = t >> 3;
+    const int nk = (d + 15) / 16, nct = (d + XBC - 1) / XBC, T = nk * nct;
+
+    auto gload = [&](XsRegs& R, int g) {
+        const int ct = g / nk, k0 = (g - ct * nk) * 16;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int ka = k0 + 4 * aq;
+            const uint32_t oa = (aid[u] >= 0 && ka < d) ? (uint32_t)(((int64_t)aid[u] * p.ent_ld + ka) * 4) : kXsOOB;
+            const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa, 0, 0);
+            R.a[u] = make_float4(__uint_as_float(va[0]), __uint_as_float(va[1]), __uint_as_float(va[2]),
+                                 __uint_as_float(va[3]));
+            const int kb = k0 + 2 * bkp + u, j = ct * XBC + 4 * bjq;
+            const uint32_t ob = (kb < d && j < d) ? (uint32_t)(((int64_t)kb * d + j) * 4) : kXsOOB;
+            const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rw, ob, 0, 0);
+            R.b[u] = make_float4(__uint_as_float(vb[0]), __uint_as_float(vb[1]), __uint_as_float(vb[2]),
+                                 __uint_as_float(vb[3]));
+            if (fuse_mask) {
+                const auto vm = __builtin_amdgcn_raw_buffer_load_b128(rm, ob, 0, 0);
+                R.m[u] = make_float4(__uint_as_float(vm[0]), __uint_as_float(vm[1]), __uint_as_float(vm[2]),
+                                     __uint_as_float(vm[3]));
+            }
+        }
+    };
+    auto sstore = [&](const XsRegs& R, int stage) {
+        unsigned char* A = xs_smem + stage * kXsStage;
+        unsigned char* Bp = A + 3 * kXsPlane;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int row = (t >> 2) + 128 * u;
+            bf16x4_t s0, s1, s2;
+            split3_x4(f32x4_t{R.a[u].x, R.a[u].y, R.a[u].z, R.a[u].w}, s0, s1, s2);
+            const int o = xs_off(row, aq >> 1) + (aq & 1) * 8;
+            *reinterpret_cast<bf16x4_t*>(A + o) = s0;
+            *reinterpret_cast<bf16x4_t*>(A + kXsPlane + o) = s1;
+            *reinterpret_cast<bf16x4_t*>(A + 2 * kXsPlane + o) = s2;
+        }
+        // B: the two k rows of this thread's 4 columns, transposed into [column][k]
+        float4 b0 = R.b[0], b1 = R.b[1];
+        if (fuse_mask) {
+            b0 = mul4(b0, R.m[0]);
+            b1 = mul4(b1, R.m[1]);
+        }
+        const float lo_k[4] = {b0.x, b0.y, b0.z, b0.w}, hi_k[4] = {b1.x, b1.y, b1.z, b1.w};
+        bf16x4_t e0, e1, e2, o0, o1, o2;  // the three terms of the four columns at k = 2 kp and 2 kp + 1
+        split3_x4(f32x4_t{lo_k[0], lo_k[1], lo_k[2], lo_k[3]}, e0, e1, e2);
+        split3_x4(f32x4_t{hi_k[0], hi_k[1], hi_k[2], hi_k[3]}, o0, o1, o2);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int cl = 4 * bjq + c;
+            const int o = xs_off(cl, bkp >> 2) + (bkp & 3) * 4;
+            *reinterpret_cast<bf16x2_t*>(Bp + o) = bf16x2_t{e0[c], o0[c]};
+            *reinterpret_cast<bf16x2_t*>(Bp + kXsPlane + o) = bf16x2_t{e1[c], o1[c]};
+            *reinterpret_cast<bf16x2_t*>(Bp + 2 * kXsPlane + o) = bf16x2_t{e2[c], o2[c]};
+        }
+    };
+    f32x16 acc[2][4];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r2 = 0; r2 < 16; ++r2) acc[i][j][r2] = 0.f;
+    };
+    auto compute = [&](int stage) {
+        const unsigned char* A = xs_smem + stage * kXsStage;
+        const unsigned char* Bp = A + 3 * kXsPlane;
+        bf16x8 a[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int o = xs_off(wr * 64 + i * 32 + col, half);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * kXsPlane + o);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int o = xs_off(wc * 128 + j * 32 + col, half);
+            bf16x8 bb[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) bb[pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * kXsPlane + o);
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0, 0, 0);
+        }
+    };
+    auto fold = [&](int ct) {  // ts_fwd_x3_kernel's per-row sums over this wave's 128 columns
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) {
+                float sq = 0.f, ab = 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int cg = ct * XBC + wc * 128 + j * 32 + col;
+                    const float c = cg < d ? cs[cg] : 0.f;
+                    const float v = acc[i][j][r2];
+                    sq = fmaf(v, v, sq);
+                    ab += fabsf(v * c);
+                }
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) {
+                    sq += __shfl_xor(sq, o, kWave);
+                    ab += __shfl_xor(ab, o, kWave);
+                }
+                if (col == 0) {
+                    const int row = wr * 64 + i * 32 + (r2 & 3) + 8 * (r2 >> 2) + 4 * half;
+                    float2& x = red[wc][row];
+                    x = make_float2(x.x + sq, x.y + ab);
+                }
+            }
+    };
+    // one chunk step: multiply stage g % 2, store chunk g + 1 (held in `nxt`) into the other stage, load chunk
+    // g + 3 into `nxt` (chunk g + 2 is in flight in the other set), fold at the end of a column super-tile
+    auto step = [&](int g, XsRegs& nxt) {
+        compute(g & 1);
+        if (g + 1 < T) sstore(nxt, (g + 1) & 1);
+        if (g + 3 < T) gload(nxt, g + 3);
+        if ((g + 1) % nk == 0) {
+            fold(g / nk);
+            zero_acc();
+        }
+        __syncthreads();
+    };
+    XsRegs R0, R1;
+    zero_acc();
+    gload(R0, 0);
+    if (T > 1) gload(R1, 1);
+    sstore(R0, 0);
+    if (T > 2) gload(R0, 2);
+    __syncthreads();
+    int g = 0;
+    for (; g + 1 < T; g += 2) {
+        step(g, R1);      // stores chunk g + 1 (R1), loads g + 3 into R1
+        step(g + 1, R0);  // stores chunk g + 2 (R0), loads g + 4 into R0
+    }
+    if (g < T) step(g, R1);
+    if (t < nrows) {
+        const float2 x0 = red[0][t], x1 = red[1][t];
+        const float2 x = make_float2(x0.x + x1.x, x0.y + x1.y);
+        const int64_t n = n0 + t;
+        p.out[b * p.out_ld + n] = p.gamma - x.y / sqrtf(x.x);
+        if (p.stats) p.stats[b * p.N + n] = x;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void ts_premul_kernel(const float4* __restrict__ W, const float4* __restrict__ mask,
                                                           float4* __restrict__ M, int64_t n4) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock)
@@ -1170,6 +1422,21 @@ void launch_rows(const TsParams& p, hipStream_t st) {
             if (!p.grouped && p.N > TBM && p.d <= kTsBigMaxDim && !big_off) {
                 TsParams q = p;
                 q.nchunk = (int)((p.N + XBR - 1) / XBR);
+                // operands split once at staging (ts_fwd_x3s_kernel, bitwise the same scores) when its buffer
+                // offsets fit 32 bits; KGE_TS_X3S=0 keeps ts_fwd_x3_kernel (A/B runs; read per call, so a test
+                // can compare the two in one process)
+                const char* xs_env = getenv("KGE_TS_X3S");
+                const bool xs_off = xs_env && xs_env[0] == '0';
+                if (!xs_off && p.d <= kXsMaxDim && p.nent * p.ent_ld * 4 < (int64_t)kXsOOB &&
+                    (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB) {
+                    const size_t lds = 2 * (size_t)kXsStage + (size_t)p.d * 4;
+                    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel),
+                                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                                 2 * kXsStage + kXsMaxDim * 4) == hipSuccess;
+                    (void)attr;
+                    hipLaunchKernelGGL(ts_fwd_x3s_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);
+                    return;
+                }
                 hipLaunchKernelGGL(ts_fwd_x3_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);
                 return;
             }

@@ -800,24 +800,46 @@ class ShardedKGE:
         self._native = {}
         return self
 
-    def _native_step(self, pos_g, neg_g, mode, temperature, adversarial, chunks, nxt):
-        m = ops.mode_id(mode)
-        if m not in (HEAD_BATCH, TAIL_BATCH):
-            raise ValueError("the sharded step needs a negative mode (0 or 1)")
-        Bg, N = neg_g.shape
-        if Bg % self.world:
-            raise ValueError("global batch must split evenly over ranks")
-        if pos_g.stride() != (3, 1) or neg_g.stride(1) != 1:
-            raise ValueError("the native step needs contiguous pos [Bg, 3] and row-major neg [Bg, N]")
+    def _native_exec(self, Bg, N, chunks):
         key = (Bg, N, default_chunks(self.world, chunks))
         ex = self._native.get(key)
         if ex is None:
             comm, probe = self._native_cfg
             ex = self._native[key] = NativeShardExec(self, Bg, N, comm=comm, probe=probe, chunks=chunks)
+        return ex
+
+    @staticmethod
+    def _native_batch(pos_g, neg_g, mode):
+        m = ops.mode_id(mode)
+        if m not in (HEAD_BATCH, TAIL_BATCH):
+            raise ValueError("the sharded step needs a negative mode (0 or 1)")
+        if pos_g.stride() != (3, 1) or neg_g.stride(1) != 1:
+            raise ValueError("the native step needs contiguous pos [Bg, 3] and row-major neg [Bg, N]")
+        return m
+
+    def plan_native(self, pos_g, neg_g, mode, chunks=None):
+        """Plans a batch ahead for the native step (kge_shard_exec_plan, on the executor's plan stream after the
+        current stream's queued work): up to three plans wait; step_forward consumes them in order, and each
+        step given `nxt` plans that batch too. Planning two batches ahead lets the host run two steps ahead
+        of the device."""
+        if self._native_cfg is None:
+            raise ValueError("plan_native needs use_native() first")
+        m = self._native_batch(pos_g, neg_g, mode)
+        Bg, N = neg_g.shape
+        if Bg % self.world:
+            raise ValueError("global batch must split evenly over ranks")
+        self._native_exec(Bg, N, chunks).plan(pos_g, neg_g, m)
+
+    def _native_step(self, pos_g, neg_g, mode, temperature, adversarial, chunks, nxt):
+        m = self._native_batch(pos_g, neg_g, mode)
+        Bg, N = neg_g.shape
+        if Bg % self.world:
+            raise ValueError("global batch must split evenly over ranks")
+        ex = self._native_exec(Bg, N, chunks)
         if nxt is not None:
-            nm = ops.mode_id(nxt[2])
-            if tuple(nxt[1].shape) != (Bg, N) or nxt[0].stride() != (3, 1) or nxt[1].stride(1) != 1:
-                raise ValueError("the next batch must have this batch's shape and layout")
+            nm = self._native_batch(nxt[0], nxt[1], nxt[2])
+            if tuple(nxt[1].shape) != (Bg, N):
+                raise ValueError("the batch planned ahead must have this batch's shape")
             nxt = (nxt[0], nxt[1], nm)
         return ex.step(pos_g, neg_g, m, temperature, adversarial, nxt)
 
@@ -830,8 +852,9 @@ class ShardedKGE:
         Host path (it bounds the step at W = 8: bench rank_host_cost): the split sizes come from the plan's
         cached layout, the exchange buffers are persistent (self._ws), the kernels get pointers and the
         stream handle computed once.
-        After use_native(...) the whole step is one C call (NativeShardExec; `plan` must then be None):
-        `nxt` = (pos, neg, mode) of the next batch, whose plan that call makes on the side (plan-ahead)."""
+        After use_native(...) the whole step is one C call (NativeShardExec; `plan` must then be None): it
+        consumes the oldest batch planned ahead (plan_native / an earlier step's `nxt`; planned inline if none
+        waits), and `nxt` = (pos, neg, mode) of the batch after the planned ones is planned on the side."""
         W, me = self.world, self.rank
         if self._native_cfg is not None and plan is None:
             return self._native_step(pos_g, neg_g, mode, temperature, adversarial, chunks, nxt)

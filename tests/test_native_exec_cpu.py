@@ -20,14 +20,14 @@ def test_workspace_size_bounds_every_buffer():
     lib = _lib()
     Bg, N, d, W, K = 4096, 1024, 500, 8, 2
     n = lib.kge_shard_exec_workspace_size(Bg, N, d, W, K)
-    # two plan slots (each with its [Bg, N+1] bucket of int2) + W copies of the query rows + the score buffers
+    # three plan slots (each with its [Bg, N+1] bucket of int2) + W copies of the query rows + the score buffers
     slot = Bg * (N + 1) * 8 + 2 * W * Bg * 4
-    assert n >= 2 * slot + W * Bg * d * 4 + Bg * d * 4 + Bg * (N + 1) * 4
-    assert n < 2 * slot + 2 * (W * Bg * d * 4 + Bg * d * 4 + Bg * (N + 1) * 4)
+    assert n >= 3 * slot + W * Bg * d * 4 + Bg * d * 4 + Bg * (N + 1) * 4
+    assert n < 3 * slot + 2 * (W * Bg * d * 4 + Bg * d * 4 + Bg * (N + 1) * 4)
     assert lib.kge_shard_exec_workspace_size(Bg, N, d, W, 3) == EINVAL  # chunks must divide the world
     assert lib.kge_shard_exec_workspace_size(Bg + 1, N, d, W, K) == EINVAL  # the batch must split over ranks
     assert lib.kge_shard_exec_workspace_size(Bg, N, d, 65, 1) == EINVAL
-    assert lib.kge_shard_exec_host_ints(8, 2) == 2 * (64 + 16)
+    assert lib.kge_shard_exec_host_ints(8, 2) == 3 * (64 + 16)
     assert lib.kge_shard_exec_host_ints(0, 1) == EINVAL
 
 

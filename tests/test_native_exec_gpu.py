@@ -49,9 +49,10 @@ def _want(m, pos, neg, mode):
     return s, o_neg, o_pos
 
 
-def _run(ranks, batches, K=None):
-    """Every rank steps through `batches` ([(pos, neg, mode)]) on its own stream, each step planning the next
-    batch (the plan-ahead chain); returns per batch the ranks' outputs."""
+def _run(ranks, batches, K=None, ahead=2):
+    """Every rank steps through `batches` ([(pos, neg, mode)]) on its own stream: the first `ahead` batches
+    planned up front, then each step planning the batch `ahead` steps later (the plan-ahead chain); returns
+    per batch the ranks' outputs."""
     W = len(ranks)
     streams = [torch.cuda.Stream() for _ in range(W)]
     torch.cuda.synchronize()
@@ -59,8 +60,10 @@ def _run(ranks, batches, K=None):
     def go(r):
         outs = []
         with torch.cuda.stream(streams[r]):
+            for b in batches[:ahead]:
+                ranks[r].plan_native(*b, chunks=K)
             for i, (pos, neg, mode) in enumerate(batches):
-                nxt = batches[i + 1] if i + 1 < len(batches) else None
+                nxt = batches[i + ahead] if ahead and i + ahead < len(batches) else None
                 outs.append(ranks[r].step_forward(pos, neg, mode, chunks=K, nxt=nxt))
         return outs
 
@@ -69,10 +72,10 @@ def _run(ranks, batches, K=None):
     return [[res[r][i] for r in range(W)] for i in range(len(batches))]
 
 
-def _check(m, ranks, batches, K=None):
+def _check(m, ranks, batches, K=None, ahead=2):
     W = len(ranks)
     Bh = batches[0][0].shape[0] // W
-    for (pos, neg, mode), outs in zip(batches, _run(ranks, batches, K)):
+    for (pos, neg, mode), outs in zip(batches, _run(ranks, batches, K, ahead)):
         s, o_neg, o_pos = _want(m, pos, neg, mode)
         for r, (g_neg, g_pos, g_s) in enumerate(outs):
             sl = slice(r * Bh, (r + 1) * Bh)
@@ -83,13 +86,14 @@ def _check(m, ranks, batches, K=None):
 
 @pytest.mark.parametrize("name", ["DistMult", "InterHT", "RotatE"])
 def test_world1_device_copies_bitwise(name):
-    """W = 1 without a communicator (the pieces are device copies): three batches chained through the
-    plan-ahead, both modes, equal the unsharded fused forward bitwise."""
+    """W = 1 without a communicator (the pieces are device copies): five batches, planned inline or chained
+    through the plan-ahead one to three batches ahead, both modes, equal the unsharded fused forward bitwise."""
     E, R, d, Bg, N = 3001, 5, 48, 24, 300
     m = _model(name, E, R, d)
     ranks = _native_ranks(m, 1, None)
-    batches = [(*_batch(E, R, Bg, N, seed=s), s % 2) for s in range(3)]
-    _check(m, ranks, batches)
+    batches = [(*_batch(E, R, Bg, N, seed=s), s % 2) for s in range(5)]
+    for ahead in (0, 1, 2, 3):  # planned inline, one, two and three batches ahead
+        _check(m, ranks, batches, ahead=ahead)
 
 
 @pytest.mark.parametrize("W,K", [(2, 1), (2, 2), (4, 2), (8, 2), (8, 4)])
@@ -155,8 +159,15 @@ def test_step_of_another_batch_than_the_planned_one_is_rejected():
     sk = _native_ranks(m, 1, None)[0]
     a, b = _batch(E, R, Bg, N, seed=1), _batch(E, R, Bg, N, seed=2)
     sk.step_forward(a[0], a[1], 0, nxt=(a[0], a[1], 1))  # plans batch a, tail-batch, for the next step
+    sk.plan_native(b[0], b[1], 0)
+    sk.plan_native(b[0], b[1], 1)  # three plans wait: a step with another next batch has no slot for it
+    with pytest.raises(KGEHipError, match="every plan slot"):
+        sk.plan_native(a[0], a[1], 0)
     with pytest.raises(KGEHipError, match="another batch or mode"):
         sk.step_forward(b[0], b[1], 1)
     with pytest.raises(KGEHipError, match="another batch or mode"):
         sk.step_forward(a[0], a[1], 0)
+    sk.step_forward(a[0], a[1], 1)  # the planned batches, in order
+    sk.step_forward(b[0], b[1], 0)
+    sk.step_forward(b[0], b[1], 1)
     torch.cuda.synchronize()

@@ -145,8 +145,10 @@ def test_native_comm_and_executor_through_rccl(rccl):
         E, R, d, B, N = 1500, 7, 64, 32, 200
         ref = ShardedKGE("DistMult", E, R, d, 24.0, device="cuda", seed=0)
         sk = ShardedKGE("DistMult", E, R, d, 24.0, device="cuda", seed=0).use_native(nc)
-        batches = [(*_batch(E, R, B, N, 20 + i)[:2], i % 2) for i in range(3)]
-        got = [sk.step_forward(p, n, m, nxt=batches[i + 1] if i + 1 < 3 else None)
+        batches = [(*_batch(E, R, B, N, 20 + i)[:2], i % 2) for i in range(4)]
+        sk.plan_native(*batches[0])
+        sk.plan_native(*batches[1])
+        got = [sk.step_forward(p, n, m, nxt=batches[i + 2] if i + 2 < 4 else None)
                for i, (p, n, m) in enumerate(batches)]
         want = [ref.step_forward(p, n, m) for p, n, m in batches]
         torch.cuda.synchronize()

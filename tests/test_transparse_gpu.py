@@ -175,3 +175,32 @@ def test_trainer_step_matches_oracle_loss():
         got = prm.detach().cpu().double()
         big = g.abs() > 1e-6 * float(g.abs().max())
         assert torch.allclose(got[big], exp[big], atol=1e-6)
+
+
+@pytest.mark.parametrize("d,N,premul", [(500, 256, True), (500, 300, False), (128, 200, True), (260, 129, False),
+                                        (1024, 160, True)])
+def test_split_once_forward_is_bitwise_the_register_split_one(monkeypatch, d, N, premul):
+    """ts_fwd_x3s_kernel (operands split once at staging, buffer loads) against ts_fwd_x3_kernel (the same
+    products split per fragment in the MFMA loop): head-batch scores and stats are bitwise equal, with
+    out-of-range ids, partial K chunks and partial column super-tiles; and within 1e-4 of the fp64 oracle."""
+    E, R, B, gamma = 300, 3, 5, 12.0
+    ent, rel, W, mask = _tables(E, R, d, seed=4)
+    pos, neg = _batch(E, R, B, N, seed=9)
+    neg[1, 3] = E + 7
+    neg[4, N - 1] = -2
+    ed, rd, Wd, md = ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV)
+    M = ops.transparse_premul(Wd, md) if premul else None
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KGE_TS_X3S", flag)
+        st = torch.empty((B * N, 2), dtype=torch.float32, device=DEV)
+        s = ops.transparse_score_raw(0, ed, rd, Wd, md, pos.to(DEV), neg.to(DEV), gamma, stats=st, M=M)
+        torch.cuda.synchronize()
+        outs.append((s.cpu(), st.cpu()))
+    assert np.array_equal(outs[0][0].numpy(), outs[1][0].numpy(), equal_nan=True)
+    assert np.array_equal(outs[0][1].numpy(), outs[1][1].numpy(), equal_nan=True)
+    ok = (neg >= 0) & (neg < E)
+    ref, _ = _oracle(ent, rel, W, mask, pos, neg.clamp(0, E - 1), 0, gamma)
+    got = outs[1][0].numpy()
+    assert rel_close(got[ok.numpy()], ref[ok.numpy()]) <= 1e-4
+    assert np.isnan(got[~ok.numpy()]).all()

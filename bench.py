@@ -1052,8 +1052,6 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS) + ["pipeline"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="A/B: issue consecutive steps on this many streams in turn (1: torch's current stream)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--train-steps", type=int, default=50, help="train-step side measurement (0 = skip)")
     ap.add_argument("--event-group", type=int, default=5,
@@ -1142,18 +1140,11 @@ def main(argv=None):
     # (a bracket around every single launch adds ~3 us to each step)
     ev_group = max(1, a.event_group)
     evs = {}
-    # --streams S > 1 (A/B): consecutive steps (independent batches) on S streams in turn, so one step's
-    # setup can overlap the previous step's tail; no event groups then (the wall clock times the steps)
-    side = [torch.cuda.Stream(device) for _ in range(a.streams)] if a.streams > 1 else None
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
         pos, neg = batches[i % len(batches)]
-        if side is not None:
-            with torch.cuda.stream(side[i % len(side)]):
-                run_step(m, pos, neg, i % 2, fn)
-            continue
         g, r = divmod(i, ev_group)
         if g % 2 == 0 and r == 0 and i + ev_group <= a.steps:
             evs[g] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -1216,8 +1207,7 @@ def main(argv=None):
         "data": "synthetic U(-(gamma+2)/d,(gamma+2)/d) tables (seed 0); positives: " + m.positives_source +
                 "; negatives RandomState(2).randint(E); 8 distinct batches resident in HBM, mode alternating head/tail",
         "config": {"workload": w["name"], "global_batch": B * world, "n_neg": N, "hidden_dim": w["hidden_dim"],
-                   "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single",
-                   **({"streams": a.streams} if a.streams > 1 else {})},
+                   "score_function": w["fn"], "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": roofline_hbm(
             step_bytes, traffic, traffic_src, kern_avg_s,
             l2_gather=l2_gather_roofline(pmc_l2_requests(a.workload, step_kernels), kern_avg_s),

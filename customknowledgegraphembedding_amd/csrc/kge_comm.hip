@@ -272,17 +272,17 @@ int loop_all_to_allv(kge_comm* c, const float* send, const size_t* sc, const siz
 
 // one all-to-all of floats on the communication stream; without a communicator (world 1) the only piece is
 // this rank's own, a device copy; KGE_EXEC_PROBE skips the collectives (host-cost probe only)
-int exchange(kge_shard_exec* x, const float* send, void* recv, const char* what) {
+int exchange(kge_shard_exec* x, const float* send, void* recv, hipStream_t cs, const char* what) {
     if (x->flags & KGE_EXEC_PROBE) return 0;
     if (!x->comm) {
         if (x->sc[0]) KGE_HIP_TRY(what, hipMemcpyAsync(static_cast<char*>(recv) + x->rd[0] * 4, send + x->sd[0],
-                                                       x->sc[0] * 4, hipMemcpyDeviceToDevice, x->comm_st));
+                                                       x->sc[0] * 4, hipMemcpyDeviceToDevice, cs));
         return 0;
     }
     if (x->comm->loop)
-        return loop_all_to_allv(x->comm, send, x->sc.data(), x->sd.data(), recv, x->rc.data(), x->rd.data(), x->comm_st);
+        return loop_all_to_allv(x->comm, send, x->sc.data(), x->sd.data(), recv, x->rc.data(), x->rd.data(), cs);
     const ncclResult_t r = rccl().all_to_allv(send, x->sc.data(), x->sd.data(), recv, x->rc.data(), x->rd.data(),
-                                              ncclFloat32, x->comm->nccl, x->comm_st);
+                                              ncclFloat32, x->comm->nccl, cs);
     if (r != ncclSuccess) return nccl_fail(what, r);
     return 0;
 }
@@ -562,13 +562,21 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
     float* q_block = reinterpret_cast<float*>(x->ws + x->L.q_block);
     float* s_send = reinterpret_cast<float*>(x->ws + x->L.s_send);
     float* s_recv = reinterpret_cast<float*>(x->ws + x->L.s_recv);
-    // the step's stream graph: compute on `st`, collectives on comm_st
-    KGE_HIP_TRY("kge_shard_exec_step", hipStreamWaitEvent(st, sl->ready, 0));
+    // the step's stream graph: compute on `st`, collectives on comm_st (the plan's arrays are complete: the
+    // host waited for its event above, so `st` needs no wait on it). KGE_EXEC_ONE_STREAM: the collectives on
+    // `st` too, in step order: no cross-stream event hops (each costs the dependent queue a wake-up), no
+    // overlap of exchanges with scoring
+    const bool one = (x->flags & KGE_EXEC_ONE_STREAM) != 0;
+    const hipStream_t cs = one ? st : x->comm_st;
+    auto hop = [&](hipEvent_t ev, hipStream_t from, hipStream_t to) -> hipError_t {
+        if (one) return hipSuccess;
+        hipError_t e = hipEventRecord(ev, from);
+        return e == hipSuccess ? hipStreamWaitEvent(to, ev, 0) : e;
+    };
     int rc = kge_shard_gather_queries(shard, x->shard_rows, shard_ld, shard_lo, pos, x->Bg, K, -1, d, W, me, mode, 0,
                                       x->slot_i(s, x->L.qown), x->slot_i(s, x->L.qslot), summ, q_send, qidx, st);
     if (rc) return rc;
-    KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(x->ev_gather, st));
-    KGE_HIP_TRY("kge_shard_exec_step", hipStreamWaitEvent(x->comm_st, x->ev_gather, 0));
+    KGE_HIP_TRY("kge_shard_exec_step", hop(x->ev_gather, st, cs));
     // 1. every chunk's query exchange: this rank's rows of the chunk (the same piece to every rank)
     size_t at = 0, qb = 0;
     size_t qb_at[kMaxChunks], q_rows[kMaxChunks];
@@ -584,9 +592,9 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
         }
         qb_at[k] = qb;
         q_rows[k] = r / (size_t)d;
-        rc = exchange(x, q_send, q_block + qb, "kge_shard_exec_step query all-to-all");
+        rc = exchange(x, q_send, q_block + qb, cs, "kge_shard_exec_step query all-to-all");
         if (rc) return rc;
-        KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(x->ev_q[k], x->comm_st));
+        if (!one) KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(x->ev_q[k], cs));
         at += (size_t)W * mine * d;
         qb += r;
     }
@@ -607,7 +615,7 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
             x->rd[o] = nrecv;
             nrecv += x->rc[o];
         }
-        KGE_HIP_TRY("kge_shard_exec_step", hipStreamWaitEvent(st, x->ev_q[k], 0));
+        if (!one) KGE_HIP_TRY("kge_shard_exec_step", hipStreamWaitEvent(st, x->ev_q[k], 0));
         if (nsend) {
             rc = kge_shard_score(x->fn, mode, q_block + qb_at[k], (int64_t)q_rows[k], d, qidx + row0, rel, nrelation, rel_ld,
                                  rel_off, shard, x->shard_rows, shard_ld, shard_lo, pos + row0 * 3, Rk, x->N, x->D,
@@ -616,14 +624,12 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
                                  homeB, row0 / homeB, s_send + sb, st);
             if (rc) return rc;
         }
-        KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(x->ev_s[k], st));
-        KGE_HIP_TRY("kge_shard_exec_step", hipStreamWaitEvent(x->comm_st, x->ev_s[k], 0));
-        rc = exchange(x, s_send + sb, s_recv, "kge_shard_exec_step score all-to-all");
+        KGE_HIP_TRY("kge_shard_exec_step", hop(x->ev_s[k], st, cs));
+        rc = exchange(x, s_send + sb, s_recv, cs, "kge_shard_exec_step score all-to-all");
         if (rc) return rc;
         sb += nsend;
     }
-    KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(x->ev_x, x->comm_st));
-    KGE_HIP_TRY("kge_shard_exec_step", hipStreamWaitEvent(st, x->ev_x, 0));
+    KGE_HIP_TRY("kge_shard_exec_step", hop(x->ev_x, cs, st));
     // 4. the home rows: scatter, positives, reductions
     rc = kge_shard_finish(s_recv, summ, hpre, pos, neg, neg_ld, x->Bg, x->N, x->nentity, W, me, mode, temperature,
                           adversarial, scores, ns_ld, out_neg, pos_scores, out_pos, st);

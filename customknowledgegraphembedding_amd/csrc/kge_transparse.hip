@@ -1093,6 +1093,255 @@ ts_fwd_x3s_kernel(TsParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Single / tail-batch forward (the grouped row source: each batch row's own head, relation pos[b,1]) with the
+// operands split once: ts_fwd_x3g_kernel. The B batch rows are few (512 at C6) and share M_r only within a
+// relation (~B / R rows each), so ts_rows_kernel's 128-row blocks gave 4 chunk blocks per relation, most of
+// them empty, each sweeping the columns 128 at a time: 279 us at C6 for 0.26 GFLOP. Here a block takes 64 rows
+// of one relation and ALL columns at once (8 waves x 64 columns, up to 512 per pass), so one block per relation
+// covers it in one pass over K; staging, planes and the pipeline are ts_fwd_x3s_kernel's.
+//   A: 64 rows x 16 k (threads 0..255, one float4 each); B: 16 k x 512 columns (two k pairs x column quads per
+//   thread), both split once into three bf16 planes, two LDS stages (108 KB), two register sets.
+//   Per wave and chunk: 2 A and 2 B fragments x 3 planes (12 ds_read_b128), 24 MFMAs.
+// The per-row sums over the columns are taken per wave (half-wave shuffles), then over the 8 waves in wave
+// order: the products are ts_rows_kernel's, the column sums in another order (scores within fp32 rounding).
+// ---------------------------------------------------------------------------------------------
+constexpr int XGR = 64, XGC = 512;
+constexpr int kXgAPlane = XGR * 32, kXgBPlane = XGC * 32;
+constexpr int kXgStage = 3 * (kXgAPlane + kXgBPlane);
+
+struct XgRegs {
+    float4 a, b[2][2], m[2][2];
+};
+
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(2))) void
+ts_fwd_x3g_kernel(TsParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char xg_smem[];  // 2 stages, then u - 1 (d floats)
+    __shared__ int rb[XGR], rid[XGR];
+    __shared__ float2 part[kXWaves][XGR];
+    __shared__ float2 red[XGR];
+    __shared__ float wsum[kXWaves];
+    __shared__ int wcnt[kXWaves];
+    float* cs = reinterpret_cast<float*>(xg_smem + 2 * kXgStage);
+
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int half = lane >> 5, col = lane & 31;
+    const int d = p.d;
+    const int64_t r = blockIdx.x / p.nchunk;  // == nrel: the out-of-range bucket
+    const int64_t skip = (int64_t)(blockIdx.x % p.nchunk) * XGR;
+    // this block's rows: the batch rows of relation bucket r, ranks [skip, skip + 64), by an ordered ballot scan
+    if (t < XGR) {
+        rb[t] = -1;
+        red[t] = make_float2(0.f, 0.f);
+    }
+    int64_t seen = 0;
+    for (int64_t s = 0; s < p.B; s += kXThreads) {
+        const int64_t b = s + t;
+        bool m = false;
+        if (b < p.B) {
+            const int64_t rr = p.pos[b * 3 + 1];
+            m = (r < p.nrel) ? (rr == r) : !(rr >= 0 && rr < p.nrel);
+        }
+        const uint64_t bal = __ballot(m);
+        if (lane == 0) wcnt[wave] = __popcll(bal);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kXWaves; ++w) {
+            before += (w < wave) ? wcnt[w] : 0;
+            total += wcnt[w];
+        }
+        if (m) {
+            const int64_t k = seen + before + __popcll(bal & ((1ull << lane) - 1ull)) - skip;
+            if (k >= 0 && k < XGR) rb[k] = (int)b;
+        }
+        seen += total;
+        __syncthreads();
+        if (seen >= skip + XGR) break;  // uniform
+    }
+    const int nrows = (int)min<int64_t>(XGR, seen - skip);
+    if (nrows <= 0) return;  // uniform
+    if (t < XGR) {
+        int id = -1;
+        if (rb[t] >= 0) {
+            const int64_t e = p.pos[(int64_t)rb[t] * 3];  // the head (Q9: the tail-batch score uses the head too)
+            if (e >= 0 && e < p.nent) id = (int)e;
+        }
+        rid[t] = id;
+    }
+    const bool rok = r >= 0 && r < p.nrel;
+    {  // u - 1 for the relation row
+        float ss = 0.f;
+        for (int j = t; j < d; j += kXThreads) {
+            const float v = rok ? p.rel[r * p.rel_ld + j] : 0.f;
+            cs[j] = v;
+            ss += v * v;
+        }
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, kWave);
+        if (lane == 0) wsum[wave] = ss;
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < kXWaves; ++w) tot += wsum[w];
+        const float rnorm = sqrtf(tot);
+        for (int j = t; j < d; j += kXThreads) cs[j] = cs[j] / rnorm - 1.f;
+    }
+    __syncthreads();
+    const rsrc_t ra = make_rsrc(p.ent, (uint32_t)(p.nent * p.ent_ld * 4));
+    const float* Wr = rok ? (p.Mpre ? p.Mpre : p.W) + r * (int64_t)d * d : p.W;
+    const uint32_t mbytes = rok ? (uint32_t)((int64_t)d * d * 4) : 0u;
+    const rsrc_t rw = make_rsrc(Wr, mbytes);
+    const bool fuse_mask = !p.Mpre;
+    const rsrc_t rm = make_rsrc(fuse_mask && rok ? p.mask + r * (int64_t)d * d : p.W, fuse_mask ? mbytes : 0u);
+    const int aid = t < 4 * XGR ? rid[t >> 2] : -1, aq = t & 3, bkp = t & 7, bjq = t >> 3;
+    const int nk = (d + 15) / 16, npass = (d + XGC - 1) / XGC, T = nk * npass;
+
+    auto gload = [&](XgRegs& R, int g) {
+        const int pc = g / nk, k0 = (g - pc * nk) * 16;
+        const int ka = k0 + 4 * aq;
+        const uint32_t oa = (aid >= 0 && ka < d) ? (uint32_t)(((int64_t)aid * p.ent_ld + ka) * 4) : kXsOOB;
+        const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa, 0, 0);
+        R.a = make_float4(__uint_as_float(va[0]), __uint_as_float(va[1]), __uint_as_float(va[2]), __uint_as_float(va[3]));
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int kb = k0 + 2 * bkp + h, j = pc * XGC + 4 * (bjq + 64 * u);
+                const uint32_t ob = (kb < d && j < d) ? (uint32_t)(((int64_t)kb * d + j) * 4) : kXsOOB;
+                const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rw, ob, 0, 0);
+                R.b[u][h] = make_float4(__uint_as_float(vb[0]), __uint_as_float(vb[1]), __uint_as_float(vb[2]),
+                                        __uint_as_float(vb[3]));
+                if (fuse_mask) {
+                    const auto vm = __builtin_amdgcn_raw_buffer_load_b128(rm, ob, 0, 0);
+                    R.m[u][h] = make_float4(__uint_as_float(vm[0]), __uint_as_float(vm[1]), __uint_as_float(vm[2]),
+                                            __uint_as_float(vm[3]));
+                }
+            }
+    };
+    auto sstore = [&](const XgRegs& R, int stage) {
+        unsigned char* A = xg_smem + stage * kXgStage;
+        unsigned char* Bp = A + 3 * kXgAPlane;
+        if (t < 4 * XGR) {
+            const int row = t >> 2;
+            bf16x4_t s0, s1, s2;
+            split3_x4(f32x4_t{R.a.x, R.a.y, R.a.z, R.a.w}, s0, s1, s2);
+            const int o = xs_off(row, aq >> 1) + (aq & 1) * 8;
+            *reinterpret_cast<bf16x4_t*>(A + o) = s0;
+            *reinterpret_cast<bf16x4_t*>(A + kXgAPlane + o) = s1;
+            *reinterpret_cast<bf16x4_t*>(A + 2 * kXgAPlane + o) = s2;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float4 b0 = R.b[u][0], b1 = R.b[u][1];
+            if (fuse_mask) {
+                b0 = mul4(b0, R.m[u][0]);
+                b1 = mul4(b1, R.m[u][1]);
+            }
+            bf16x4_t e0, e1, e2, o0, o1, o2;
+            split3_x4(f32x4_t{b0.x, b0.y, b0.z, b0.w}, e0, e1, e2);
+            split3_x4(f32x4_t{b1.x, b1.y, b1.z, b1.w}, o0, o1, o2);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int cl = 4 * (bjq + 64 * u) + c;
+                const int o = xs_off(cl, bkp >> 2) + (bkp & 3) * 4;
+                *reinterpret_cast<bf16x2_t*>(Bp + o) = bf16x2_t{e0[c], o0[c]};
+                *reinterpret_cast<bf16x2_t*>(Bp + kXgBPlane + o) = bf16x2_t{e1[c], o1[c]};
+                *reinterpret_cast<bf16x2_t*>(Bp + 2 * kXgBPlane + o) = bf16x2_t{e2[c], o2[c]};
+            }
+        }
+    };
+    f32x16 acc[2][2];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r2 = 0; r2 < 16; ++r2) acc[i][j][r2] = 0.f;
+    };
+    auto compute = [&](int stage) {
+        const unsigned char* A = xg_smem + stage * kXgStage;
+        const unsigned char* Bp = A + 3 * kXgAPlane;
+        bf16x8 a[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int o = xs_off(i * 32 + col, half);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * kXgAPlane + o);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int o = xs_off(wave * 64 + j * 32 + col, half);
+            bf16x8 bb[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) bb[pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * kXgBPlane + o);
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0, 0, 0);
+        }
+    };
+    auto fold = [&](int pc) {  // this pass's per-row sums: per wave over its 64 columns, then over the waves
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) {
+                float sq = 0.f, ab = 0.f;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int cg = pc * XGC + wave * 64 + j * 32 + col;
+                    const float c = cg < d ? cs[cg] : 0.f;
+                    const float v = acc[i][j][r2];
+                    sq = fmaf(v, v, sq);
+                    ab += fabsf(v * c);
+                }
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) {
+                    sq += __shfl_xor(sq, o, kWave);
+                    ab += __shfl_xor(ab, o, kWave);
+                }
+                if (col == 0) part[wave][i * 32 + (r2 & 3) + 8 * (r2 >> 2) + 4 * half] = make_float2(sq, ab);
+            }
+        __syncthreads();
+        if (t < XGR) {
+            float2 x = red[t];
+#pragma unroll
+            for (int w = 0; w < kXWaves; ++w) x = make_float2(x.x + part[w][t].x, x.y + part[w][t].y);
+            red[t] = x;
+        }
+    };
+    auto step = [&](int g, XgRegs& nxt) {
+        compute(g & 1);
+        if (g + 1 < T) sstore(nxt, (g + 1) & 1);
+        if (g + 3 < T) gload(nxt, g + 3);
+        if ((g + 1) % nk == 0) {
+            fold(g / nk);
+            zero_acc();
+        }
+        __syncthreads();
+    };
+    XgRegs R0, R1;
+    zero_acc();
+    gload(R0, 0);
+    if (T > 1) gload(R1, 1);
+    sstore(R0, 0);
+    if (T > 2) gload(R0, 2);
+    __syncthreads();
+    int g = 0;
+    for (; g + 1 < T; g += 2) {
+        step(g, R1);
+        step(g + 1, R0);
+    }
+    if (g < T) step(g, R1);
+    if (t < nrows) {
+        const float2 x = red[t];
+        const int64_t b = rb[t];
+        p.out[b * p.out_ld] = p.gamma - x.y / sqrtf(x.x);
+        if (p.stats) p.stats[b * p.N] = x;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void ts_premul_kernel(const float4* __restrict__ W, const float4* __restrict__ mask,
                                                           float4* __restrict__ M, int64_t n4) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock)
@@ -1419,6 +1668,21 @@ void launch_rows(const TsParams& p, hipStream_t st) {
                 const char* e = getenv("KGE_TS_BIG");
                 return e && e[0] == '0';
             }();
+            const char* xg_env = getenv("KGE_TS_X3S");
+            if (p.grouped && !(xg_env && xg_env[0] == '0') && p.d <= kXsMaxDim &&
+                p.nent * p.ent_ld * 4 < (int64_t)kXsOOB && (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB) {
+                // single / tail-batch rows: 64 rows of one relation x all columns per block (ts_fwd_x3g_kernel)
+                TsParams q = p;
+                q.nchunk = (int)((p.B + XGR - 1) / XGR);
+                const size_t lds = 2 * (size_t)kXgStage + (size_t)p.d * 4;
+                static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3g_kernel),
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                             2 * kXgStage + kXsMaxDim * 4) == hipSuccess;
+                (void)attr;
+                hipLaunchKernelGGL(ts_fwd_x3g_kernel, dim3((unsigned)((p.nrel + 1) * q.nchunk)), dim3(kXThreads), lds, st,
+                                   q);
+                return;
+            }
             if (!p.grouped && p.N > TBM && p.d <= kTsBigMaxDim && !big_off) {
                 TsParams q = p;
                 q.nchunk = (int)((p.N + XBR - 1) / XBR);

@@ -237,7 +237,7 @@ class NativeShardExec:
     world (collectives skipped, outputs meaningless: the host-cost probe). The workspace and the pinned
     summary buffers are torch allocations owned here."""
 
-    def __init__(self, sk, Bg, N, comm=None, probe=False, chunks=None):
+    def __init__(self, sk, Bg, N, comm=None, probe=False, chunks=None, one_stream=False):
         import ctypes
         lib = _lib.load()
         W, K = sk.world, default_chunks(sk.world, chunks)
@@ -249,7 +249,8 @@ class NativeShardExec:
         hi = lib.kge_shard_exec_host_ints(W, K)
         self.host = torch.empty(hi, dtype=torch.int32, pin_memory=True)
         h = ctypes.c_void_p()
-        check(lib.kge_shard_exec_create(ctypes.addressof(h), None if comm is None else comm.handle, 1 if probe else 0,
+        flags = (1 if probe else 0) | (2 if one_stream else 0)  # KGE_EXEC_PROBE, KGE_EXEC_ONE_STREAM
+        check(lib.kge_shard_exec_create(ctypes.addressof(h), None if comm is None else comm.handle, flags,
                                         sk.fn, sk.nentity, sk.shard.shape[0], sk.entity_dim, sk.D, Bg, N, W, sk.rank,
                                         K, ws, nbytes, self.host.data_ptr(), hi), "kge_shard_exec_create")
         self.handle = h.value
@@ -790,22 +791,32 @@ class ShardedKGE:
             at += n
         return out, send
 
-    def use_native(self, comm=None, probe=False):
+    def use_native(self, comm=None, probe=False, one_stream=None):
         """Run step_forward through the native executor (NativeShardExec: one C call per rank-step, RCCL
         issued from C++): `comm` a NativeComm (W > 1, or W = 1 through RCCL), None at W = 1 (device copies),
-        or `probe` (collectives skipped: host-cost measurement only). One executor per batch shape."""
+        or `probe` (collectives skipped: host-cost measurement only). One executor per batch shape.
+        one_stream: the collectives on the step's own stream (KGE_EXEC_ONE_STREAM), the default: at C4 x 8 a
+        rank-step's kernels run back to back in 100 us of device time that way, against 144-161 us with the
+        collectives on a communication stream, whose cross-stream event hops (the dependent queue's wake-up)
+        cost more than the overlap they buy (profiles/r04_native_timeline.txt); KGE_SHARD_ONE_STREAM=0 keeps
+        the communication stream. With one stream the batch is one chunk unless `chunks` is given."""
+        import os
         if comm is None and self.world > 1 and not probe:
             raise ValueError("the native executor needs a NativeComm at world > 1")
-        self._native_cfg = (comm, bool(probe))
+        if one_stream is None:
+            one_stream = os.environ.get("KGE_SHARD_ONE_STREAM", "1") != "0"
+        self._native_cfg = (comm, bool(probe), bool(one_stream))
         self._native = {}
         return self
 
     def _native_exec(self, Bg, N, chunks):
+        if chunks is None and self._native_cfg[2]:
+            chunks = 1  # one stream: no exchange overlaps scoring, and one scoring launch is the shortest
         key = (Bg, N, default_chunks(self.world, chunks))
         ex = self._native.get(key)
         if ex is None:
-            comm, probe = self._native_cfg
-            ex = self._native[key] = NativeShardExec(self, Bg, N, comm=comm, probe=probe, chunks=chunks)
+            comm, probe, one = self._native_cfg
+            ex = self._native[key] = NativeShardExec(self, Bg, N, comm=comm, probe=probe, chunks=chunks, one_stream=one)
         return ex
 
     @staticmethod

@@ -32,12 +32,12 @@ def _batch(E, R, Bg, N, seed):
     return pos.to(DEV), neg.to(DEV)
 
 
-def _native_ranks(m, W, group):
+def _native_ranks(m, W, group, one_stream=False):
     tables = (m.entity_embedding.detach(), m.relation_embedding.detach(), m._gamma_f, m._range_f, 0.0)
     ranks = [ShardedKGE(m.model_name, m.nentity, m.nrelation, m.hidden_dim, m._gamma_f, device=DEV, world=W,
                         rank=r, full_tables=tables) for r in range(W)]
     for r, sk in enumerate(ranks):
-        sk.use_native(group.comm(r) if group is not None else None)
+        sk.use_native(group.comm(r) if group is not None else None, one_stream=one_stream)
     return ranks
 
 
@@ -96,16 +96,18 @@ def test_world1_device_copies_bitwise(name):
         _check(m, ranks, batches, ahead=ahead)
 
 
-@pytest.mark.parametrize("W,K", [(2, 1), (2, 2), (4, 2), (8, 2), (8, 4)])
+@pytest.mark.parametrize("W,K,one", [(2, 1, False), (2, 2, False), (4, 2, False), (8, 2, False), (8, 4, False),
+                                     (4, 2, True), (8, 1, True)])
 @pytest.mark.parametrize("name", ["DistMult", "InterHT"])
-def test_loopback_ranks_bitwise(name, W, K):
+def test_loopback_ranks_bitwise(name, W, K, one):
     """W loopback ranks (one thread and one stream each): every home's outputs equal the unsharded kernels'
-    bitwise, over a chain of batches alternating head / tail (each step plans the next one)."""
+    bitwise, over a chain of batches alternating head / tail (each step plans the next one); with the
+    collectives on a communication stream or on the step's own (KGE_EXEC_ONE_STREAM)."""
     E, R, d, Bh, N = 5003, 5, 64, 8, 300
     m = _model(name, E, R, d)
     group = LoopbackGroup(W)
     try:
-        ranks = _native_ranks(m, W, group)
+        ranks = _native_ranks(m, W, group, one_stream=one)
         batches = [(*_batch(E, R, W * Bh, N, seed=10 + s), s % 2) for s in range(4)]
         _check(m, ranks, batches, K)
         for sk in ranks:

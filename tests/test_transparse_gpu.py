@@ -204,3 +204,35 @@ def test_split_once_forward_is_bitwise_the_register_split_one(monkeypatch, d, N,
     got = outs[1][0].numpy()
     assert rel_close(got[ok.numpy()], ref[ok.numpy()]) <= 1e-4
     assert np.isnan(got[~ok.numpy()]).all()
+
+
+@pytest.mark.parametrize("d,B,R,premul", [(500, 200, 3, True), (500, 130, 5, False), (1024, 70, 2, True),
+                                          (516, 90, 4, False)])
+@pytest.mark.parametrize("mode", [1, 3])
+def test_grouped_forward_all_columns_per_block(monkeypatch, d, B, R, premul, mode):
+    """Single / tail-batch rows (one relation's rows per block, all columns at once: ts_fwd_x3g_kernel): within
+    1e-4 of the fp64 oracle, within fp32 rounding of ts_rows_kernel's column order (KGE_TS_X3S=0), with rows of
+    out-of-range relations and heads (NaN), more than 64 rows per relation and d past one 512-column pass."""
+    E, gamma = 400, 12.0
+    ent, rel, W, mask = _tables(E, R, d, seed=5)
+    pos, neg = _batch(E, R, B, 3, seed=11)
+    pos[3, 1] = R + 2   # zero relation row -> NaN
+    pos[5, 0] = E + 1   # zero head row -> NaN
+    ed, rd, Wd, md = ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV)
+    M = ops.transparse_premul(Wd, md) if premul else None
+    got = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KGE_TS_X3S", flag)
+        st = torch.empty((B, 2), dtype=torch.float32, device=DEV)
+        s = ops.transparse_score_raw(mode, ed, rd, Wd, md, pos.to(DEV), neg.to(DEV), gamma, stats=st, M=M)
+        torch.cuda.synchronize()
+        got[flag] = (s.cpu().numpy(), st.cpu().numpy())
+    bad = np.zeros(B, dtype=bool)
+    bad[[3, 5]] = True
+    new, old = got["1"][0][:, 0], got["0"][0][:, 0]
+    assert np.isnan(new[bad]).all() and np.isnan(old[bad]).all()
+    assert np.abs(new[~bad] - old[~bad]).max() <= 1e-5 * max(1.0, np.abs(old[~bad]).max())
+    ok_pos = pos.clone()
+    ok_pos[3, 1], ok_pos[5, 0] = 0, 0
+    ref, _ = _oracle(ent, rel, W, mask, ok_pos, neg, mode, gamma)
+    assert rel_close(new[~bad], ref[~bad, 0]) <= 1e-4

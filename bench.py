@@ -677,15 +677,18 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
     return {"metric": f"ranked queries/sec, {w['name']}", "value": Bq * a.steps * world / dt, "unit": "queries/s",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "gemm_numerics": "fp32 operands split in registers into 3 bf16 terms each (24 significant bits), the six products "
-                             "A_i.B_j^T with i + j <= 2 on v_mfma_f32_32x32x16_bf16, fp32 accumulation: error vs fp64 "
-                             "within the fp32 MFMA path's (tests/test_eval_gpu.py)",
+            "gemm_numerics": "fp32 operands split once at staging into 3 bf16 terms each (24 significant bits), the six "
+                             "products A_i.B_j^T with i + j <= 2 on v_mfma_f32_32x32x16_bf16, fp32 accumulation: error "
+                             "vs fp64 within the fp32 MFMA path's (tests/test_eval_gpu.py)",
             "data": "synthetic triples (random init: MRR is not a quality number)",
             "config": {"workload": w["name"], "queries_per_step": Bq * world, "entities": E, "K": K,
                        "parallelism": f"replicas{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": mfma_flops / gemm_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                          "frac": mfma_flops / gemm_s / 1e12 / 2500.0, "traffic": None,
-                         "kernel": "gemm_nt_f32x3_kernel (v_mfma_f32_32x32x16_bf16, six products per 16 k)",
+                         "kernel": ("gemm_nt_f32x3_kernel (v_mfma_f32_32x32x16_bf16, six products per 16 k, operands "
+                                    "split per fragment)" if os.environ.get("KGE_GEMM_X3S", "1") == "0" else
+                                    "gemm_nt_x3s_kernel (256 x 256 tiles, operands split once at staging into bf16 "
+                                    "planes, six products per 16 k on v_mfma_f32_32x32x16_bf16)"),
                          "kernel_avg_us": gemm_s * 1e6,
                          "fp32_equivalent_tflops": flops / gemm_s / 1e12,
                          "fp32_equivalent_over_fp32_mfma_peak": flops / gemm_s / 1e12 / 157.3},
@@ -763,9 +766,12 @@ def transparse_bench(w, a, device):
             "config": {"workload": w["name"], "global_batch": B, "n_neg": N, "d": d},
             "roofline": ({"bound": "mfma", "achieved": mfma_flops / k_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                           "frac": mfma_flops / k_s / 1e12 / 2500.0, "traffic": None,
-                          "kernel": ("ts_fwd_x3_kernel (256 negatives of one batch row per block, M_r chunks staged "
-                                     "once for all of them; bf16x3 split in registers, six products on "
-                                     "v_mfma_f32_32x32x16_bf16, fp32 accumulation)"
+                          "kernel": (("ts_fwd_x3s_kernel (256 negatives of one batch row per block, M_r chunks staged "
+                                      "once for all of them; operands split once at staging into bf16 planes, six "
+                                      "products on v_mfma_f32_32x32x16_bf16, fp32 accumulation)")
+                                     if os.environ.get("KGE_TS_X3S", "1") != "0" else
+                                     ("ts_fwd_x3_kernel (256 negatives of one batch row per block; bf16x3 split in "
+                                      "registers, six products on v_mfma_f32_32x32x16_bf16)"))
                                      if os.environ.get("KGE_TS_BIG", "1") != "0" else
                                      "ts_rows_kernel<TS_FWD, 4, true> (128-row blocks, bf16x3 on the bf16 MFMA)"),
                           "kernel_avg_us": k_s * 1e6, "fp32_equivalent_tflops": flops / k_s / 1e12,

@@ -150,3 +150,25 @@ def test_countries_auc_pr_matches_oracle():
     ent, rel = m.entity_embedding.detach().cpu().double(), m.relation_embedding.detach().cpu().double()
     s = O.score("TransE", ent, rel, torch.tensor(sample), None, "single", 1.0)[:, 0].numpy()
     assert abs(got["auc_pr"] - average_precision_score(np.array(y), s)) < 1e-9
+
+
+@pytest.mark.parametrize("M,N,K,lda", [(1, 1, 4, 4), (37, 300, 64, 64), (257, 513, 1000, 1000), (300, 131, 12, 16),
+                                       (1024, 1500, 2000, 2000), (64, 14951, 1000, 1004)])
+def test_gemm_split_once_is_bitwise_the_register_split_kernel(monkeypatch, M, N, K, lda):
+    """gemm_nt_x3s_kernel (operands split once at staging into bf16 planes, 256 x 256 tiles) against
+    gemm_nt_f32x3_kernel (the same six products per 16-k step, split per fragment in the MFMA loop): C is
+    bitwise equal, with partial tiles in M, N and K and a padded leading dimension."""
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    A = (torch.randn(M, lda, generator=g) * torch.logspace(-2, 2, lda)).to(DEV)
+    Bm = torch.randn(N, K, generator=g).to(DEV)
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KGE_GEMM_X3S", flag)
+        C = torch.full((M, N + 3), -7.0, device=DEV)
+        assert lib.kge_gemm_nt_bf16x3(A.data_ptr(), lda, Bm.data_ptr(), K, C.data_ptr(), N + 3, M, N, K, st) == 0
+        torch.cuda.synchronize()
+        out.append(C.cpu())
+    assert torch.equal(out[0], out[1])
+    assert bool((out[1][:, N:] == -7.0).all())  # nothing written past N

@@ -771,7 +771,7 @@ def transparse_bench(w, a, device):
                                       "products on v_mfma_f32_32x32x16_bf16, fp32 accumulation)")
                                      if os.environ.get("KGE_TS_X3S", "1") != "0" else
                                      ("ts_fwd_x3_kernel (256 negatives of one batch row per block; bf16x3 split in "
-                                      "registers, six products on v_mfma_f32_32x32x16_bf16)"))
+                                      "registers, six products on v_mfma_f32_32x32x16_bf16)")
                                      if os.environ.get("KGE_TS_BIG", "1") != "0" else
                                      "ts_rows_kernel<TS_FWD, 4, true> (128-row blocks, bf16x3 on the bf16 MFMA)"),
                           "kernel_avg_us": k_s * 1e6, "fp32_equivalent_tflops": flops / k_s / 1e12,

@@ -766,14 +766,7 @@ def transparse_bench(w, a, device):
             "config": {"workload": w["name"], "global_batch": B, "n_neg": N, "d": d},
             "roofline": ({"bound": "mfma", "achieved": mfma_flops / k_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                           "frac": mfma_flops / k_s / 1e12 / 2500.0, "traffic": None,
-                          "kernel": (("ts_fwd_x3s_kernel (256 negatives of one batch row per block, M_r chunks staged "
-                                      "once for all of them; operands split once at staging into bf16 planes, six "
-                                      "products on v_mfma_f32_32x32x16_bf16, fp32 accumulation)")
-                                     if os.environ.get("KGE_TS_X3S", "1") != "0" else
-                                     ("ts_fwd_x3_kernel (256 negatives of one batch row per block; bf16x3 split in "
-                                      "registers, six products on v_mfma_f32_32x32x16_bf16)")
-                                     if os.environ.get("KGE_TS_BIG", "1") != "0" else
-                                     "ts_rows_kernel<TS_FWD, 4, true> (128-row blocks, bf16x3 on the bf16 MFMA)"),
+                          "kernel": ts_kernel_name(),
                           "kernel_avg_us": k_s * 1e6, "fp32_equivalent_tflops": flops / k_s / 1e12,
                           "fp32_equivalent_over_fp32_mfma_peak": flops / k_s / 1e12 / 157.3}
                          if x3 else
@@ -781,6 +774,19 @@ def transparse_bench(w, a, device):
                           "frac": flops / k_s / 1e12 / 157.3, "traffic": None,
                           "kernel": "ts_rows_kernel<TS_FWD> (v_mfma_f32_32x32x2_f32)", "kernel_avg_us": k_s * 1e6}),
             "train_step": train, "build": kge.build_id()}
+
+
+def ts_kernel_name():
+    """The head-batch TranSparse forward kernel launch_rows<TS_FWD> picks (kge_transparse.hip) under the A/B
+    knobs KGE_TS_BIG and KGE_TS_X3S."""
+    if os.environ.get("KGE_TS_BIG", "1") == "0":
+        return "ts_rows_kernel<TS_FWD, 4, true> (128-row blocks, bf16x3 on the bf16 MFMA)"
+    if os.environ.get("KGE_TS_X3S", "1") == "0":
+        return ("ts_fwd_x3_kernel (256 negatives of one batch row per block; bf16x3 split in registers, six products "
+                "on v_mfma_f32_32x32x16_bf16)")
+    return ("ts_fwd_x3s_kernel (256 negatives of one batch row per block, M_r chunks staged once for all of them; "
+            "operands split once at staging into bf16 planes, six products on v_mfma_f32_32x32x16_bf16, fp32 "
+            "accumulation)")
 
 
 def train_step_bench(m, batches, steps, warmup):

@@ -977,20 +977,27 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         }
         __syncthreads();
         if (w == 0) {  // bucket v = lane: prefix over the waves in row order, then over the buckets
+            // (the counts are loaded all together and summed in registers: a dependent LDS round trip per wave
+            // slot cost ~1.5 us of the block's setup)
+            int y[MU * NWV];
+#pragma unroll
+            for (int c = 0; c < MU * NWV; ++c) y[c] = wc[c * NB + lane];
             int run = 0;
+#pragma unroll
             for (int c = 0; c < MU * NWV; ++c) {
-                const int y = wc[c * NB + lane];
-                wc[c * NB + lane] = run;
-                run += y;
+                const int v = y[c];
+                y[c] = run;
+                run += v;
             }
             int incl = run;
 #pragma unroll
             for (int o = 1; o < kWave; o <<= 1) {
-                const int y = __shfl_up(incl, o, kWave);
-                if (lane >= o) incl += y;
+                const int v = __shfl_up(incl, o, kWave);
+                if (lane >= o) incl += v;
             }
             const int base = incl - run;
-            for (int c = 0; c < MU * NWV; ++c) wc[c * NB + lane] += base;
+#pragma unroll
+            for (int c = 0; c < MU * NWV; ++c) wc[c * NB + lane] = y[c] + base;
         }
         __syncthreads();
 #pragma unroll
@@ -1028,8 +1035,10 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         return true;
     };
     // the ids are loaded once, all in flight together, when the block's walk fits TPI per thread (C2: 4 112
-    // items over 512 threads); otherwise the walk is made twice (count, then scatter)
-    constexpr int TPI = 16;
+    // items over 768 threads); otherwise the walk is made twice (count, then scatter)
+    // 17 at 16 waves: a 16-row block's 16 x 1 025 tail-batch items at N = 1 024 (C4) over 1 024 threads, walked
+    // once (C4 tail-batch 94.5 -> 88 us); 16 at fewer waves, where the 17th slot measured ~1 us slower at C3
+    constexpr int TPI = NWV >= 16 ? 17 : 16;
     int wbk[TPI], wcd[TPI];
     const bool in_regs = nf <= (int64_t)TPI * NT;  // block-uniform
     // (their loads are issued here, before the query build, so both latencies overlap)
@@ -1079,15 +1088,15 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     if constexpr (FN == KGE_INTERHT) {
         // relation slots: one per run of equal relations among the block's rows (first QS runs; the rows of
         // later runs read their relation third from the table per candidate)
-        if (t == 0) {
-            int sl = -1;
-            int64_t prev = INT64_MIN;
-            for (int r = 0; r < nr; ++r) {
-                if (rrow[r] != prev) {
-                    ++sl;
-                    prev = rrow[r];
-                }
-                q2slot[r] = sl < QS ? sl : -1;
+        static_assert(kTileMaxRows <= kWave, "one lane per row");
+        if (w == 0) {  // lane r: row r opens a run when its relation differs from row r - 1's
+            const bool in = lane < nr;
+            const int64_t cur = in ? rrow[lane] : 0;
+            const bool open = in && (lane == 0 || cur != rrow[lane - 1]);
+            const uint64_t m = __ballot(open);
+            if (in) {
+                const int sl = __popcll(m & (lane == 63 ? ~0ull : (2ull << lane) - 1)) - 1;
+                q2slot[lane] = sl < QS ? sl : -1;
             }
         }
     }

@@ -631,7 +631,7 @@ int tile_plan(int fn, ScoreParams& p) {
     const char* wenv = getenv("KGE_TILE_WAVES");
     if (wenv && (atoi(wenv) == 8 || atoi(wenv) == 12 || atoi(wenv) == 16)) p.tile_waves = atoi(wenv);
     const int64_t NT = (int64_t)p.tile_waves * kWave;
-    const int64_t qrow = tile_nq(fn) * opb + 8 + 8 + 4, lrow = (p.N + 1) * 4;
+    const int64_t qrow = tile_nq(fn) * opb + 8 + 8 + 8 + 4, lrow = (p.N + 1) * 4;  // + rrow, brow, qid, q2slot
     const int64_t fixed = kTileBuckets * 4 + 16;
     // the list region also holds the relation sort's per-wave bucket counts ([ceil(kTileSortMaxB / NT) NWV][64],
     // step_fwd_tile_kernel step 0), sized for the block's actual wave count

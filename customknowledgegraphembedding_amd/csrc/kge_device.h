@@ -907,10 +907,14 @@ step_fwd_xcd_kernel(ScoreParams p) {
 // and walks its row's ids once per phase) a row's query is built 8 times per launch, not 8 P times.
 // Every candidate is scored by cand_score with the same operand values as every other form: the scores
 // are bitwise those of step_fwd_kernel / step_fwd_xcd_kernel.
-// LDS (dynamic, p.tile_lds bytes): query images [R][tile_nq][G * 64] vecf<V>, relation rows [R] (int64),
+// LDS (dynamic, p.tile_lds bytes): query images [R][tile_nq][G * 64] vecf<V>, relation rows, batch rows and
+// query entity ids [R] (int64 each),
 // bucket counts / cursors [kTileBuckets], the item count, the sorted list [R (N + 1)] of (row << 16 | column)
 // (column N: the row's positive).
 // ---------------------------------------------------------------------------------------------
+#ifndef KGE_TILE_EXP
+#define KGE_TILE_EXP 0  // A/B experiments on the setup only (scripts/gpu_r04_l.sh); 0 in every shipped build
+#endif
 template <int V, int G>
 struct TileQueryIH {  // InterHT: q0, q1 from LDS, the relation third in registers
     LdsOperand<V> q0, q1;
@@ -928,7 +932,8 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     vecf<V>* q2img = qimg + (size_t)R * NQ * W;               // [QS][W] InterHT relation thirds
     int64_t* rrow = reinterpret_cast<int64_t*>(q2img + (size_t)QS * W);
     int64_t* brow = rrow + R;
-    int* q2slot = reinterpret_cast<int*>(brow + R);
+    int64_t* qid = brow + R;  // the rows' query entity ids, read with the relation ids in step 0
+    int* q2slot = reinterpret_cast<int*>(qid + R);
     int* hist = q2slot + R;
     int* cntp = hist + kTileBuckets;
     int* list = cntp + 4;  // also the relation sort's keys before the list is built
@@ -951,12 +956,16 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         constexpr int MU = (kTileSortMaxB + NT - 1) / NT, NB = kTileSortRel;
         int* wc = list;  // [MU NWV][NB] per-wave bucket counts, then their exclusive prefixes
         int bk[MU], wr[MU];
+        int64_t rv[MU], qv[MU];
 #pragma unroll
         for (int u = 0; u < MU; ++u) {
             const int i = u * NT + t;
             bk[u] = NB;
+            rv[u] = qv[u] = 0;
             if (i < p.B) {
                 const int64_t rr = p.r_idx ? p.r_idx[i * p.r_stride] : i;
+                rv[u] = rr;
+                qv[u] = p.q_idx ? p.q_idx[i * p.q_stride] : i;
                 bk[u] = (rr >= 0 && rr < p.r_rows) ? (int)min<int64_t>(rr, NB - 2) : NB - 1;
             }
         }
@@ -1004,10 +1013,17 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         for (int u = 0; u < MU; ++u) {
             if (bk[u] >= NB) continue;
             const int64_t rank = wc[(u * NWV + w) * NB + bk[u]] + wr[u];
-            if (rank >= g0 && rank < g0 + nr) brow[rank - g0] = u * NT + t;
+            if (rank >= g0 && rank < g0 + nr) {
+                brow[rank - g0] = u * NT + t;
+                qid[rank - g0] = qv[u];
+                rrow[rank - g0] = rv[u];
+            }
         }
     } else if (t < nr) {
-        brow[t] = g0 + t;
+        const int64_t b = g0 + t;
+        brow[t] = b;
+        qid[t] = p.q_idx ? p.q_idx[b * p.q_stride] : b;
+        rrow[t] = p.r_idx ? p.r_idx[b * p.r_stride] : b;
     }
     __syncthreads();
     if (p.tile_dry == 1) return;  // A/B knob KGE_TILE_DRY=<level>: the setup up to this point alone
@@ -1040,7 +1056,11 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     // once (C4 tail-batch 94.5 -> 88 us); 16 at fewer waves, where the 17th slot measured ~1 us slower at C3
     constexpr int TPI = NWV >= 16 ? 17 : 16;
     int wbk[TPI], wcd[TPI];
+#if KGE_TILE_EXP == 1
+    const bool in_regs = false;  // experiment: the walk made after the query build (the two-pass form)
+#else
     const bool in_regs = nf <= (int64_t)TPI * NT;  // block-uniform
+#endif
     // (their loads are issued here, before the query build, so both latencies overlap)
     if (in_regs) {
 #pragma unroll
@@ -1052,7 +1072,18 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     }
 
     // 1. the rows' query operands; with fewer waves than rows, two rows per wave built side by side (branch-free:
-    //    both rows' loads in flight together)
+    //    both rows' loads in flight together). The ids come from LDS (step 0 read them with the relation ids), so
+    //    the rows' loads are not behind a dependent id load
+    auto build_row = [&](int r, Query<FN, CH, V, G>& q, int64_t& ri, bool& rok) {
+        const int64_t qi = qid[r];
+        ri = rrow[r];  // the raw relation id until put() replaces it with the checked one
+        bool qok = qi >= 0 && qi < p.q_rows;
+        rok = ri >= 0 && ri < p.r_rows;
+#if KGE_TILE_EXP == 2
+        qok = rok = false;  // experiment: the query rows read as zeros (no memory traffic)
+#endif
+        q.build(p.qent + (qok ? qi : 0) * p.q_ld, qok, p.rel + (rok ? ri : 0) * p.r_ld + p.r_off, rok, p.D, lane, p);
+    };
     auto put = [&](int r, const Query<FN, CH, V, G>& q, int64_t ri, bool rok) {
         vecf<V>* qr = qimg + (size_t)r * NQ * W;
 #pragma unroll
@@ -1066,19 +1097,19 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         for (int r = w; r < nr; r += 2 * NWV) {
             const int r2 = r + NWV < nr ? r + NWV : r;
             Query<FN, CH, V, G> qa, qb;
-            int64_t qi, ri, qi2, ri2;
-            bool qok, rok, qok2, rok2;
-            build_query_for<FN, CH, V, G>(p, brow[r], lane, qa, qi, ri, qok, rok);
-            build_query_for<FN, CH, V, G>(p, brow[r2], lane, qb, qi2, ri2, qok2, rok2);
+            int64_t ri, ri2;
+            bool rok, rok2;
+            build_row(r, qa, ri, rok);
+            build_row(r2, qb, ri2, rok2);
             put(r, qa, ri, rok);
             if (r2 != r) put(r2, qb, ri2, rok2);
         }
     } else {
         for (int r = w; r < nr; r += NWV) {
             Query<FN, CH, V, G> q;
-            int64_t qi, ri;
-            bool qok, rok;
-            build_query_for<FN, CH, V, G>(p, brow[r], lane, q, qi, ri, qok, rok);
+            int64_t ri;
+            bool rok;
+            build_row(r, q, ri, rok);
             put(r, q, ri, rok);
         }
     }

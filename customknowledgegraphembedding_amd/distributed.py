@@ -652,7 +652,7 @@ class ShardedKGE:
                              double_relation_embedding, triple_relation_embedding, device="cpu", seed=seed)
             ent, rel = ref.entity_embedding.detach(), ref.relation_embedding.detach()
             self.gamma, self.emb_range = ref._gamma_f, ref._range_f
-            self.modulus = float(ref.modulus.reshape(-1)[0]) if model_name == "pRotatE" else 0.0
+            self.modulus = float(ref.modulus.detach().reshape(-1)[0]) if model_name == "pRotatE" else 0.0
         else:
             ent, rel, self.gamma, self.emb_range, self.modulus = full_tables
         self.entity_dim, self.relation_dim = ent.shape[1], rel.shape[1]
@@ -686,7 +686,7 @@ class ShardedKGE:
         rel = model.relation_embedding.data
         if isinstance(comm, (ThreadComm, _ThreadCommRank)):
             rel = rel.clone()
-        modulus = float(model.modulus.reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0
+        modulus = float(model.modulus.detach().reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0
         return cls(model.model_name, model.nentity, model.nrelation, model.hidden_dim, model._gamma_f,
                    device=ent.device, group=group, kernels=kernels, world=world, rank=rank, comm=comm,
                    full_tables=(ent, rel, model._gamma_f, model._range_f, modulus))

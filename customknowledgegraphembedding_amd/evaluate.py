@@ -79,7 +79,7 @@ def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor
                                      out.stride(0), B, E, K, st), "kge_gemm_nt_bf16x3")
         return out
     cand = torch.arange(E, device=dev, dtype=torch.int64).unsqueeze(0).expand(B, E)  # row stride 0
-    modulus = float(model.modulus.reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0
+    modulus = float(model.modulus.detach().reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0
     return ops.score_indexed_raw(FN_IDS[model.model_name], m, ent, rel, model._rel_off, positive_sample, cand,
                                  model._D, model._gamma_f, model._range_f, modulus, out=out)
 

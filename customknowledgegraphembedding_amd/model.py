@@ -75,7 +75,7 @@ class _KGEBase(nn.Module):
                 ew = head.shape[-1]
                 D = ew // 2 if name in SPLIT_ENTITY else ew
                 rel_off = D if name == "InterHT" else 0
-                mod = float(self.modulus.reshape(-1)[0]) if name == "pRotatE" else 0.0
+                mod = float(self.modulus.detach().reshape(-1)[0]) if name == "pRotatE" else 0.0
                 return ops.score_dense(fn, m, head, relation, tail, D, self._gamma_f, self._range_f,
                                        rel_off=rel_off, modulus=mod)
 
@@ -238,7 +238,7 @@ class TFKGEModel(_KGEBase):
                                          one_call=False)
             loss_sum += loss
             return loss
-        modulus = float(self.modulus.reshape(-1)[0]) if is_p else 0.0
+        modulus = float(self.modulus.detach().reshape(-1)[0]) if is_p else 0.0
         stats = (torch.empty((negative_sample.shape[0] * negative_sample.shape[1], 2), dtype=torch.float32,
                              device=ent.device) if self.model_name == "InterHT" else None)
         out_neg, out_pos, ns, ps = ops.step_forward_raw(fn, m, ent.detach(), rel.detach(), self._rel_off,

@@ -36,7 +36,7 @@ def _batch(E, R, Bg, N, seed, bad=False):
 
 
 def _ranks(m, W, comm=None):
-    mod = float(m.modulus.reshape(-1)[0]) if m.model_name == "pRotatE" else 0.0
+    mod = float(m.modulus.detach().reshape(-1)[0]) if m.model_name == "pRotatE" else 0.0
     tables = (m.entity_embedding.detach(), m.relation_embedding.detach(), m._gamma_f, m._range_f, mod)
     comm = comm or ThreadComm(W)
     return [ShardedKGE(m.model_name, m.nentity, m.nrelation, m.hidden_dim, m._gamma_f, device=DEV, world=W,
@@ -81,7 +81,7 @@ def _check_world(name, W, K, E, R, d, Bh, N, seed, bad=False):
     m = _model(name, E, R, d)
     fn = FN_IDS[name]
     ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
-    mod = float(m.modulus.reshape(-1)[0]) if name == "pRotatE" else 0.0
+    mod = float(m.modulus.detach().reshape(-1)[0]) if name == "pRotatE" else 0.0
     pos, neg = _batch(E, R, W * Bh, N, seed, bad)
     ranks = _ranks(m, W)
     for mode in (0, 1):

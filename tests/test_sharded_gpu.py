@@ -27,7 +27,7 @@ def test_shards_sum_to_unsharded_bitwise(name, mode):
     pos = torch.from_numpy(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1)).to(DEV)
     neg = torch.from_numpy(g.randint(E, size=(B, N))).to(DEV)
     ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
-    mod = float(m.modulus.reshape(-1)[0]) if name == "pRotatE" else 0.0
+    mod = float(m.modulus.detach().reshape(-1)[0]) if name == "pRotatE" else 0.0
     fn = FN_IDS[name]
     want = ops.score_indexed_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f, mod)
     qcol = 2 if mode == 0 else 0

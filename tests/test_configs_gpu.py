@@ -4,7 +4,8 @@ flags (model.py:4-44 / upstream KGEModel.train_step: adversarial vs mean, temper
 L3 regularisation) against the oracle's fp64 autograd.
 
 Full-size kernels run over the whole [B, N] batch; the fp64 oracle checks sampled rows (the
-oracle's [rows, N, d] gather finishes in seconds). Bar: |got - ref| <= 1e-4 max(1, |ref|)."""
+oracle's [rows, N, d] gather finishes in seconds), and every row in chunks for C2 (scores and row outputs, both
+modes) and C3 / C4 (scores, one mode each). Bar: |got - ref| <= 1e-4 max(1, |ref|)."""
 import os
 import types
 
@@ -63,6 +64,48 @@ def _step_forward_vs_oracle(name, E, R, d, gamma, de, dr, tr, key, B, N):
 def test_c2_wn18rr_interht_full_size_real_positives():
     """C2: WN18RR InterHT d=1000 -de -tr gamma=24, B=512, N=256, positives from train.txt."""
     _step_forward_vs_oracle("InterHT", 40943, 11, 1000, 24.0, True, False, True, "wn18rr", 512, 256)
+
+
+def _all_rows_vs_oracle(name, E, R, d, gamma, de, dr, tr, key, B, N, modes, outputs, chunk=64):
+    """Every batch row of a full-size step (not the sampled ROWS) against the fp64 oracle, in chunks of rows
+    so the oracle's [chunk, N, d] gathers stay small: the raw scores, and with `outputs` the two calls' row
+    outputs (self-adversarial negative term, positive log-sigmoid)."""
+    m = kge.TFKGEModel(name, E, R, d, gamma, double_entity_embedding=de, double_relation_embedding=dr,
+                       triple_relation_embedding=tr, device=DEV, seed=0)
+    ent = m.entity_embedding.detach().cpu().double()
+    rel = m.relation_embedding.detach().cpu().double()
+    pos, neg = _batch(key, E, B, N, seed=3)
+    fn = FN_IDS[name]
+    for mode in modes:
+        out_neg, out_pos, ns, _ = ops.step_forward_raw(fn, mode, m.entity_embedding.detach(),
+                                                       m.relation_embedding.detach(), m._rel_off, pos.to(DEV),
+                                                       neg.to(DEV), m._D, m._gamma_f, m._range_f)
+        torch.cuda.synchronize()
+        ns, out_neg, out_pos = ns.cpu().numpy(), out_neg.cpu().numpy(), out_pos.cpu().numpy()
+        worst = 0.0
+        for r0 in range(0, B, chunk):
+            rows = slice(r0, min(B, r0 + chunk))
+            ref_s = O.score(name, ent, rel, pos[rows], neg[rows], mode, gamma, m._range_f).numpy()
+            worst = max(worst, rel_close(ns[rows], ref_s))
+            if outputs:
+                ref_n = O.tf_call(name, ent, rel, pos[rows], neg[rows], mode, gamma, m._range_f).numpy()[:, 0]
+                ref_p = O.tf_call(name, ent, rel, pos[rows], neg[rows], 3, gamma, m._range_f).numpy()[:, 0]
+                worst = max(worst, rel_close(out_neg[rows], ref_n), rel_close(out_pos[rows], ref_p))
+        assert worst <= TOL, (name, mode, worst)
+
+
+def test_c2_every_row_full_size():
+    """C2 (the headline): all 512 rows x 256 negatives of a full-size WN18RR InterHT step, both modes, scores
+    and both calls' row outputs against the fp64 oracle (the tile order's whole output, not sampled rows)."""
+    _all_rows_vs_oracle("InterHT", 40943, 11, 1000, 24.0, True, False, True, "wn18rr", 512, 256, (0, 1), True)
+
+
+def test_c3_c4_every_row_scores_full_size():
+    """C3 head-batch and C4 tail-batch: every row's raw scores of a full-size step against the fp64 oracle
+    (the other modes and the row outputs are covered on sampled rows above)."""
+    _all_rows_vs_oracle("RotatE", 14541, 237, 1000, 9.0, True, False, False, "fb15k237", 512, 256, (0,), False)
+    _all_rows_vs_oracle("DistMult", 123182, 37, 500, 24.0, False, False, False, "yago3_10", 512, 1024, (1,), False,
+                        chunk=32)
 
 
 def test_c2_xcd_phases_bitwise():

@@ -1448,6 +1448,29 @@ __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
 //   * positive triple: single-mode score (tail formula) -> raw + logsigmoid   (model.py:127-146)
 //   * negative row b: sum softmax(T s) logsigmoid(-s) or mean logsigmoid(-s)  (model.py:168-171)
 // ---------------------------------------------------------------------------------------------
+// The forward row reductions' exp / log on the hardware v_exp_f32 / v_log_f32 (KGE_RR_HW = 1; ~1 ulp, well inside
+// the 1e-4 parity bar): with libm's expf / log1pf the C4 reduction (1 024 scores per row, 16 per lane, three
+// transcendentals each) was compute-bound at 8.1 us per launch, 4.8 us on the hardware units
+// (profiles/r04_tile_setup_ab.txt). Every form's reduction (fused, neg_rows, neg_reduce, the row-sharded finish)
+// uses these two, so the forms stay bitwise equal to one another.
+#ifndef KGE_RR_HW
+#define KGE_RR_HW 1
+#endif
+__device__ __forceinline__ float rr_exp(float x) {
+#if KGE_RR_HW
+    return __expf(x);
+#else
+    return expf(x);
+#endif
+}
+__device__ __forceinline__ float rr_log_sigmoid(float x) {
+#if KGE_RR_HW
+    return fminf(x, 0.f) - __logf(1.f + __expf(-fabsf(x)));
+#else
+    return log_sigmoid(x);
+#endif
+}
+
 __device__ __forceinline__ float row_reduce(const float* row, int64_t N, float T, int adversarial, int lane) {
     if (adversarial) {
         float m = -INFINITY;
@@ -1456,14 +1479,14 @@ __device__ __forceinline__ float row_reduce(const float* row, int64_t N, float T
         float z = 0.f, w = 0.f;
         for (int64_t n = lane; n < N; n += kWave) {
             const float x = row[n];
-            const float e = expf(T * x - m);
+            const float e = rr_exp(T * x - m);
             z += e;
-            w += e * log_sigmoid(-x);
+            w += e * rr_log_sigmoid(-x);
         }
         return wave_sum(w) / wave_sum(z);
     }
     float w = 0.f;
-    for (int64_t n = lane; n < N; n += kWave) w += log_sigmoid(-row[n]);
+    for (int64_t n = lane; n < N; n += kWave) w += rr_log_sigmoid(-row[n]);
     return wave_sum(w) / (float)N;
 }
 
@@ -1483,16 +1506,16 @@ __device__ __forceinline__ float row_reduce_vals(const float (&v)[NR], int64_t N
 #pragma unroll
         for (int k = 0; k < NR; ++k)
             if (lane + (int64_t)k * kWave < N) {
-                const float e = expf(T * v[k] - m);
+                const float e = rr_exp(T * v[k] - m);
                 z += e;
-                wsum += e * log_sigmoid(-v[k]);
+                wsum += e * rr_log_sigmoid(-v[k]);
             }
         return wave_sum(wsum) / wave_sum(z);
     }
     float wsum = 0.f;
 #pragma unroll
     for (int k = 0; k < NR; ++k)
-        if (lane + (int64_t)k * kWave < N) wsum += log_sigmoid(-v[k]);
+        if (lane + (int64_t)k * kWave < N) wsum += rr_log_sigmoid(-v[k]);
     return wave_sum(wsum) / (float)N;
 }
 

@@ -446,8 +446,8 @@ __global__ __launch_bounds__(kBlock) void shard_finish_block_kernel(
     for (int j = 0; j < SPW; ++j) {
         const int k = w * SPW + j;
         if (lane + (int64_t)k * kWave < N) {
-            if (adversarial) ev[k][lane] = expf(T * v[j] - m);
-            lv[k][lane] = log_sigmoid(-v[j]);
+            if (adversarial) ev[k][lane] = rr_exp(T * v[j] - m);  // row_reduce's exp / log (kge_device.h)
+            lv[k][lane] = rr_log_sigmoid(-v[j]);
         }
     }
     __syncthreads();

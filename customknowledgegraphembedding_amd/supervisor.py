@@ -162,7 +162,7 @@ class Trainer:
             # as the row-sharded path records it
             self.metrics.update_state(self.strategy.sum_over_replicas(loss.detach())
                                       * self.strategy.num_replicas_in_sync)
-            return loss
+            return loss.detach()  # the backward has run; the value is what the caller reads
 
         return self.strategy.run(train_step_fn, next(data_iter))
 

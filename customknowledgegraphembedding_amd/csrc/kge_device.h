@@ -257,6 +257,9 @@ constexpr bool rel_split(int fn) { return fn == KGE_COMPLEX; }
 #ifndef KGE_ROT_CHUNK
 #define KGE_ROT_CHUNK 4  // RotatE query build: cos / sin of this many elements per iteration of a rolled loop
 #endif
+#ifndef KGE_ROT_HW
+#define KGE_ROT_HW 1  // RotatE query build on the hardware sin / cos (0: libm, rolled KGE_ROT_CHUNK at a time)
+#endif
 template <int FN, bool CH, int V, int G>
 struct Query {
     vecf<V> q0[G], q1[G], q2[G];
@@ -306,6 +309,23 @@ struct Query {
         // with wave-uniform selects): libm's cosf / sinf carry their large-argument reduction state, and
         // G V of them interleaved made the XCD-sliced kernels spill (98 VGPRs at D = 1000)
         float rc[G][V], rs[G][V];
+#if KGE_ROT_HW
+        // the hardware v_sin_f32 / v_cos_f32 (__sinf / __cosf, the phase scaled to revolutions): the phases are
+        // r / phase_div, within [-pi, pi] at initialisation (|r| <= the embedding range) and a few pi after
+        // training, where they are accurate to ~1e-6 absolute (the scores' 1e-4 bar is orders looser); two
+        // instructions per element instead of libm's argument reduction, which put the query build of the tile
+        // kernel's setup and of the head-batch positives on a long VALU chain
+        if constexpr (FN == KGE_ROTATE) {
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    const float ph = ra[k].a[i] / p.phase_div;
+                    rc[k][i] = __cosf(ph);
+                    rs[k][i] = __sinf(ph);
+                }
+        }
+#else
         if constexpr (FN == KGE_ROTATE) {
             constexpr int RU = KGE_ROT_CHUNK < G * V ? KGE_ROT_CHUNK : G * V;  // elements per iteration
 #pragma unroll 1
@@ -331,6 +351,7 @@ struct Query {
                 }
             }
         }
+#endif
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             const bool in = (lane + k * kWave) < DV;

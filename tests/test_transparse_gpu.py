@@ -166,7 +166,7 @@ def test_trainer_step_matches_oracle_loss():
     ns = O.tf_call_transparse(t[0], t[1], t[2], mask, pos, neg, 0, 12.0)
     ps = O.tf_call_transparse(t[0], t[1], t[2], mask, pos, neg, 3, 12.0)
     ref = (-(wd * ps).sum() / wd.sum() - (wd * ns).sum() / wd.sum()) / 2
-    assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+    assert abs(float(loss) - float(ref.detach())) <= 1e-5 * max(1.0, abs(float(ref.detach())))
     ref.backward()
     # one Keras Adam step from zero moments: every touched coordinate moves by ~lr * sign(g)
     for p0, prm, g in zip((ent, rel, W), (m.entity_embedding, m.relation_embedding, m.W), (t[0].grad, t[1].grad,

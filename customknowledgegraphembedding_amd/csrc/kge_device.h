@@ -530,7 +530,12 @@ __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Q& q,
                     acc += __builtin_amdgcn_sqrtf(xr * xr + xi * xi);  // hardware sqrt, as the packed form
                 } else if constexpr (FN == KGE_PROTATE) {
                     const float pc = x / p.phase_div;
-                    acc += fabsf(sinf(CH ? (pc + q.q0[k].a[i]) : (q.q0[k].a[i] - pc)));
+                    const float z = CH ? (pc + q.q0[k].a[i]) : (q.q0[k].a[i] - pc);
+#if KGE_ROT_HW
+                    acc += fabsf(__sinf(z));  // |z| <= ~3 pi: the hardware v_sin_f32 (see Query::build's RotatE)
+#else
+                    acc += fabsf(sinf(z));
+#endif
                 }
             }
     }

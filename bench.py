@@ -273,6 +273,42 @@ def run_step(m, pos, neg, mode, fn, ev=None):
     return out
 
 
+class StepRunner:
+    """The headline step loop: step i scores batch i % len(batches) in mode i % 2. With a planner
+    (ops.StepPlanner, the default where the tile form applies; KGE_BENCH_UNPLANNED=1 turns it off) step i is
+    kge_step_forward_planned on the plan step i - 1 made in its launch's tail, and it makes step i + 1's plan
+    the same way: one plan per step, inside the step. Without one, step i is kge_step_forward (its setup in
+    the scoring launch)."""
+
+    def __init__(self, m, batches, fn, planned=True):
+        self.m, self.batches, self.fn = m, batches, fn
+        ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
+        B, N = batches[0][1].shape
+        mod = float(m.modulus.detach().reshape(-1)[0]) if m.model_name == "pRotatE" else 0.0
+        self.planner = None
+        if planned and ops.StepPlanner.available(fn, ent, rel, m._rel_off, m._D, B, N):
+            self.planner = ops.StepPlanner(fn, ent, rel, m._rel_off, m._D, B, N, m._gamma_f, m._range_f,
+                                           modulus=mod)
+        self.next_i = None  # the step the pending plan is for
+
+    def batch(self, i):
+        return self.batches[i % len(self.batches)]
+
+    def __call__(self, i, mode=None):
+        """Step i (mode: i % 2 unless forced; a forced-mode run plans the next step in the same mode)."""
+        md = i % 2 if mode is None else mode
+        pos, neg = self.batch(i)
+        if self.planner is None:
+            return run_step(self.m, pos, neg, md, self.fn)
+        if self.next_i != (i, md):
+            self.planner.plan(pos, neg, md)  # the chain starts here (a run's first step, or a new chain)
+        npos, nneg = self.batch(i + 1)
+        nmd = (i + 1) % 2 if mode is None else mode
+        out = self.planner.step(nxt=(npos, nneg, nmd))
+        self.next_i = (i + 1, nmd)
+        return out
+
+
 def _global_batches(w, world, n, device):
     """n global batches of world x B rows (identical on every rank: the replicas' batches replicated
     by seed): YAGO3-10 positives (RandomState(0) permutation), RandomState negatives."""
@@ -307,7 +343,7 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
     elif w.get("scheme") == "gather":
         def step(b, i):
             return sk.step_forward_gather(b[0], b[1], i % 2)
-    elif sk.world > 1 and dist_on and os.environ.get("KGE_SHARD_NATIVE", "1") != "0":
+    elif sk.world > 1 and dist_on and os.environ.get("KGE_SHARD_NATIVE", "0") == "1":
         # the native executor (one C call per rank-step, RCCL issued from C++ through its own communicator):
         # each step also plans the next batch, on the executor's plan stream, overlapping this step
         from customknowledgegraphembedding_amd.distributed import NativeComm
@@ -323,7 +359,8 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
         # split sizes copied to the host asynchronously) is issued before step i's work, so the host
         # never waits for it; it is device work inside the timed region like the rest of the step, on a
         # side stream (KGE_PLAN_STREAM=main: the step's own stream) where it overlaps step i's scoring
-        # (the Python host path: KGE_SHARD_NATIVE=0)
+        # (the Python host path, the default of this standalone workload; KGE_SHARD_NATIVE=1: the native
+        # executor, which the headline's N > 1 section runs after checking it, rowshard_multi)
         plans = {}
         side = torch.cuda.Stream(device) if os.environ.get("KGE_PLAN_STREAM", "side") == "side" else None
 
@@ -348,6 +385,155 @@ def sharded_bench(w, a, world, rank, device, dist_on, train=False):
     if dist_on:
         tdist.barrier()
     return time.perf_counter() - t0
+
+
+# The native executor's two forms measured at N > 1: the collectives on the step's own stream with
+# one chunk (the default: no cross-stream event hops, profiles/r04_native_timeline.txt), and on a communication
+# stream with two chunks (half of each exchange under the other chunk's scoring)
+ROWSHARD_VARIANTS = (("one_stream_1chunk", dict(one_stream=True, chunks=1)),
+                     ("two_stream_2chunk", dict(one_stream=False, chunks=2)))
+ROWSHARD_DEFAULT = "one_stream_1chunk"
+ROWSHARD_RANK_KEYS = ("rank", "step_us", "kernel_busy_us", "query_a2a_us", "score_a2a_us", "host_wait_us",
+                      "host_call_us")
+
+
+def _gather_objects(obj, world):
+    import torch.distributed as tdist
+    out = [None] * world
+    tdist.all_gather_object(out, obj)
+    return out
+
+
+def _max_over_ranks(x, device):
+    import torch.distributed as tdist
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def rowshard_report(w, world, steps, variants, per_rank, n_ranks_seen, native_status, matches):
+    """The N > 1 row-sharded record (yago3_10_rowshard): the per-variant max-over-ranks step times, the selected
+    form's throughput, every rank's diagnosis (device spans of one step from the executor's timing events, the
+    host time per call and its wait for plans), what the communicator saw, and whether the native step's
+    outputs equal the torch.distributed path's on the same batch (its first cross-process run checks itself)."""
+    trip = (w["B"] * w["N"] + w["B"]) * world
+    var = {k: {"ms_per_step": v * 1e3, "triples_per_s": trip / v} for k, v in variants.items()}
+    sel = ROWSHARD_DEFAULT if (ROWSHARD_DEFAULT in var and native_status == "ok" and matches) else "torchcomm_python"
+    return {"workload": w["name"], "n_gpus": world, "global_batch": w["B"] * world, "n_neg": w["N"], "steps": steps,
+            "selected": sel, "triples_per_s": var[sel]["triples_per_s"], "ms_per_step": var[sel]["ms_per_step"],
+            "variants": var, "per_rank": per_rank, "n_ranks_seen": n_ranks_seen, "native_status": native_status,
+            "native_matches_torchcomm": matches,
+            "what": "distributed.ShardedKGE.step_forward: entity table row-sharded over the ranks, owner-computes "
+                    "scoring, one RCCL all-to-all of the owners' compacted query rows and one of the owned scores; "
+                    "variants: the native executor (one C call per rank-step, ncclAllToAllv from C++) with the "
+                    "collectives on the step's stream (1 chunk) or on a communication stream (2 chunks), and the "
+                    "Python path over torch.distributed; selected: the native default when its communicator "
+                    "checked out and its outputs equal the Python path's bitwise, else the Python path"}
+
+
+def rowshard_multi(w, a, world, rank, device):
+    """N > 1: the row-sharded forward step through (1) the Python path over torch.distributed (RCCL via torch)
+    and (2) the native executor in both ROWSHARD_VARIANTS, after a known-answer check of the native communicator
+    (ncclCommCount, one all-to-all of rank-tagged values) agreed on by every rank; then one diagnosis pass with
+    the executor's timing events. A native failure is recorded (native_status) and the Python path stands."""
+    import torch.distributed as tdist
+    from customknowledgegraphembedding_amd.distributed import NativeComm, ShardedKGE, TorchComm
+    sk = ShardedKGE(w["fn"], w["nentity"], w["nrelation"], w["hidden_dim"], w["gamma"], device=device, seed=0,
+                    comm=TorchComm())
+    sk.exchange = True  # the exchange path at every world size (at world 1 its pieces are a rank's own)
+    batches = _global_batches(w, world, 4, device)
+    lib = kge.load()
+    variants = {}
+
+    def timed(step, n_warm, n):
+        for i in range(n_warm):
+            step(i)
+        torch.cuda.synchronize()
+        tdist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n_warm, n_warm + n):
+            step(i)
+        torch.cuda.synchronize()
+        tdist.barrier()
+        return _max_over_ranks(time.perf_counter() - t0, device)
+
+    # (1) the Python path: plans made a step ahead on a side stream
+    plans, side = {}, torch.cuda.Stream(device)
+
+    def py_step(i):
+        b, nb = batches[i % 4], batches[(i + 1) % 4]
+        plan = plans.pop(i, None) or sk.plan(b[0], b[1], i % 2)
+        plans[i + 1] = sk.plan(nb[0], nb[1], (i + 1) % 2, stream=side)
+        return sk.step_forward(b[0], b[1], i % 2, plan=plan)
+    ref = [t.clone() for t in sk.step_forward(batches[0][0], batches[0][1], 0)]
+    variants["torchcomm_python"] = timed(py_step, a.warmup, a.steps) / a.steps
+    # (2) the native communicator, checked before any executor uses it
+    status, comm, seen = "ok", None, None
+    try:
+        comm = NativeComm(device=device)
+        seen = int(lib.kge_comm_size(comm.handle))
+        send = torch.tensor([rank * 1000.0 + o for o in range(world)], device=device)
+        recv = torch.empty(world, device=device)
+        comm.all_to_all(recv, send, [1] * world, [1] * world)
+        torch.cuda.synchronize()
+        want = torch.tensor([o * 1000.0 + rank for o in range(world)], device=device)
+        if seen != world or not torch.equal(recv, want):
+            status = f"known-answer check failed: ncclCommCount {seen}, all-to-all {recv.tolist()}"
+    except Exception as e:  # noqa: BLE001
+        status = "native communicator: " + repr(e)
+    bad = torch.tensor([0 if status == "ok" else 1], device=device)
+    tdist.all_reduce(bad, op=tdist.ReduceOp.MAX)  # every rank takes the native path, or none does
+    if status == "ok" and int(bad.item()):
+        status = "another rank's native communicator check failed"
+    matches = None
+    per_rank = {"rank": rank}
+    if status == "ok":
+        for name, cfg in ROWSHARD_VARIANTS:
+            sk.use_native(comm, one_stream=cfg["one_stream"])
+            ch = cfg["chunks"]
+            got = [t.clone() for t in sk.step_forward(batches[0][0], batches[0][1], 0, chunks=ch)]
+            same = all(bool(((x == y) | (torch.isnan(x) & torch.isnan(y))).all()) for x, y in zip(got, ref))
+            matches = same if matches is None else (matches and same)
+            sk.plan_native(batches[1][0], batches[1][1], 1, chunks=ch)
+            sk.plan_native(batches[2][0], batches[2][1], 0, chunks=ch)
+
+            def nat_step(i, ch=ch):
+                b, nb = batches[(i + 1) % 4], batches[(i + 3) % 4]
+                return sk.step_forward(b[0], b[1], (i + 1) % 2, chunks=ch, nxt=(nb[0], nb[1], (i + 3) % 2))
+            variants[name] = timed(nat_step, a.warmup, a.steps) / a.steps
+        # diagnosis: the default form with timing events, a few steps; device spans of each, host time per call
+        cfg = dict(ROWSHARD_VARIANTS)[ROWSHARD_DEFAULT]
+        sk.use_native(comm, one_stream=cfg["one_stream"], timing=True)
+        ch = cfg["chunks"]
+        sk.plan_native(batches[0][0], batches[0][1], 0, chunks=ch)
+        sk.plan_native(batches[1][0], batches[1][1], 1, chunks=ch)
+        spans, calls, waits = [], [], []
+        ex = None
+        for i in range(8):
+            b, nb = batches[i % 4], batches[(i + 2) % 4]
+            t0 = time.perf_counter()
+            sk.step_forward(b[0], b[1], i % 2, chunks=ch, nxt=(nb[0], nb[1], i % 2))
+            calls.append((time.perf_counter() - t0) * 1e6)
+            ex = ex or next(iter(sk._native.values()))
+            waits.append(ex.host_wait_us())
+            spans.append(ex.timings())
+        torch.cuda.synchronize()
+        tdist.barrier()
+        sp = spans[2:]  # after the first steps' ramp
+        per_rank.update({
+            "step_us": statistics.median(x["step_us"] for x in sp),
+            "kernel_busy_us": statistics.median(x["gather_us"] + x["finish_us"] + sum(x["score_us"]) for x in sp),
+            "query_a2a_us": statistics.median(sum(x["query_a2a_us"]) for x in sp),
+            "score_a2a_us": statistics.median(sum(x["score_a2a_us"]) for x in sp),
+            "host_wait_us": statistics.median(waits[2:]), "host_call_us": statistics.median(calls[2:]),
+            "spans_of_one_step": sp[-1]})
+        sk.use_native(None, probe=True)  # closes the executors
+        comm.close()
+    else:
+        per_rank.update({k: None for k in ROWSHARD_RANK_KEYS if k != "rank"})
+    per = _gather_objects(per_rank, world)
+    return rowshard_report(w, world, a.steps, variants, per, seen, status, matches)
 
 
 def rank0_step_parts(ranks, pos, neg, mode, chunks=None):
@@ -989,12 +1175,19 @@ def dry_run(a, world, rank):
         ranks_seen = int(seen.item())
     else:
         ranks_seen = 0
+    line = {"metric": METRIC, "value": 0.0, "unit": "triples/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": el / max(1, a.steps) * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "dry run (no kernels)",
+            "config": {"workload": "dry-run", "parallelism": f"replicas{world}"},
+            "dry_run": True, "rank_sum": ranks_seen}
+    if world > 1:
+        # the N > 1 row-sharded record's shape (rowshard_report), every rank's entry gathered as on the GPU
+        per = _gather_objects({k: (rank if k == "rank" else 0.0) for k in ROWSHARD_RANK_KEYS}, world)
+        line["yago3_10_rowshard"] = rowshard_report(
+            WORKLOADS["c4s"], world, a.steps, {k: max(el, 1e-9) for k in ["torchcomm_python"] +
+                                               [n for n, _ in ROWSHARD_VARIANTS]}, per, world, "ok", True)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "triples/s", "n_gpus": world, "steps": a.steps,
-                          "warmup": a.warmup, "ms_per_step": el / max(1, a.steps) * 1e3, "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "dry run (no kernels)",
-                          "config": {"workload": "dry-run", "parallelism": f"replicas{world}"},
-                          "dry_run": True, "rank_sum": ranks_seen}), flush=True)
+        print(json.dumps(line), flush=True)
     if world > 1:
         tdist.destroy_process_group()
 
@@ -1031,30 +1224,29 @@ def sharded_watchdog(line, rank, timeout_s):
     return t
 
 
+def sharded_single(line, ws, sa, device):
+    """c4s at one GPU: the unsharded fused forward through ShardedKGE (no exchange at one rank)."""
+    el = sharded_bench(ws, sa, 1, 0, device, False)
+    line["yago3_10_rowshard"] = {
+        "workload": ws["name"], "n_gpus": 1, "global_batch": ws["B"], "n_neg": ws["N"],
+        "triples_per_s": (ws["B"] * ws["N"] + ws["B"]) * sa.steps / el,
+        "ms_per_step": el / sa.steps * 1e3, "steps": sa.steps,
+        "what": "distributed.ShardedKGE.step_forward at 1 rank: the unsharded fused forward (no exchange)"}
+
+
 def sharded_lines(line, a, world, rank, device, dist):
-    """c4s beside the headline: ShardedKGE.step_forward and .train_step at this world size, and at one GPU
-    the simulated 8-rank step (shard_sim_bench)."""
-    if dist:
-        import torch.distributed as tdist
+    """c4s beside the headline: ShardedKGE.step_forward (at N > 1 the self-checking, per-rank diagnosed
+    rowshard_multi) and .train_step at this world size, and at one GPU the simulated 8-rank step
+    (shard_sim_bench)."""
     ws = WORKLOADS["c4s"]
     sa = argparse.Namespace(**{**vars(a), "steps": a.sharded_steps, "warmup": 3})
-    el = sharded_bench(ws, sa, world, rank, device, dist)  # symmetric on every rank
     if dist:
-        t = torch.tensor([el], device=device, dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        el = float(t.item())
-    line["yago3_10_rowshard"] = {
-        "workload": ws["name"], "n_gpus": world, "global_batch": ws["B"] * world, "n_neg": ws["N"],
-        "triples_per_s": (ws["B"] * ws["N"] + ws["B"]) * world * sa.steps / el,
-        "ms_per_step": el / sa.steps * 1e3, "steps": sa.steps,
-        "what": "distributed.ShardedKGE.step_forward: entity table row-sharded over the ranks, owner-computes "
-                "scoring; per chunk one RCCL all-to-all of the owners' compacted query rows and one of the "
-                "owned scores (exchange plan made a step ahead); at 1 rank the unsharded fused forward"}
+        line["yago3_10_rowshard"] = rowshard_multi(ws, sa, world, rank, device)
+    else:
+        sharded_single(line, ws, sa, device)
     el = sharded_bench(ws, sa, world, rank, device, dist, train=True)
     if dist:
-        t = torch.tensor([el], device=device, dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        el = float(t.item())
+        el = _max_over_ranks(el, device)
     line["yago3_10_rowshard_train"] = {
         "workload": ws["name"] + ", train step", "n_gpus": world, "global_batch": ws["B"] * world,
         "n_neg": ws["N"], "triples_per_s": (ws["B"] * ws["N"] + ws["B"]) * world * sa.steps / el,
@@ -1153,9 +1345,9 @@ def main(argv=None):
         if dist:
             tdist.barrier()
 
+    runner = StepRunner(m, batches, fn, planned=os.environ.get("KGE_BENCH_UNPLANNED", "0") != "1")
     for i in range(a.warmup):
-        pos, neg = batches[i % len(batches)]
-        run_step(m, pos, neg, i % 2, fn)
+        runner(i)
     torch.cuda.synchronize()
 
     # kernel timing: event pairs bracket groups of `ev_group` consecutive launches (every other
@@ -1167,32 +1359,44 @@ def main(argv=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        pos, neg = batches[i % len(batches)]
         g, r = divmod(i, ev_group)
         if g % 2 == 0 and r == 0 and i + ev_group <= a.steps:
             evs[g] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             evs[g][0].record()
-        run_step(m, pos, neg, i % 2, fn)
+        runner(a.warmup + i)  # continues the warmup's plan chain: one plan per timed step, made inside it
         if g in evs and r == ev_group - 1:
             evs[g][1].record()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [evs[g][0].elapsed_time(evs[g][1]) / ev_group for g in sorted(evs)]
-    # SURVEY §8d per-mode kernel times, after the timed region, timed like kern_ms: a group of ev_group
-    # same-mode steps is queued first (untimed, it keeps the device busy), then one event pair brackets the
-    # next ev_group, so the first launch's host latency does not land inside the pair
+    # SURVEY §8d per-mode STEP times (both launches of a step and the gap between them, device time), after the
+    # timed region, timed like kern_ms: a group of ev_group same-mode steps is queued first (untimed, it keeps
+    # the device busy), then one event pair brackets the next ev_group, so the first launch's host latency does
+    # not land inside the pair
     per_mode = {}
     for mode in (0, 1):
         e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         for i in range(2 * ev_group):
             if i == ev_group:
                 e[0].record()
-            pos, neg = batches[i % len(batches)]
-            run_step(m, pos, neg, mode, fn)
+            runner(i, mode)
         e[1].record()
         torch.cuda.synchronize()
         per_mode[mode] = e[0].elapsed_time(e[1]) / ev_group
+    # the same step without the plan made ahead (kge_step_forward: the tile kernel's setup in the scoring
+    # launch), device time per step over the same alternating batches: what the plan saves
+    unplanned_us = None
+    if runner.planner is not None:
+        plain = StepRunner(m, batches, fn, planned=False)
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        for i in range(4 * ev_group):
+            if i == 2 * ev_group:
+                e[0].record()
+            plain(i)
+        e[1].record()
+        torch.cuda.synchronize()
+        unplanned_us = e[0].elapsed_time(e[1]) / (2 * ev_group) * 1e3
     head_ms, tail_ms = [per_mode[0]], [per_mode[1]]
     if not kern_ms:  # fewer steps than one event group
         kern_ms = head_ms + tail_ms
@@ -1239,8 +1443,13 @@ def main(argv=None):
                        "gathered in XCD-sliced ascending-id order, then the row reductions)",
                     2: "step_fwd_tile_kernel + neg_rows_kernel (the step's two launches: negatives and positives "
                        "in row-group x XCD-slice tiles, queries in LDS, each block's candidates swept in entity "
-                       "order; then the row reductions)"}[order],
-            kernel_avg_us_head_batch=head_ms[0] * 1e3, kernel_avg_us_tail_batch=tail_ms[0] * 1e3,
+                       "order, planned a step ahead by the previous launch's tail blocks; then the row "
+                       "reductions)"}[order],
+            step_us_head_batch=head_ms[0] * 1e3, step_us_tail_batch=tail_ms[0] * 1e3,
+            step_plan=("kge_step_forward_planned: each step's id-only setup (row groups, entity-sorted candidate "
+                       "lists) made by the previous step's tail blocks; one plan per timed step"
+                       if runner.planner is not None else "none (kge_step_forward)"),
+            unplanned_step_us=unplanned_us,
             unique_row_bytes_per_step=uniq * ent_dim_ * 4, row_reuse=(B * N + 2 * B) / max(1, uniq)),
         "build": kge.build_id(),
     }

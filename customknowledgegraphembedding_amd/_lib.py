@@ -46,6 +46,15 @@ SIGNATURES = {
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p],
     ),
+    "kge_step_plan_size": (_c_i64, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
+    "kge_step_plan": (
+        _c_i, [_c_i, _c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p,
+               _c_p]),
+    "kge_step_forward_planned": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f,
+         _c_f, _c_i, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p],
+    ),
     "kge_step_finish": (
         _c_i,
         [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64,
@@ -90,6 +99,8 @@ SIGNATURES = {
                _c_p, _c_i64]),
     "kge_shard_exec_destroy": (_c_i, [_c_p]),
     "kge_shard_exec_host_wait_us": (ctypes.c_double, [_c_p, _c_i]),
+    "kge_shard_exec_timings": (_c_i, [_c_p, _c_p, _c_i]),
+    "kge_comm_size": (_c_i, [_c_p]),
     "kge_shard_exec_plan": (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_p]),
     "kge_shard_exec_step": (
         _c_i, [_c_p, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64, _c_i, _c_f, _c_f, _c_f,

@@ -36,6 +36,22 @@ __global__ __launch_bounds__(kBlock) void neg_rows_kernel(ScoreParams p) {
     if (lane == 0) p.out_neg[b] = r;
 }
 
+// ... and, with p.tile_next.plan set, blocks past the rows' make the next batch's step plan (kge_step_forward_planned:
+// the row reductions use few CUs, the plan blocks run beside them)
+__global__ __launch_bounds__(kBlock) void neg_rows_plan_kernel(ScoreParams p) {
+    __shared__ int sm[plan_lds_ints(kBlock)];
+    const int rb = (int)((p.B + kWavesPerBlock - 1) / kWavesPerBlock);
+    if ((int)blockIdx.x >= rb) {
+        tile_plan_group<kWavesPerBlock>(p.tile_next, (int)blockIdx.x - rb, sm);
+        return;
+    }
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= p.B) return;
+    const int lane = threadIdx.x & 63;
+    const float r = row_reduce_fast(p.out + b * p.out_ld, p.N, p.temperature, p.adversarial, lane);
+    if (lane == 0) p.out_neg[b] = r;
+}
+
 // With `ps` set it also writes the positive branch's d_ps[b] = d_out_pos[b] * sigmoid(-ps[b])
 // (logsigmoid backward, model.py:145), saving the separate launch in the train step.
 __global__ __launch_bounds__(kBlock) void neg_reduce_bwd_kernel(const float* __restrict__ s, int64_t B, int64_t N,
@@ -468,8 +484,11 @@ int run_score(int fn, int mode, ScoreParams& p, int kind, void* stream) {
     } else if (kind == KIND_STEP_FWD_TILE || kind == KIND_SCORE_TILE) {
         if (p.tile_rows < 1 || p.tile_lds > kTileLdsMax) return fail(KGE_EINVAL, "tile plan missing");
         // one block of tile_waves waves per (group of tile_rows batch rows, entity slice): run_score's
-        // block count is waves / kWavesPerBlock
-        waves = (p.B + p.tile_rows - 1) / p.tile_rows * 8 * kWavesPerBlock;
+        // block count is waves / kWavesPerBlock; then, for a planned step, one tail block per group of the
+        // next batch's plan
+        const int64_t groups = (p.B + p.tile_rows - 1) / p.tile_rows;
+        p.tile_blocks = (int)(groups * 8);
+        waves = (groups * 8 + (p.tile_next.plan ? plan_groups(p.tile_next.B, p.tile_next.R) : 0)) * kWavesPerBlock;
     } else if (kind == KIND_STEP_FWD_XCD || kind == KIND_SCORE_SHARD_XCD || kind == KIND_SHARD_BUCKET) {
         waves = (p.B + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock * 8;  // 8 slice blocks per 4 rows
         if (kind == KIND_STEP_FWD_XCD && p.xcd_phases > 1) waves *= p.xcd_phases;
@@ -660,6 +679,36 @@ int tile_plan(int fn, ScoreParams& p) {
     return 1;
 }
 
+// The tile parameters of a planned step (kge_step_plan / kge_step_forward_planned): tile_plan's choice for
+// 16-B aligned tables of these shapes, so that a plan is made without the tables. Returns the rows per group
+// (0: the tile form does not apply).
+int planned_tile_params(int fn, int64_t nentity, int64_t ent_ld, int64_t nrelation, int64_t rel_ld, int64_t rel_off,
+                        int64_t B, int64_t N, int64_t D, ScoreParams& p) {
+    if (B <= 0 || N <= 0 || D <= 0 || nentity <= 0 || nentity >= ((int64_t)1 << 31) || B >= ((int64_t)1 << 31))
+        return 0;
+    const float* tab = reinterpret_cast<const float*>((uintptr_t)4096);
+    fill_indexed(p, fn, KGE_TAIL_BATCH, tab, nentity, ent_ld, tab, nrelation, rel_ld, rel_off, nullptr, nullptr, 0, B,
+                 N, D, 0.f, 1.f, 0.f);
+    return tile_plan(fn, p) ? p.tile_rows : 0;
+}
+
+PlanArgs plan_args(const ScoreParams& tp, int mode, int64_t nentity, int64_t nrelation, const int64_t* pos,
+                   const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, void* plan) {
+    PlanArgs a;
+    a.pos = pos;
+    a.neg = neg;
+    a.neg_ld = neg_ld;
+    a.B = B;
+    a.N = N;
+    a.nent = nentity;
+    a.nrel = nrelation;
+    a.mode = mode;
+    a.R = tp.tile_rows;
+    a.sort = tp.tile_sort != 0;
+    a.plan = reinterpret_cast<int*>(plan);
+    return a;
+}
+
 }  // namespace
 
 int set_error(int code, const char* msg) { return fail(code, msg); }
@@ -772,6 +821,97 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
     }
     // one launch: negatives + the per-row finish (positive, reduction)
     return run_score(fn, mode, p, (cand_stats && fn == KGE_INTERHT) ? KIND_STEP_FWD_STATS : KIND_STEP_FWD, stream);
+}
+
+int64_t kge_step_plan_size(int fn, int64_t nentity, int64_t ent_ld, int64_t nrelation, int64_t rel_ld,
+                           int64_t rel_off, int64_t B, int64_t N, int64_t D) {
+    if (fn < KGE_TRANSE || fn > KGE_PROTATE) return 0;
+    ScoreParams tp;
+    const int R = planned_tile_params(fn, nentity, ent_ld, nrelation, rel_ld, rel_off, B, N, D, tp);
+    return R ? plan_words(B, N, R) * 4 : 0;
+}
+
+int kge_step_plan(int fn, int mode, int64_t nentity, int64_t ent_ld, int64_t nrelation, int64_t rel_ld,
+                  int64_t rel_off, const int64_t* pos, const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N,
+                  int64_t D, void* plan, void* stream) {
+    if (fn < KGE_TRANSE || fn > KGE_PROTATE) return fail(KGE_EINVAL, "unknown score function id " + std::to_string(fn));
+    if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH)
+        return fail(KGE_EINVAL, "kge_step_plan needs a negative mode (0 or 1)");
+    if (B <= 0 || N <= 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (!pos || !neg || !plan) return fail(KGE_EINVAL, "null pointer");
+    if (!aligned(plan, 16)) return fail(KGE_EINVAL, "the plan must be 16-B aligned");
+    ScoreParams tp;
+    if (!planned_tile_params(fn, nentity, ent_ld, nrelation, rel_ld, rel_off, B, N, D, tp))
+        return fail(KGE_ENOTSUP, "the tile form does not apply to this shape (kge_step_plan_size is 0)");
+    const PlanArgs a = plan_args(tp, mode, nentity, nrelation, pos, neg, neg_ld, B, N, plan);
+    const unsigned groups = (unsigned)plan_groups(B, tp.tile_rows);
+    if (tp.tile_waves == 16)
+        hipLaunchKernelGGL(tile_plan_kernel<16>, dim3(groups), dim3(16 * kWave), plan_lds_ints(16 * kWave) * 4,
+                           (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(tile_plan_kernel<12>, dim3(groups), dim3(12 * kWave), plan_lds_ints(12 * kWave) * 4,
+                           (hipStream_t)stream, a);
+    return check_launch("kge_step_plan");
+}
+
+int kge_step_forward_planned(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                             int64_t nrelation, int64_t rel_ld, int64_t rel_off, int64_t B, int64_t N, int64_t D,
+                             float gamma, float emb_range, float modulus, float temperature, int adversarial,
+                             const void* plan, const int64_t* next_pos, const int64_t* next_neg, int64_t next_neg_ld,
+                             int next_mode, void* next_plan, float* neg_scores, int64_t ns_ld, float* out_neg,
+                             float* pos_scores, float* out_pos, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_forward_planned needs a negative mode (0 or 1)");
+    if (B <= 0 || N <= 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
+    if (!ent || !rel || !plan || !neg_scores || !out_neg || !out_pos) return fail(KGE_EINVAL, "null pointer");
+    if (next_plan) {
+        if (next_mode != KGE_HEAD_BATCH && next_mode != KGE_TAIL_BATCH)
+            return fail(KGE_EINVAL, "the next batch needs a negative mode (0 or 1)");
+        if (!next_pos || !next_neg) return fail(KGE_EINVAL, "next_plan needs next_pos and next_neg");
+        if (next_plan == plan) return fail(KGE_EINVAL, "next_plan must not be the plan this step reads");
+        if (!aligned(next_plan, 16)) return fail(KGE_EINVAL, "the plan must be 16-B aligned");
+    }
+    if (!aligned(plan, 16)) return fail(KGE_EINVAL, "the plan must be 16-B aligned");
+    ScoreParams tp;
+    const int R = planned_tile_params(fn, nentity, ent_ld, nrelation, rel_ld, rel_off, B, N, D, tp);
+    ScoreParams p;
+    fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, nullptr, nullptr, 0, B, N, D,
+                 gamma, emb_range, modulus);
+    if (!R || !tile_plan(fn, p) || p.tile_rows != R)
+        return fail(KGE_ENOTSUP, "the tile form does not apply to these tables (unaligned rows, or "
+                                 "kge_step_plan_size is 0): use kge_step_forward");
+    p.out = neg_scores;
+    p.out_ld = ns_ld;
+    p.pos_base = nullptr;
+    p.temperature = temperature;
+    p.adversarial = adversarial;
+    p.out_neg = out_neg;
+    p.out_pos_raw = pos_scores;
+    p.out_pos_ls = out_pos;
+    p.tile_pos = 1;
+    p.tile_plan = reinterpret_cast<const int*>(plan);
+    // where the next batch's plan is made: the tile launch's tail blocks, or beside the row reductions
+    const char* at = getenv("KGE_PLAN_AT");  // A/B of the placement (temporary)
+    const bool at_rows = at && strcmp(at, "rows") == 0;
+    PlanArgs nx{};
+    if (next_plan)
+        nx = plan_args(tp, next_mode, nentity, nrelation, next_pos, next_neg, next_neg_ld, B, N, next_plan);
+    if (next_plan && !at_rows) {
+        p.tile_next = nx;
+        p.tile_lds = std::max(p.tile_lds, plan_lds_ints(p.tile_waves * kWave) * 4);
+    }
+    rc = run_score(fn, mode, p, KIND_STEP_FWD_TILE, stream);
+    if (rc) return rc;
+    const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (next_plan && at_rows) {
+        p.tile_next = nx;
+        hipLaunchKernelGGL(neg_rows_plan_kernel, dim3((unsigned)(blocks + plan_groups(B, tp.tile_rows))), dim3(kBlock),
+                           0, (hipStream_t)stream, p);
+    } else {
+        hipLaunchKernelGGL(neg_rows_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, p);
+    }
+    return check_launch("kge_step_forward_planned row reductions");
 }
 
 int kge_score_sharded(int fn, int mode, const float* qent, int64_t q_ld, const float* rel, int64_t nrelation,

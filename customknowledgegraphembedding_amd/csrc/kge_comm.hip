@@ -76,6 +76,7 @@ struct Rccl {
     ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                hipStream_t) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
+    ncclResult_t (*count)(const ncclComm_t, int*) = nullptr;
     bool ok = false;
 };
 
@@ -93,6 +94,7 @@ const Rccl& rccl() {
         x.all_to_allv = reinterpret_cast<decltype(x.all_to_allv)>(sym("ncclAllToAllv"));
         x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(sym("ncclAllReduce"));
         x.error_string = reinterpret_cast<decltype(x.error_string)>(sym("ncclGetErrorString"));
+        x.count = reinterpret_cast<decltype(x.count)>(sym("ncclCommCount"));
         x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_to_allv && x.all_reduce && x.error_string;
         return x;
     }();
@@ -209,6 +211,12 @@ struct kge_shard_exec {
                ev_x = nullptr;
     std::vector<size_t> sc, sd, rc, rd;  // ncclAllToAllv counts / displacements (elements)
     double wait_us = 0;                  // host time spent waiting for plans' summaries (kge_shard_exec_host_wait_us)
+    // KGE_EXEC_TIMING: timing events of the last step (kge_shard_exec_timings): t[0] its start, t[1] after the
+    // query gather, per chunk k the query exchange (t[2 + 6k], t[3 + 6k]), the scoring (t[4 + 6k], t[5 + 6k]) and
+    // the score exchange (t[6 + 6k], t[7 + 6k]), then the finish (t[2 + 6K], t[3 + 6K])
+    static constexpr int kTimingEvents = 4 + 6 * kMaxChunks;
+    hipEvent_t t[kTimingEvents] = {};
+    bool timed = false;  // the last step recorded them
 
     int* slot_i(int s, size_t off) { return reinterpret_cast<int*>(ws + s * L.slot + off); }
 };
@@ -463,6 +471,8 @@ int kge_shard_exec_create(kge_shard_exec** out, kge_comm* comm, int flags, int f
         ev(&s.ready);
         ev(&s.freed);
     }
+    if (flags & KGE_EXEC_TIMING)
+        for (int i = 0; i < kge_shard_exec::kTimingEvents && e == hipSuccess; ++i) e = hipEventCreate(&x->t[i]);
     if (e == hipSuccess) {
         // the slots start free: their `freed` events complete at once
         for (int i = 0; i < kSlots && e == hipSuccess; ++i) e = hipEventRecord(x->slot[i].freed, x->plan_st);
@@ -493,9 +503,43 @@ int kge_shard_exec_destroy(kge_shard_exec* x) {
         drop(s.ready);
         drop(s.freed);
     }
+    for (auto& t : x->t) drop(t);
     if (x->comm_st) (void)hipStreamDestroy(x->comm_st);
     if (x->plan_st) (void)hipStreamDestroy(x->plan_st);
     delete x;
+    return set_error(0, "");
+}
+
+int kge_comm_size(kge_comm* comm) {
+    if (!comm) return set_error(KGE_EINVAL, "kge_comm_size: null pointer");
+    if (comm->loop || !comm->nccl) return comm->world;
+    if (!rccl().count) return set_error(KGE_ENOTSUP, "kge_comm_size: ncclCommCount not found");
+    int n = 0;
+    const ncclResult_t r = rccl().count(comm->nccl, &n);
+    if (r != ncclSuccess) return nccl_fail("ncclCommCount", r);
+    return n;
+}
+
+int kge_shard_exec_timings(kge_shard_exec* x, float* out, int n) {
+    if (!x || !out) return set_error(KGE_EINVAL, "kge_shard_exec_timings: null pointer");
+    if (!(x->flags & KGE_EXEC_TIMING)) return set_error(KGE_EINVAL, "kge_shard_exec_timings: made without KGE_EXEC_TIMING");
+    if (!x->timed) return set_error(KGE_EINVAL, "kge_shard_exec_timings: no timed step yet");
+    const int K = x->chunks;
+    if (n < 3 + 3 * K) return set_error(KGE_EINVAL, "kge_shard_exec_timings: out needs 3 + 3 chunks floats");
+    const int fin = 2 + 6 * K;
+    KGE_HIP_TRY("kge_shard_exec_timings", hipEventSynchronize(x->t[fin + 1]));
+    auto span = [&](int a, int b) {
+        float ms = 0.f;
+        return hipEventElapsedTime(&ms, x->t[a], x->t[b]) == hipSuccess ? ms * 1e3f : -1.f;
+    };
+    out[0] = span(0, fin + 1);  // the step, first kernel to last
+    out[1] = span(0, 1);        // the query gather
+    out[2] = span(fin, fin + 1);  // the finish
+    for (int k = 0; k < K; ++k) {
+        out[3 + 3 * k] = span(2 + 6 * k, 3 + 6 * k);  // query all-to-all
+        out[4 + 3 * k] = span(4 + 6 * k, 5 + 6 * k);  // owner-computes scoring
+        out[5 + 3 * k] = span(6 + 6 * k, 7 + 6 * k);  // score all-to-all
+    }
     return set_error(0, "");
 }
 
@@ -573,9 +617,14 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
         hipError_t e = hipEventRecord(ev, from);
         return e == hipSuccess ? hipStreamWaitEvent(to, ev, 0) : e;
     };
+    const bool tm = (x->flags & KGE_EXEC_TIMING) != 0;
+    auto mark = [&](int i, hipStream_t on) -> hipError_t { return tm ? hipEventRecord(x->t[i], on) : hipSuccess; };
+    x->timed = false;
+    KGE_HIP_TRY("kge_shard_exec_step", mark(0, st));
     int rc = kge_shard_gather_queries(shard, x->shard_rows, shard_ld, shard_lo, pos, x->Bg, K, -1, d, W, me, mode, 0,
                                       x->slot_i(s, x->L.qown), x->slot_i(s, x->L.qslot), summ, q_send, qidx, st);
     if (rc) return rc;
+    KGE_HIP_TRY("kge_shard_exec_step", mark(1, st));
     KGE_HIP_TRY("kge_shard_exec_step", hop(x->ev_gather, st, cs));
     // 1. every chunk's query exchange: this rank's rows of the chunk (the same piece to every rank)
     size_t at = 0, qb = 0;
@@ -592,8 +641,10 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
         }
         qb_at[k] = qb;
         q_rows[k] = r / (size_t)d;
+        KGE_HIP_TRY("kge_shard_exec_step", mark(2 + 6 * k, cs));
         rc = exchange(x, q_send, q_block + qb, cs, "kge_shard_exec_step query all-to-all");
         if (rc) return rc;
+        KGE_HIP_TRY("kge_shard_exec_step", mark(3 + 6 * k, cs));
         if (!one) KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(x->ev_q[k], cs));
         at += (size_t)W * mine * d;
         qb += r;
@@ -616,6 +667,7 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
             nrecv += x->rc[o];
         }
         if (!one) KGE_HIP_TRY("kge_shard_exec_step", hipStreamWaitEvent(st, x->ev_q[k], 0));
+        KGE_HIP_TRY("kge_shard_exec_step", mark(4 + 6 * k, st));
         if (nsend) {
             rc = kge_shard_score(x->fn, mode, q_block + qb_at[k], (int64_t)q_rows[k], d, qidx + row0, rel, nrelation, rel_ld,
                                  rel_off, shard, x->shard_rows, shard_ld, shard_lo, pos + row0 * 3, Rk, x->N, x->D,
@@ -624,16 +676,22 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
                                  homeB, row0 / homeB, s_send + sb, st);
             if (rc) return rc;
         }
+        KGE_HIP_TRY("kge_shard_exec_step", mark(5 + 6 * k, st));
         KGE_HIP_TRY("kge_shard_exec_step", hop(x->ev_s[k], st, cs));
+        KGE_HIP_TRY("kge_shard_exec_step", mark(6 + 6 * k, cs));
         rc = exchange(x, s_send + sb, s_recv, cs, "kge_shard_exec_step score all-to-all");
         if (rc) return rc;
+        KGE_HIP_TRY("kge_shard_exec_step", mark(7 + 6 * k, cs));
         sb += nsend;
     }
     KGE_HIP_TRY("kge_shard_exec_step", hop(x->ev_x, cs, st));
     // 4. the home rows: scatter, positives, reductions
+    KGE_HIP_TRY("kge_shard_exec_step", mark(2 + 6 * K, st));
     rc = kge_shard_finish(s_recv, summ, hpre, pos, neg, neg_ld, x->Bg, x->N, x->nentity, W, me, mode, temperature,
                           adversarial, scores, ns_ld, out_neg, pos_scores, out_pos, st);
     if (rc) return rc;
+    KGE_HIP_TRY("kge_shard_exec_step", mark(3 + 6 * K, st));
+    x->timed = tm;
     KGE_HIP_TRY("kge_shard_exec_step", hipEventRecord(sl->freed, st));
     sl->planned = false;
     x->cur = (s + 1) % kSlots;

@@ -254,12 +254,15 @@ constexpr bool rel_split(int fn) { return fn == KGE_COMPLEX; }
 //   q0,q1,q2: per-element query operands kept in VGPRs; zero on groups past D.
 //   na_inv,nb_inv: InterHT query reciprocal norms (1/||a||, 1/||b||; no epsilon, Q7)
 // ---------------------------------------------------------------------------------------------
-#ifndef KGE_ROT_CHUNK
-#define KGE_ROT_CHUNK 4  // RotatE query build: cos / sin of this many elements per iteration of a rolled loop
-#endif
-#ifndef KGE_ROT_HW
-#define KGE_ROT_HW 1  // RotatE query build on the hardware sin / cos (0: libm, rolled KGE_ROT_CHUNK at a time)
-#endif
+// The hardware v_sin_f32 / v_cos_f32 take their argument in revolutions and are defined for |x| <= 256 of
+// them. hw_sin / hw_cos scale a phase in radians to revolutions and keep only its fraction (v_fract_f32) before
+// the instruction: one more VALU op, and a phase of any size (trained embeddings are unconstrained) stays in the
+// instruction's range. The scaled phase carries the fp32 rounding of x / 2 pi: at |x| = 500 rad (80 revolutions)
+// that is <= 2.4e-5 rad, against the scores' 1e-4 relative bar (tests/test_parity_gpu.py::test_trained_range_*).
+constexpr float kInv2Pi = 0.15915494309189535f;
+__device__ __forceinline__ float hw_sin(float x) { return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(x * kInv2Pi)); }
+__device__ __forceinline__ float hw_cos(float x) { return __builtin_amdgcn_cosf(__builtin_amdgcn_fractf(x * kInv2Pi)); }
+
 template <int FN, bool CH, int V, int G>
 struct Query {
     vecf<V> q0[G], q1[G], q2[G];
@@ -305,53 +308,20 @@ struct Query {
             na_inv = rsqrt_f(wave_sum(sa));
             nb_inv = rsqrt_f(wave_sum(sb));
         }
-        // RotatE: the relation phases' cos / sin one element at a time (a rolled loop picking the element
-        // with wave-uniform selects): libm's cosf / sinf carry their large-argument reduction state, and
-        // G V of them interleaved made the XCD-sliced kernels spill (98 VGPRs at D = 1000)
+        // RotatE: the relation phases' cos / sin on the hardware units (hw_cos / hw_sin: two instructions and a
+        // fract per element; libm's argument reduction put the query build of the tile kernel's setup and of the
+        // head-batch positives on a long VALU chain, and G V of them interleaved spilled the tile kernel)
         float rc[G][V], rs[G][V];
-#if KGE_ROT_HW
-        // the hardware v_sin_f32 / v_cos_f32 (__sinf / __cosf, the phase scaled to revolutions): the phases are
-        // r / phase_div, within [-pi, pi] at initialisation (|r| <= the embedding range) and a few pi after
-        // training, where they are accurate to ~1e-6 absolute (the scores' 1e-4 bar is orders looser); two
-        // instructions per element instead of libm's argument reduction, which put the query build of the tile
-        // kernel's setup and of the head-batch positives on a long VALU chain
         if constexpr (FN == KGE_ROTATE) {
 #pragma unroll
             for (int k = 0; k < G; ++k)
 #pragma unroll
                 for (int i = 0; i < V; ++i) {
                     const float ph = ra[k].a[i] / p.phase_div;
-                    rc[k][i] = __cosf(ph);
-                    rs[k][i] = __sinf(ph);
+                    rc[k][i] = hw_cos(ph);
+                    rs[k][i] = hw_sin(ph);
                 }
         }
-#else
-        if constexpr (FN == KGE_ROTATE) {
-            constexpr int RU = KGE_ROT_CHUNK < G * V ? KGE_ROT_CHUNK : G * V;  // elements per iteration
-#pragma unroll 1
-            for (int e0 = 0; e0 < G * V; e0 += RU) {
-#pragma unroll
-                for (int u = 0; u < RU; ++u) {
-                    float r = 0.f;
-#pragma unroll
-                    for (int k = 0; k < G; ++k)
-#pragma unroll
-                        for (int i = 0; i < V; ++i)
-                            if (k * V + i == e0 + u) r = ra[k].a[i];
-                    const float ph = r / p.phase_div;
-                    const float c = cosf(ph), sn = sinf(ph);
-#pragma unroll
-                    for (int k = 0; k < G; ++k)
-#pragma unroll
-                        for (int i = 0; i < V; ++i)
-                            if (k * V + i == e0 + u) {
-                                rc[k][i] = c;
-                                rs[k][i] = sn;
-                            }
-                }
-            }
-        }
-#endif
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             const bool in = (lane + k * kWave) < DV;
@@ -531,11 +501,7 @@ __device__ __forceinline__ float cand_score(const Cand<FN, V, G>& c, const Q& q,
                 } else if constexpr (FN == KGE_PROTATE) {
                     const float pc = x / p.phase_div;
                     const float z = CH ? (pc + q.q0[k].a[i]) : (q.q0[k].a[i] - pc);
-#if KGE_ROT_HW
-                    acc += fabsf(__sinf(z));  // |z| <= ~3 pi: the hardware v_sin_f32 (see Query::build's RotatE)
-#else
-                    acc += fabsf(sinf(z));
-#endif
+                    acc += fabsf(hw_sin(z));  // the hardware v_sin_f32 on the fraction of z's revolutions
                 }
             }
     }
@@ -947,6 +913,211 @@ struct TileQueryIH {  // InterHT: q0, q1 from LDS, the relation third in registe
     vecf<V> q2[G];
 };
 
+// One group of a step plan (kge_internal.h: the plan layout), made by one block of NWV waves: the group's batch
+// rows (InterHT: ranks [g R, g R + R) of the batch in (relation, row) order, the same stable counting sort as
+// step_fwd_tile_kernel's step 0; else rows g R + r), their positives, and the group's items — every candidate
+// of its rows, and in tail-batch mode each row's positive as column N — counting-sorted by (entity slice,
+// entity bucket) into the group's list. The tile kernel's block (g, x) then sweeps list[soff[x], soff[x + 1]).
+// Order inside a bucket: arbitrary (LDS atomics); every item is scored on its own, so the scores do not depend
+// on it. sm: plan_lds_ints(NWV * 64) ints of LDS.
+template <int NWV>
+__device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
+    constexpr int NT = NWV * kWave, NB = kTileSortRel, MU = (kTileSortMaxB + NT - 1) / NT;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int R = a.R;
+    const int64_t g0 = (int64_t)g * R;
+    const int nr = (int)min<int64_t>(R, a.B - g0);
+    int* brow = sm;                        // [kTileMaxRows]
+    int* hist = brow + kTileMaxRows;       // [8][kTileBuckets]
+    int* wc = hist + 8 * kTileBuckets;     // [MU NWV][NB] the sort's per-wave bucket counts
+    if (a.sort) {  // step_fwd_tile_kernel's step 0 on the relation ids pos[i][1]
+        int bk[MU], wr[MU];
+        int64_t rv[MU];
+#pragma unroll
+        for (int u = 0; u < MU; ++u) rv[u] = a.pos[min<int64_t>(u * NT + t, a.B - 1) * 3 + 1];  // all in flight
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            const int64_t rr = rv[u];
+            bk[u] = u * NT + t >= a.B ? NB : ((rr >= 0 && rr < a.nrel) ? (int)min<int64_t>(rr, NB - 2) : NB - 1);
+        }
+        for (int i = t; i < MU * NWV * NB; i += NT) wc[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            wr[u] = 0;
+            if (u * NT >= a.B) continue;  // block-uniform
+            uint64_t todo = __ballot(bk[u] < NB);
+            while (todo) {
+                const int v = __builtin_amdgcn_readlane(bk[u], __builtin_ctzll(todo));
+                const uint64_t m = __ballot(bk[u] == v);
+                if (bk[u] == v) wr[u] = lanes_below(m);
+                if (lane == 0) wc[(u * NWV + w) * NB + v] = __popcll(m);
+                todo &= ~m;
+            }
+        }
+        __syncthreads();
+        if (w == 0) {
+            int y[MU * NWV];
+#pragma unroll
+            for (int c = 0; c < MU * NWV; ++c) y[c] = wc[c * NB + lane];
+            int run = 0;
+#pragma unroll
+            for (int c = 0; c < MU * NWV; ++c) {
+                const int v = y[c];
+                y[c] = run;
+                run += v;
+            }
+            int incl = run;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const int v = __shfl_up(incl, o, kWave);
+                if (lane >= o) incl += v;
+            }
+            const int base = incl - run;
+#pragma unroll
+            for (int c = 0; c < MU * NWV; ++c) wc[c * NB + lane] = y[c] + base;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            if (bk[u] >= NB) continue;
+            const int64_t rank = wc[(u * NWV + w) * NB + bk[u]] + wr[u];
+            if (rank >= g0 && rank < g0 + nr) brow[rank - g0] = u * NT + t;
+        }
+    } else if (t < nr) {
+        brow[t] = (int)(g0 + t);
+    }
+    for (int i = t; i < 8 * kTileBuckets; i += NT) hist[i] = 0;
+    __syncthreads();
+    // the items: (slice, bucket) key, checked id, code
+    const int Np = a.mode == KGE_HEAD_BATCH ? (int)a.N : (int)a.N + 1;
+    const int nf = nr * Np;
+    const int64_t S = (a.nent + 7) / 8;
+    const float invS = 1.f / (float)S, bscale = (float)kTileBuckets / (float)S, inv_np = 1.f / (float)Np;
+    // an item's id, by address select and one load (no branch: a walk's loads all go out together)
+    auto item_row = [&](int f, int& r) {
+        r = (int)((float)f * inv_np);  // f < 2^21: the float quotient corrected to the exact one
+        if (r * Np > f) --r;
+        if ((r + 1) * Np <= f) ++r;
+        const int n = f - r * Np;
+        const int64_t b = brow[r];
+        const int64_t* src = n < a.N ? a.neg + b * a.neg_ld + n : a.pos + b * 3 + 2;
+        return src;
+    };
+    auto classify = [&](int f, int r, int64_t id, int& key, int& idc, int& code) {
+        const int n = f - r * Np;
+        const bool valid = id >= 0 && id < a.nent;
+        int x = 0, bk = 0;
+        if (valid) {
+            x = min(7, (int)((float)id * invS));
+            if ((int64_t)x * S > id) --x;
+            if ((int64_t)(x + 1) * S <= id) ++x;
+            bk = min(kTileBuckets - 1, (int)((float)(int)(id - (int64_t)x * S) * bscale));
+        }
+        key = x * kTileBuckets + bk;
+        idc = valid ? (int)id : -1;
+        code = (r << 16) | n;
+    };
+    auto item = [&](int f, int& key, int& idc, int& code) {
+        int r;
+        const int64_t id = *item_row(f, r);
+        classify(f, r, id, key, idc, code);
+    };
+    constexpr int TPI = 17;  // C2's 16 x 257 items over 768 threads walked once; larger groups twice
+    const bool in_regs = nf <= TPI * NT;
+    int ky[TPI], ic[TPI], cd[TPI];
+    if (in_regs) {
+        int64_t idv[TPI];
+        int rr[TPI];
+#pragma unroll
+        for (int u = 0; u < TPI; ++u) idv[u] = *item_row(min(u * NT + t, nf - 1), rr[u]);
+#pragma unroll
+        for (int u = 0; u < TPI; ++u) {
+            const int f = u * NT + t;
+            ky[u] = -1;
+            if (f < nf) classify(f, rr[u], idv[u], ky[u], ic[u], cd[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < TPI; ++u)
+            if (ky[u] >= 0) atomicAdd(&hist[ky[u]], 1);
+    } else {
+        for (int f = t; f < nf; f += NT) {
+            int k, i, c;
+            item(f, k, i, c);
+            atomicAdd(&hist[k], 1);
+        }
+    }
+    // the rows' (b, h, r, t), ids checked (-1: out of range); the header
+    auto chk = [](int64_t id, int64_t n) { return (id >= 0 && id < n) ? (int)id : -1; };
+    if (t < R) {
+        int4 m = make_int4(-1, -1, -1, -1);
+        if (t < nr) {
+            const int64_t b = brow[t];
+            m = make_int4((int)b, chk(a.pos[b * 3], a.nent), chk(a.pos[b * 3 + 1], a.nrel), chk(a.pos[b * 3 + 2], a.nent));
+        }
+        reinterpret_cast<int4*>(a.plan + kPlanHdr)[(int64_t)g * R + t] = m;
+    }
+    if (g == 0 && t == 0) {
+        int* h = a.plan;
+        h[0] = kPlanMagic;
+        h[1] = (int)a.B;
+        h[2] = (int)a.N;
+        h[3] = a.mode;
+        h[4] = R;
+        h[5] = (int)a.nent;
+        h[6] = a.sort;
+    }
+    __syncthreads();
+    if (w == 0) {  // exclusive scan of the 8 x 256 counts, 32 per lane; the slice starts
+        constexpr int PL = 8 * kTileBuckets / kWave;
+        int v[PL], sum = 0;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) {
+            v[i] = hist[lane * PL + i];
+            sum += v[i];
+        }
+        int incl = sum;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const int y = __shfl_up(incl, o, kWave);
+            if (lane >= o) incl += y;
+        }
+        int run = incl - sum;
+        int* soff = a.plan + plan_soff(a.B, R) + (int64_t)g * 9;
+        if ((lane * PL) % kTileBuckets == 0) soff[lane * PL / kTileBuckets] = run;  // slice x starts at lane 8 x
+        if (lane == kWave - 1) soff[8] = incl;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) {
+            hist[lane * PL + i] = run;
+            run += v[i];
+        }
+    }
+    __syncthreads();
+    int2* list = reinterpret_cast<int2*>(a.plan + plan_list(a.B, R)) + (int64_t)g * R * (a.N + 1);
+    if (in_regs) {
+        int at[TPI];
+#pragma unroll
+        for (int u = 0; u < TPI; ++u) at[u] = ky[u] >= 0 ? atomicAdd(&hist[ky[u]], 1) : -1;
+#pragma unroll
+        for (int u = 0; u < TPI; ++u)
+            if (at[u] >= 0) list[at[u]] = make_int2(ic[u], cd[u]);
+    } else {
+        for (int f = t; f < nf; f += NT) {
+            int k, i, c;
+            item(f, k, i, c);
+            list[atomicAdd(&hist[k], 1)] = make_int2(i, c);
+        }
+    }
+}
+
+// kge_step_plan: a batch's plan on its own (the first batch of a planned run; later plans come from the tail
+// blocks of the step before)
+template <int NWV>
+__global__ __launch_bounds__(NWV * kWave) void tile_plan_kernel(PlanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char plan_smem[];
+    tile_plan_group<NWV>(a, (int)blockIdx.x, reinterpret_cast<int*>(plan_smem));
+}
+
 template <int FN, bool CH, int V, int G, int NWV>
 __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char tile_smem[];
@@ -964,10 +1135,40 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     int* cntp = hist + kTileBuckets;
     int* list = cntp + 4;  // also the relation sort's keys before the list is built
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (p.tile_next.plan && (int)blockIdx.x >= p.tile_blocks) {
+        // a tail block: the NEXT batch's plan, on the CUs the scoring blocks free up at the end of the launch
+        tile_plan_group<NWV>(p.tile_next, (int)blockIdx.x - p.tile_blocks, reinterpret_cast<int*>(tile_smem));
+        return;
+    }
     const int x = (int)(blockIdx.x & 7);
-    const int64_t g0 = (int64_t)(blockIdx.x >> 3) * R;
+    const int gi = (int)(blockIdx.x >> 3);
+    const int64_t g0 = (int64_t)gi * R;
     const int nr = (int)min<int64_t>(R, p.B - g0);
     if (nr <= 0) return;  // block-uniform
+    // a planned step (kge_step_forward_planned): rows, ids and this block's sorted items come from the plan
+    const int* pl = p.tile_plan;
+    const int4* pmeta = pl ? reinterpret_cast<const int4*>(pl + kPlanHdr) + (int64_t)gi * R : nullptr;
+    const int2* plist = pl ? reinterpret_cast<const int2*>(pl + plan_list(p.B, R)) + (int64_t)gi * R * (p.N + 1) : nullptr;
+    int plo = 0, pcnt = 0;
+    if (pl) {
+        const int mode = CH ? KGE_HEAD_BATCH : KGE_TAIL_BATCH;
+        if (pl[0] != kPlanMagic || pl[1] != (int)p.B || pl[2] != (int)p.N || pl[3] != mode || pl[4] != R ||
+            pl[5] != (int)p.c_rows) {
+            // not this batch shape's plan: every output of the block's rows (by index) becomes NaN, loudly
+            if (x == 0)
+                for (int r = w; r < nr; r += NWV) {
+                    for (int64_t n = lane; n < p.N; n += kWave) p.out[(g0 + r) * p.out_ld + n] = __builtin_nanf("");
+                    if (lane == 0) {
+                        if (p.out_pos_raw) p.out_pos_raw[g0 + r] = __builtin_nanf("");
+                        p.out_pos_ls[g0 + r] = __builtin_nanf("");
+                    }
+                }
+            return;
+        }
+        const int* so = pl + plan_soff(p.B, R) + (int64_t)gi * 9;
+        plo = so[x];
+        pcnt = so[x + 1] - plo;
+    }
     const int64_t S = (p.c_rows + 7) / 8;
     const int64_t e_lo = min((int64_t)x * S, p.c_rows), e_hi = min(p.c_rows, e_lo + S);
     // column N: the row's positive (its tail) in tail-batch mode, where it shares the negatives' query; head-batch
@@ -978,7 +1179,14 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     //    so that a block's rows share few relations and their relation thirds fit QS LDS slots), else rows g0 + r.
     //    A stable counting sort over kTileSortRel relation buckets: row i = (u NWV + w) 64 + lane is ranked inside
     //    its wave by ballots (one per distinct bucket of the wave), then by the bucket counts of the earlier waves.
-    if (p.tile_sort) {
+    if (pl) {
+        if (t < nr) {
+            const int4 m = pmeta[t];
+            brow[t] = m.x;
+            qid[t] = CH ? m.w : m.y;
+            rrow[t] = m.z;
+        }
+    } else if (p.tile_sort) {
         constexpr int MU = (kTileSortMaxB + NT - 1) / NT, NB = kTileSortRel;
         int* wc = list;  // [MU NWV][NB] per-wave bucket counts, then their exclusive prefixes
         int bk[MU], wr[MU];
@@ -1085,7 +1293,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
 #if KGE_TILE_EXP == 1
     const bool in_regs = false;  // experiment: the walk made after the query build (the two-pass form)
 #else
-    const bool in_regs = nf <= (int64_t)TPI * NT;  // block-uniform
+    const bool in_regs = !pl && nf <= (int64_t)TPI * NT;  // block-uniform
 #endif
     // (their loads are issued here, before the query build, so both latencies overlap)
     if (in_regs) {
@@ -1157,7 +1365,8 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             }
         }
     }
-    if (in_regs) {
+    if (pl) {
+    } else if (in_regs) {
 #pragma unroll
         for (int u = 0; u < TPI; ++u)
             if (wbk[u] >= 0) atomicAdd(&hist[wbk[u]], 1);
@@ -1179,7 +1388,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             for (int k = 0; k < G; ++k) q2img[(size_t)sl * W + lane + k * kWave] = bload<V>(sr, goff<V>(lane, k));
         }
     }
-    if (w == 0) {  // exclusive scan of the bucket counts (4 per lane)
+    if (!pl && w == 0) {  // exclusive scan of the bucket counts (4 per lane)
         constexpr int PL = kTileBuckets / kWave;
         int v[PL], s = 0;
 #pragma unroll
@@ -1202,7 +1411,8 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         if (lane == kWave - 1) cntp[0] = incl;
     }
     __syncthreads();
-    if (in_regs) {
+    if (pl) {
+    } else if (in_regs) {
         int at[TPI];
 #pragma unroll
         for (int u = 0; u < TPI; ++u) at[u] = wbk[u] >= 0 ? atomicAdd(&hist[wbk[u]], 1) : -1;
@@ -1216,7 +1426,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         }
     }
     __syncthreads();
-    const int cnt = cntp[0];
+    const int cnt = pl ? pcnt : cntp[0];
 
     if (p.tile_dry) return;
     // 3. the sweep: wave w takes items w, w + NWV, w + 2 NWV, ...; with KGE_TILE_DEPTH = 2 the next item's
@@ -1230,10 +1440,16 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         int code = 0;
         int64_t my_id = 0;
         if (lane < nc) {
-            code = list[c0 + NWV * lane];
-            const int r = code >> 16, n = code & 0xFFFF;
-            const int64_t b = brow[r];
-            my_id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
+            if (pl) {  // (checked entity id, code): no dependent id load
+                const int2 e = plist[plo + c0 + NWV * lane];
+                code = e.y;
+                my_id = e.x;
+            } else {
+                code = list[c0 + NWV * lane];
+                const int r = code >> 16, n = code & 0xFFFF;
+                const int64_t b = brow[r];
+                my_id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
+            }
         }
         auto load = [&](Item& it, int j) {
             bool ok;
@@ -1307,11 +1523,12 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         // (model.py:127-146), one wave per row
         for (int r = w; r < nr; r += NWV) {
             const int64_t b = brow[r];
-            const int64_t tt = p.pos_base[b * 3 + 2], row = tt - p.c_base;
+            const int4 pm = pl ? pmeta[r] : make_int4(0, 0, 0, 0);
+            const int64_t tt = pl ? pm.w : p.pos_base[b * 3 + 2], row = tt - p.c_base;
             const bool valid = row >= 0 && row < p.c_rows;
             if (valid ? (row < e_lo || row >= e_hi) : x != 0) continue;  // wave-uniform
             Query<FN, false, V, G> qp;
-            const int64_t hi = p.pos_base[b * 3], rj = p.pos_base[b * 3 + 1];
+            const int64_t hi = pl ? pm.y : p.pos_base[b * 3], rj = pl ? pm.z : p.pos_base[b * 3 + 1];
             const bool hok = hi >= 0 && hi < p.q_rows, rjok = rj >= 0 && rj < p.r_rows;
             qp.build(p.qent + (hok ? hi : 0) * p.q_ld, hok, p.rel + (rjok ? rj : 0) * p.r_ld + p.r_off, rjok, p.D,
                      lane, p);
@@ -1474,28 +1691,20 @@ __global__ __launch_bounds__(kBlock) void score_fwd_kernel(ScoreParams p) {
 //   * positive triple: single-mode score (tail formula) -> raw + logsigmoid   (model.py:127-146)
 //   * negative row b: sum softmax(T s) logsigmoid(-s) or mean logsigmoid(-s)  (model.py:168-171)
 // ---------------------------------------------------------------------------------------------
-// The forward row reductions' exp / log on the hardware v_exp_f32 / v_log_f32 (KGE_RR_HW = 1; ~1 ulp, well inside
-// the 1e-4 parity bar): with libm's expf / log1pf the C4 reduction (1 024 scores per row, 16 per lane, three
+// The forward row reductions' exp / log on the hardware v_exp_f32 / v_log_f32 (~1 ulp, well inside the 1e-4
+// parity bar): with libm's expf / log1pf the C4 reduction (1 024 scores per row, 16 per lane, three
 // transcendentals each) was compute-bound at 8.1 us per launch, 4.8 us on the hardware units
 // (profiles/r04_tile_setup_ab.txt). Every form's reduction (fused, neg_rows, neg_reduce, the row-sharded finish)
 // uses these two, so the forms stay bitwise equal to one another.
-#ifndef KGE_RR_HW
-#define KGE_RR_HW 1
-#endif
-__device__ __forceinline__ float rr_exp(float x) {
-#if KGE_RR_HW
-    return __expf(x);
-#else
-    return expf(x);
-#endif
+// log1p(e) for e = exp(-|x|) in [0, 1]: below 1/128 the series e (1 - e (1/2 - e / 3)) (relative error < e^3 / 4,
+// under 2^-22), above it the hardware log of 1 + e. log(1 + e) alone returns 0 for e < 2^-24 and loses the
+// relative accuracy of a small row loss (a well-separated row's logsigmoid(-s) ~ -e^s).
+__device__ __forceinline__ float rr_log1p(float e) {
+    const float series = e * (1.f - e * (0.5f - e * (1.f / 3.f)));
+    return e < (1.f / 128.f) ? series : __logf(1.f + e);
 }
-__device__ __forceinline__ float rr_log_sigmoid(float x) {
-#if KGE_RR_HW
-    return fminf(x, 0.f) - __logf(1.f + __expf(-fabsf(x)));
-#else
-    return log_sigmoid(x);
-#endif
-}
+__device__ __forceinline__ float rr_exp(float x) { return __expf(x); }
+__device__ __forceinline__ float rr_log_sigmoid(float x) { return fminf(x, 0.f) - rr_log1p(__expf(-fabsf(x))); }
 
 __device__ __forceinline__ float row_reduce(const float* row, int64_t N, float T, int adversarial, int lane) {
     if (adversarial) {

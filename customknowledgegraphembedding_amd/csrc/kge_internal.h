@@ -54,6 +54,41 @@ constexpr int shard_nq(int fn) {
 }
 constexpr int kFwdGradMaxG = 4;  // the fused forward + query gradient keeps 6 accumulators per element
 
+// ---------------------------------------------------------------------------------------------
+// The tile scorer's step plan (kge_step_plan / kge_step_forward_planned): everything step_fwd_tile_kernel
+// derives from a batch's ids alone, made ahead of the step. int32 words:
+//   [0, kPlanHdr)                 header: magic, B, N, mode, rows per group R, nentity, the relation sort flag
+//   meta  [groups][R][4]          per row of a group in the block's row order: batch row b (-1 past the batch),
+//                                 then its positive (h, r, t) with out-of-range ids as -1
+//   soff  [groups][9]             per group, the start of each entity slice's items in its list, then the total
+//   list  [groups][R (N + 1)][2]  per group, its items sorted by (slice, entity bucket): (candidate entity id
+//                                 or -1 when out of range, row << 16 | column) — column N: the row's positive
+// The plan is a snapshot of the batch's ids: the planned step reads no id but the plan's.
+// ---------------------------------------------------------------------------------------------
+constexpr int kPlanMagic = 0x4B475031;  // "KGP1"
+constexpr int kPlanHdr = 16;
+__host__ __device__ inline int64_t plan_groups(int64_t B, int R) { return (B + R - 1) / R; }
+__host__ __device__ inline int64_t plan_soff(int64_t B, int R) { return kPlanHdr + plan_groups(B, R) * R * 4; }
+__host__ __device__ inline int64_t plan_list(int64_t B, int R) { return (plan_soff(B, R) + plan_groups(B, R) * 9 + 3) & ~(int64_t)3; }
+__host__ __device__ inline int64_t plan_words(int64_t B, int64_t N, int R) {
+    return plan_list(B, R) + plan_groups(B, R) * R * (N + 1) * 2;
+}
+// one plan to make: the next batch's ids (same B, N) and where its plan goes
+struct PlanArgs {
+    const int64_t* pos;
+    const int64_t* neg;
+    int64_t neg_ld;
+    int64_t B, N, nent, nrel;
+    int mode;  // KGE_HEAD_BATCH / KGE_TAIL_BATCH
+    int R;     // batch rows per group
+    int sort;  // rows ranked by relation (InterHT, B <= kTileSortMaxB)
+    int* plan;
+};
+// LDS ints of one plan block of NT threads: row list, (slice, bucket) counts, the relation sort's wave counts
+__host__ __device__ constexpr int plan_lds_ints(int NT) {
+    return kTileMaxRows + 8 * kTileBuckets + (kTileSortMaxB + NT - 1) / NT * (NT / 64) * kTileSortRel;
+}
+
 // Parameters of one scoring launch. Rows are addressed as base + row * ld (floats).
 //   query entity row of batch row b:  q_idx ? q_idx[b * q_stride] : b
 //   relation row of batch row b:      r_idx ? r_idx[b * r_stride] : b      (+ r_off floats)
@@ -89,6 +124,9 @@ struct ScoreParams {
     int tile_sort;        // step_fwd_tile_kernel: 0, or the power of two >= B of the (relation, row) sort
     int tile_waves;       // step_fwd_tile_kernel: waves per block (8 or 16)
     int tile_dry;         // step_fwd_tile_kernel: setup only, no scoring (A/B knob KGE_TILE_DRY)
+    const int* tile_plan; // step_fwd_tile_kernel: this batch's plan (kge_step_forward_planned), or null
+    int tile_blocks;      // step_fwd_tile_kernel: scoring blocks; blocks past them make the next batch's plan
+    PlanArgs tile_next;   // ... that plan (tile_next.plan null: none)
     float* out;
     int64_t out_ld;
     int64_t B, N;

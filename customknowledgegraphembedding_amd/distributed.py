@@ -45,6 +45,7 @@ in an oracle-backed backend to check the orchestration with gloo (tests/test_dis
 """
 from __future__ import annotations
 
+import collections
 import warnings
 
 import numpy as np
@@ -52,7 +53,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from ._lib import FN_IDS, HEAD_BATCH, SINGLE, TAIL_BATCH, check
+from ._lib import FN_IDS, HEAD_BATCH, SINGLE, TAIL_BATCH, KGEHipError, check
 from . import _lib
 from .model import _dims_for
 
@@ -237,7 +238,7 @@ class NativeShardExec:
     world (collectives skipped, outputs meaningless: the host-cost probe). The workspace and the pinned
     summary buffers are torch allocations owned here."""
 
-    def __init__(self, sk, Bg, N, comm=None, probe=False, chunks=None, one_stream=False):
+    def __init__(self, sk, Bg, N, comm=None, probe=False, chunks=None, one_stream=False, timing=False):
         import ctypes
         lib = _lib.load()
         W, K = sk.world, default_chunks(sk.world, chunks)
@@ -249,30 +250,76 @@ class NativeShardExec:
         hi = lib.kge_shard_exec_host_ints(W, K)
         self.host = torch.empty(hi, dtype=torch.int32, pin_memory=True)
         h = ctypes.c_void_p()
-        flags = (1 if probe else 0) | (2 if one_stream else 0)  # KGE_EXEC_PROBE, KGE_EXEC_ONE_STREAM
+        # KGE_EXEC_PROBE, KGE_EXEC_ONE_STREAM, KGE_EXEC_TIMING
+        flags = (1 if probe else 0) | (2 if one_stream else 0) | (4 if timing else 0)
         check(lib.kge_shard_exec_create(ctypes.addressof(h), None if comm is None else comm.handle, flags,
                                         sk.fn, sk.nentity, sk.shard.shape[0], sk.entity_dim, sk.D, Bg, N, W, sk.rank,
                                         K, ws, nbytes, self.host.data_ptr(), hi), "kge_shard_exec_create")
         self.handle = h.value
         self.sk = sk
         self.comm = comm
+        # the batches planned ahead, oldest first: (pos, neg, mode, their tensor versions). The plan stream reads
+        # their ids asynchronously, and the C side matches a step to its plan by pointer: holding the tensors
+        # here until their step keeps the caching allocator from handing their memory to another batch, and the
+        # versions catch an in-place change of the ids between plan and step (the plan would be stale)
+        self._fifo = collections.deque()
+        self.broken = None  # the error of a failed step: the executor (and, under RCCL, its peers) is unusable
+
+    def _live(self):
+        if self.broken is not None:
+            raise KGEHipError(f"the native executor failed earlier ({self.broken}); an exec error is fatal to its "
+                              "communicator: make a new ShardedKGE / NativeComm")
 
     def plan(self, pos_g, neg_g, mode):
+        self._live()
         check(self.lib.kge_shard_exec_plan(self.handle, pos_g.data_ptr(), neg_g.data_ptr(), neg_g.stride(0), mode,
                                            _st(neg_g)), "kge_shard_exec_plan")
+        self._fifo.append((pos_g, neg_g, mode, pos_g._version, neg_g._version))
 
     def step(self, pos_g, neg_g, mode, temperature, adversarial, nxt=None):
+        self._live()
+        if self._fifo:
+            p0, n0, m0, v0, w0 = self._fifo[0]
+            if p0 is not pos_g or n0 is not neg_g or m0 != mode:
+                raise ValueError("NativeShardExec.step: the oldest batch planned ahead is another batch or mode "
+                                 "(steps must consume the planned batches in order)")
+            if pos_g._version != v0 or neg_g._version != w0:
+                raise ValueError("NativeShardExec.step: the batch's ids changed in place after it was planned")
         sk, B, N = self.sk, self.B, self.N
         out = torch.empty(B * (N + 3), dtype=torch.float32, device=sk.device)
         base = out.data_ptr()
         sh, rel = sk.shard, sk.relation_embedding
         npos, nneg, nmode = (nxt[0].data_ptr(), nxt[1].data_ptr(), nxt[2]) if nxt is not None else (None, None, 0)
-        check(self.lib.kge_shard_exec_step(
-            self.handle, sh.data_ptr(), sh.stride(0), sk.lo, rel.data_ptr(), rel.shape[0], rel.stride(0), sk.rel_off,
-            pos_g.data_ptr(), neg_g.data_ptr(), neg_g.stride(0), mode, sk.gamma, sk.emb_range, sk.modulus,
-            temperature, int(adversarial), npos, nneg, nmode, base, N, base + B * N * 4, base + B * (N + 1) * 4,
-            base + B * (N + 2) * 4, _st(sh)), "kge_shard_exec_step")
+        try:
+            check(self.lib.kge_shard_exec_step(
+                self.handle, sh.data_ptr(), sh.stride(0), sk.lo, rel.data_ptr(), rel.shape[0], rel.stride(0),
+                sk.rel_off, pos_g.data_ptr(), neg_g.data_ptr(), neg_g.stride(0), mode, sk.gamma, sk.emb_range,
+                sk.modulus, temperature, int(adversarial), npos, nneg, nmode, base, N, base + B * N * 4,
+                base + B * (N + 1) * 4, base + B * (N + 2) * 4, _st(sh)), "kge_shard_exec_step")
+        except KGEHipError as e:
+            self.broken = str(e)
+            raise
+        if self._fifo:
+            self._fifo.popleft()
+        if nxt is not None:
+            self._fifo.append((nxt[0], nxt[1], nxt[2], nxt[0]._version, nxt[1]._version))
         return out[B * N:B * (N + 1)], out[B * (N + 2):], out[:B * N].view(B, N)
+
+    def timings(self):
+        """KGE_EXEC_TIMING executors: the last step's device spans in us (kge_shard_exec_timings): step,
+        query gather, finish, and per chunk (query all-to-all, scoring, score all-to-all)."""
+        import ctypes
+        n = 3 + 3 * self.K
+        buf = (ctypes.c_float * n)()
+        check(self.lib.kge_shard_exec_timings(self.handle, ctypes.addressof(buf), n), "kge_shard_exec_timings")
+        v = list(buf)
+        return {"step_us": v[0], "gather_us": v[1], "finish_us": v[2],
+                "query_a2a_us": [v[3 + 3 * k] for k in range(self.K)],
+                "score_us": [v[4 + 3 * k] for k in range(self.K)],
+                "score_a2a_us": [v[5 + 3 * k] for k in range(self.K)]}
+
+    def host_wait_us(self, reset=True):
+        return float(self.lib.kge_shard_exec_host_wait_us(self.handle, int(reset)))
 
     def close(self):
         """Destroys the executor (its streams and events); its buffers go with this object. Not done at
@@ -791,7 +838,7 @@ class ShardedKGE:
             at += n
         return out, send
 
-    def use_native(self, comm=None, probe=False, one_stream=None):
+    def use_native(self, comm=None, probe=False, one_stream=None, timing=False):
         """Run step_forward through the native executor (NativeShardExec: one C call per rank-step, RCCL
         issued from C++): `comm` a NativeComm (W > 1, or W = 1 through RCCL), None at W = 1 (device copies),
         or `probe` (collectives skipped: host-cost measurement only). One executor per batch shape.
@@ -805,7 +852,9 @@ class ShardedKGE:
             raise ValueError("the native executor needs a NativeComm at world > 1")
         if one_stream is None:
             one_stream = os.environ.get("KGE_SHARD_ONE_STREAM", "1") != "0"
-        self._native_cfg = (comm, bool(probe), bool(one_stream))
+        for ex in getattr(self, "_native", {}).values():
+            ex.close()
+        self._native_cfg = (comm, bool(probe), bool(one_stream), bool(timing))
         self._native = {}
         return self
 
@@ -815,8 +864,9 @@ class ShardedKGE:
         key = (Bg, N, default_chunks(self.world, chunks))
         ex = self._native.get(key)
         if ex is None:
-            comm, probe, one = self._native_cfg
-            ex = self._native[key] = NativeShardExec(self, Bg, N, comm=comm, probe=probe, chunks=chunks, one_stream=one)
+            comm, probe, one, timing = self._native_cfg
+            ex = self._native[key] = NativeShardExec(self, Bg, N, comm=comm, probe=probe, chunks=chunks, one_stream=one,
+                                                     timing=timing)
         return ex
 
     @staticmethod

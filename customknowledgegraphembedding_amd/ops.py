@@ -150,6 +150,103 @@ def step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range,
     return out_neg, out_pos, neg_scores, pos_scores
 
 
+class StepPlanner:
+    """step_forward_raw with the tile scorer's id-only setup made one step AHEAD (kge_step_plan /
+    kge_step_forward_planned): a step loop that knows its next batch (run.py's prefetching input pipeline,
+    run.py:40-66) hands it to the current step, whose launch's tail blocks plan it, so the next step's blocks
+    start on their sorted candidates at once. Outputs are bitwise step_forward_raw's.
+
+        sp = StepPlanner(fn, ent, rel, rel_off, D, B, N, gamma, emb_range)
+        sp.plan(pos0, neg0, mode0)                    # the first batch's plan: one launch
+        out = sp.step(nxt=(pos1, neg1, mode1))        # batch 0's step + batch 1's plan
+        out = sp.step(nxt=(pos2, neg2, mode2))        # batch 1's step + ...
+
+    A plan is a snapshot of its batch's ids (the planned step reads no id but the plan's). The planner keeps
+    the tensors of the batch being planned until the step that consumes the plan, and two plan buffers
+    (the step reads one while its tail blocks write the other). The tables may change between steps (they are
+    read at step time). `available(...)` is False when the tile form does not apply (use step_forward_raw)."""
+
+    def __init__(self, fn, ent, rel, rel_off, D, B, N, gamma, emb_range, modulus=0.0, temperature=1.0,
+                 adversarial=True):
+        _need_gpu(ent, rel)
+        _fp32(ent, "entity_embedding")
+        _fp32(rel, "relation_embedding")
+        self.fn, self.ent, self.rel, self.rel_off, self.D = fn, ent, rel, rel_off, D
+        self.B, self.N = B, N
+        self.gamma, self.emb_range, self.modulus = float(gamma), float(emb_range), float(modulus)
+        self.temperature, self.adversarial = float(temperature), int(bool(adversarial))
+        nbytes = self.plan_size(fn, ent, rel, rel_off, D, B, N)
+        if nbytes <= 0:
+            raise _lib.KGEHipError("kge_step_plan_size is 0: the tile form does not apply to this shape "
+                                   "(use step_forward_raw)")
+        self._bufs = [torch.empty(nbytes, dtype=torch.uint8, device=ent.device) for _ in range(2)]
+        self._cur = None       # index of the buffer holding the next step's plan
+        self._mode = None      # that plan's batch mode
+        self._held = None      # the tensors that plan was made from (kept alive until its step)
+
+    @staticmethod
+    def plan_size(fn, ent, rel, rel_off, D, B, N):
+        return int(_lib.load().kge_step_plan_size(fn, ent.shape[0], ent.stride(0), rel.shape[0], rel.stride(0),
+                                                  rel_off, B, N, D))
+
+    @classmethod
+    def available(cls, fn, ent, rel, rel_off, D, B, N):
+        return cls.plan_size(fn, ent, rel, rel_off, D, B, N) > 0
+
+    def _check_batch(self, pos, neg, mode):
+        _need_gpu(pos, neg)
+        _i64(pos, "positive_sample")
+        _i64(neg, "negative_sample")
+        if mode not in (HEAD_BATCH, TAIL_BATCH):
+            raise ValueError("a planned step needs a negative mode (0 head-batch or 1 tail-batch)")
+        if tuple(pos.shape) != (self.B, 3) or not pos.is_contiguous():
+            raise ValueError(f"positive_sample must be a contiguous [{self.B}, 3] int64 tensor")
+        if tuple(neg.shape) != (self.B, self.N) or neg.stride(1) != 1:
+            raise ValueError(f"negative_sample must be a row-contiguous [{self.B}, {self.N}] int64 tensor")
+
+    def plan(self, pos, neg, mode):
+        """The plan of the batch the next step() scores (a run's first batch; later ones come from step)."""
+        self._check_batch(pos, neg, mode)
+        buf = 0 if self._cur is None else self._cur
+        rc = _lib.load().kge_step_plan(self.fn, mode, self.ent.shape[0], self.ent.stride(0), self.rel.shape[0],
+                                       self.rel.stride(0), self.rel_off, pos.data_ptr(), neg.data_ptr(),
+                                       neg.stride(0), self.B, self.N, self.D, self._bufs[buf].data_ptr(),
+                                       _stream(self.ent.device))
+        check(rc, "kge_step_plan")
+        self._cur, self._mode, self._held = buf, mode, (pos, neg)
+
+    def step(self, nxt=None, out=None):
+        """Both model calls on the planned batch -> (out_neg [B], out_pos [B], neg_scores [B, N],
+        pos_scores [B]); with nxt = (pos, neg, mode) the same launch plans that batch for the next step."""
+        if self._cur is None:
+            raise RuntimeError("StepPlanner.step: no batch planned (call plan() first, or pass nxt to step)")
+        dev = self.ent.device
+        if out is None:
+            out = (torch.empty((self.B,), dtype=torch.float32, device=dev),
+                   torch.empty((self.B,), dtype=torch.float32, device=dev),
+                   torch.empty((self.B, self.N), dtype=torch.float32, device=dev),
+                   torch.empty((self.B,), dtype=torch.float32, device=dev))
+        out_neg, out_pos, neg_scores, pos_scores = out
+        nbuf, npos, nneg, nmode = None, None, None, 0
+        if nxt is not None:
+            npos, nneg, nmode = nxt
+            self._check_batch(npos, nneg, nmode)
+            nbuf = 1 - self._cur
+        rc = _lib.load().kge_step_forward_planned(
+            self.fn, self._mode, self.ent.data_ptr(), self.ent.shape[0], self.ent.stride(0), self.rel.data_ptr(),
+            self.rel.shape[0], self.rel.stride(0), self.rel_off, self.B, self.N, self.D, self.gamma,
+            self.emb_range, self.modulus, self.temperature, self.adversarial, self._bufs[self._cur].data_ptr(),
+            ctypes_ptr(npos), ctypes_ptr(nneg), 0 if nneg is None else nneg.stride(0), nmode,
+            None if nbuf is None else self._bufs[nbuf].data_ptr(), neg_scores.data_ptr(), neg_scores.stride(0),
+            out_neg.data_ptr(), pos_scores.data_ptr(), out_pos.data_ptr(), _stream(dev))
+        check(rc, "kge_step_forward_planned")
+        if nxt is None:
+            self._cur, self._mode, self._held = None, None, None
+        else:
+            self._cur, self._mode, self._held = nbuf, nmode, (npos, nneg)
+        return out_neg, out_pos, neg_scores, pos_scores
+
+
 def step_finish_raw(fn, ent, rel, rel_off, pos, D, gamma, emb_range, neg_scores, modulus=0.0,
                     temperature=1.0, adversarial=True):
     """Second launch of step_forward_raw: positives + per-row reductions of `neg_scores`."""

@@ -28,6 +28,27 @@ def test_gpus2_self_launches_two_ranks_one_line():
     line = lines[0]
     assert line["n_gpus"] == 2 and line["steps"] == 3 and line["dry_run"]
     assert line["rank_sum"] == 1  # ranks 0 and 1 both joined the process group
+    # the N > 1 row-sharded record: per-variant step times, the selected form, and every rank's diagnosis
+    rs = line["yago3_10_rowshard"]
+    assert set(rs["variants"]) == {"torchcomm_python", "one_stream_1chunk", "two_stream_2chunk"}
+    assert rs["selected"] == bench.ROWSHARD_DEFAULT and rs["n_ranks_seen"] == 2
+    assert [r["rank"] for r in rs["per_rank"]] == [0, 1]
+    assert all(set(bench.ROWSHARD_RANK_KEYS) <= set(r) for r in rs["per_rank"])
+    assert rs["native_status"] == "ok" and rs["native_matches_torchcomm"] is True
+
+
+def test_rowshard_report_falls_back_to_the_python_path():
+    """A native communicator that failed its check, or a native step whose outputs differ from the
+    torch.distributed path's, leaves the Python path's numbers as the selected ones."""
+    w = bench.WORKLOADS["c4s"]
+    var = {"torchcomm_python": 2e-4, "one_stream_1chunk": 1e-4, "two_stream_2chunk": 1.2e-4}
+    ok = bench.rowshard_report(w, 8, 20, var, [], 8, "ok", True)
+    assert ok["selected"] == "one_stream_1chunk" and abs(ok["ms_per_step"] - 0.1) < 1e-9
+    assert ok["triples_per_s"] == (512 * 1024 + 512) * 8 / 1e-4
+    bad = bench.rowshard_report(w, 8, 20, var, [], 8, "ok", False)
+    assert bad["selected"] == "torchcomm_python"
+    err = bench.rowshard_report(w, 8, 20, {"torchcomm_python": 2e-4}, [], None, "native communicator: boom", None)
+    assert err["selected"] == "torchcomm_python" and abs(err["ms_per_step"] - 0.2) < 1e-9
 
 
 def test_gpus1_dry_run_is_single_process():

@@ -159,3 +159,26 @@ def test_native_comm_and_executor_through_rccl(rccl):
             ex.close()
     finally:
         nc.close()
+
+
+def test_bench_rowshard_multi_checks_itself_through_rccl(rccl):
+    """bench.py's N > 1 row-sharded section (rowshard_multi) at world 1 through RCCL: the native communicator's
+    known-answer check (ncclCommCount, a rank-tagged all-to-all), both executor forms' outputs equal to the
+    torch.distributed path's bitwise, the per-rank diagnosis from the executor's timing events, and the report
+    the driver's multi-GPU line carries."""
+    import argparse
+
+    import bench
+    import customknowledgegraphembedding_amd as kge
+    from customknowledgegraphembedding_amd import ops
+    bench.kge, bench.ops = kge, ops
+    a = argparse.Namespace(steps=3, warmup=1)
+    rep = bench.rowshard_multi(bench.WORKLOADS["c4s"], a, 1, 0, torch.device("cuda", 0))
+    assert rep["native_status"] == "ok" and rep["native_matches_torchcomm"] is True, rep
+    assert rep["n_ranks_seen"] == 1 and rep["selected"] == bench.ROWSHARD_DEFAULT
+    assert set(rep["variants"]) == {"torchcomm_python", "one_stream_1chunk", "two_stream_2chunk"}
+    (r0,) = rep["per_rank"]
+    assert all(r0[k] is not None and r0[k] >= 0 for k in bench.ROWSHARD_RANK_KEYS)
+    assert 0 < r0["kernel_busy_us"] <= r0["step_us"]
+    sp = r0["spans_of_one_step"]
+    assert len(sp["score_us"]) == 1 and len(sp["query_a2a_us"]) == 1

@@ -30,6 +30,27 @@ _c_f = ctypes.c_float
 _c_p = ctypes.c_void_p
 _c_i = ctypes.c_int
 
+
+
+class Forms(ctypes.Structure):
+    """struct kge_forms (include/kge_hip.h): an explicit kernel-form choice for the _ex entry points (A/B runs
+    and the bitwise cross-form tests); `forms(step_order="xcd", tile_rows=3)` builds one, the rest left to the
+    library."""
+    _fields_ = [("step_order", ctypes.c_int), ("xcd_phases", ctypes.c_int), ("tile_rows", ctypes.c_int),
+                ("tile_q2slots", ctypes.c_int), ("tile_waves", ctypes.c_int), ("gemm_form", ctypes.c_int),
+                ("transparse_form", ctypes.c_int)]
+
+
+_ORDERS = {"row": 0, "xcd": 1, "tile": 2}
+
+
+def forms(step_order=None, xcd_phases=0, tile_rows=0, tile_q2slots=None, tile_waves=0, gemm_form=0,
+          transparse_form=0):
+    so = -1 if step_order is None else (_ORDERS[step_order] if isinstance(step_order, str) else int(step_order))
+    return Forms(so, int(xcd_phases), int(tile_rows or 0), -1 if tile_q2slots is None else int(tile_q2slots),
+                 int(tile_waves or 0), int(gemm_form), int(transparse_form))
+
+
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
     "kge_abi_version": (_c_i, []),
@@ -45,6 +66,16 @@ SIGNATURES = {
         _c_i,
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
          _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p],
+    ),
+    "kge_score_indexed_ex": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_p, _c_i64, _c_p, _c_p],
+    ),
+    "kge_step_forward_ex": (
+        _c_i,
+        [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_i64,
+         _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
     ),
     "kge_step_plan_size": (_c_i64, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
     "kge_step_plan": (
@@ -109,6 +140,7 @@ SIGNATURES = {
         _c_i, [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
     "kge_gemm_nt": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p]),
     "kge_gemm_nt_bf16x3": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p]),
+    "kge_gemm_nt_bf16x3_ex": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p]),
     "kge_rank_filtered": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "kge_score_dense": (
         _c_i,
@@ -154,6 +186,10 @@ SIGNATURES = {
     "kge_sampler_destroy": (None, [_c_p]),
     "kge_transparse_score": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_i64,
                                     _c_i64, _c_i64, _c_i64, _c_f, _c_p, _c_i64, _c_p, _c_p]),
+    "kge_transparse_score_workspace_size": (ctypes.c_size_t, [_c_i, _c_i64, _c_i64, _c_i64]),
+    "kge_transparse_score_ex": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p,
+                                       _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_p, _c_i64, _c_p, _c_p, _c_p,
+                                       ctypes.c_size_t, _c_p]),
     "kge_transparse_bwd_workspace_size": (ctypes.c_size_t, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
     "kge_transparse_premul": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p]),
     "kge_transparse_score_bwd": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p,

@@ -602,10 +602,9 @@ void fill_dense(ScoreParams& p, int fn, int mode, const float* head, int64_t hea
 
 bool empty(int64_t B, int64_t N) { return B == 0 || N == 0; }
 
-// phases of kge_step_forward's XCD-sliced order (step_fwd_xcd_kernel): KGE_XCD_PHASES overrides (A/B runs)
-int xcd_phases(int64_t nentity, int64_t ent_ld) {
-    const char* env = getenv("KGE_XCD_PHASES");  // read per call: tests switch it inside one process
-    const int forced = env ? atoi(env) : 0;
+// phases of kge_step_forward's XCD-sliced order (step_fwd_xcd_kernel): forms->xcd_phases chooses (A/B runs)
+int xcd_phases(int64_t nentity, int64_t ent_ld, const kge_forms* forms) {
+    const int forced = forms ? forms->xcd_phases : 0;
     if (forced > 0) return std::min(forced, 16);
     // a table larger than the 256 MB Infinity Cache is swept in phases of ~96 MB (C2's 327.5 MB: 4 phases,
     // 139 -> 128.5 us); a table that fits gains nothing and pays the extra id walks (C3's 116 MB at 4
@@ -617,20 +616,20 @@ int xcd_phases(int64_t nentity, int64_t ent_ld) {
 
 // kge_step_forward's candidate order: 0 batch-row-major (KIND_STEP_FWD), 1 XCD-sliced ascending ids per wave
 // (KIND_STEP_FWD_XCD), 2 row-group x XCD-slice tiles (KIND_STEP_FWD_TILE, when its LDS plan fits).
-// KGE_STEP_ORDER=row|xcd|tile overrides the choice (A/B runs; read per call: tests switch it in one process).
-int step_order(int64_t nentity, int64_t N) {
-    const char* s = getenv("KGE_STEP_ORDER");
-    const int forced =
-        !s ? -1 : (strcmp(s, "tile") == 0 ? 2 : (strcmp(s, "xcd") == 0 ? 1 : (strcmp(s, "row") == 0 ? 0 : -1)));
+// forms->step_order chooses (A/B runs and the cross-form tests).
+int step_order(int64_t nentity, int64_t N, const kge_forms* forms = nullptr) {
+    const int forced = forms ? forms->step_order : -1;
     if (nentity >= (int64_t)8 << 25) return 0;  // sort keys hold (id - slice start) << 6
-    if (forced >= 0) return forced;
+    if (forced >= 0 && forced <= 2) return forced;
     return N >= 128 ? 2 : 0;
 }
-bool use_xcd_order(int64_t nentity, int64_t N) { return step_order(nentity, N) != 0; }
+bool use_xcd_order(int64_t nentity, int64_t N, const kge_forms* forms = nullptr) {
+    return step_order(nentity, N, forms) != 0;
+}
 
 // Rows per block of the tile kernel (step_fwd_tile_kernel) and its dynamic LDS: 0 when the plan does not fit
-// (then the XCD-sliced form runs). KGE_TILE_ROWS caps the row count (A/B runs).
-int tile_plan(int fn, ScoreParams& p) {
+// (then the XCD-sliced form runs). forms->tile_rows caps the row count, tile_waves / tile_q2slots choose.
+int tile_plan(int fn, ScoreParams& p, const kge_forms* forms = nullptr) {
     int V = 1, G = 1;
     if (pick_vg(p, V, G)) return 0;
     if (G > kFwdGradMaxG || p.N + 1 > 65536 || p.c_rows <= 0) return 0;
@@ -644,11 +643,11 @@ int tile_plan(int fn, ScoreParams& p) {
     // waves per block (each two candidate rows deep): 12 for candidate rows of 4 KB or more (3 waves per SIMD
     // at <= 168 VGPRs; C2 InterHT 105 -> 95 us and C3 RotatE 124-131 -> 115-120 us against 8 waves, whose
     // 2 waves per SIMD leave the score's VALU exposed; 16 spills), 16 for smaller rows (C4 DistMult: 2 KB rows
-    // need the waves for bytes in flight). KGE_TILE_WAVES overrides (8, 12, 16).
+    // need the waves for bytes in flight). forms->tile_waves chooses (8, 12, 16).
     const int64_t row_bytes = (int64_t)p.D * 4 * (is_split(fn) ? 2 : 1);
     p.tile_waves = row_bytes >= 4096 ? 12 : 16;
-    const char* wenv = getenv("KGE_TILE_WAVES");
-    if (wenv && (atoi(wenv) == 8 || atoi(wenv) == 12 || atoi(wenv) == 16)) p.tile_waves = atoi(wenv);
+    const int fw = forms ? forms->tile_waves : 0;
+    if (fw == 8 || fw == 12 || fw == 16) p.tile_waves = fw;
     const int64_t NT = (int64_t)p.tile_waves * kWave;
     const int64_t qrow = tile_nq(fn) * opb + 8 + 8 + 8 + 4, lrow = (p.N + 1) * 4;  // + rrow, brow, qid, q2slot
     const int64_t fixed = kTileBuckets * 4 + 16;
@@ -657,15 +656,13 @@ int tile_plan(int fn, ScoreParams& p) {
     const int64_t sort_ints = P2 ? (kTileSortMaxB + NT - 1) / NT * p.tile_waves * kTileSortRel : 0;
     auto lds = [&](int64_t R, int64_t QS) { return R * qrow + QS * opb + fixed + std::max(R * lrow, sort_ints * 4); };
     int64_t R = kTileMaxRows;
-    const char* env = getenv("KGE_TILE_ROWS");
-    if (env && atoi(env) > 0) R = std::min<int64_t>(R, atoi(env));
+    if (forms && forms->tile_rows > 0) R = std::min<int64_t>(R, forms->tile_rows);
     while (R >= 1 && lds(R, 0) > kTileLdsMax) --R;
     if (R < 1) return 0;
     int64_t QS = 0;
     if (fn == KGE_INTERHT)
         while (QS < R && lds(R, QS + 1) <= kTileLdsMax) ++QS;
-    const char* qenv = getenv("KGE_TILE_Q2SLOTS");
-    if (qenv) QS = std::min<int64_t>(QS, std::max(0, atoi(qenv)));
+    if (forms && forms->tile_q2slots >= 0) QS = std::min<int64_t>(QS, forms->tile_q2slots);
 #ifdef KGE_PROFILING_KNOBS
     // profiling-only A/B knobs (a build with -DKGE_PROFILING_KNOBS): KGE_TILE_DRY=<level> runs the setup alone and
     // writes no scores; KGE_TILE_NOSORT keeps the batch-row order
@@ -736,6 +733,14 @@ int kge_score_indexed(int fn, int mode, const float* ent, int64_t nentity, int64
                       int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
                       int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
                       float* scores, int64_t scores_ld, void* stream) {
+    return kge_score_indexed_ex(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B,
+                                N, D, gamma, emb_range, modulus, scores, scores_ld, nullptr, stream);
+}
+
+int kge_score_indexed_ex(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                         int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                         int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
+                         float* scores, int64_t scores_ld, const kge_forms* forms, void* stream) {
     int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
     if (B < 0 || N < 0 || D <= 0) return fail(KGE_EINVAL, "bad shape (B, N, D)");
@@ -748,8 +753,8 @@ int kge_score_indexed(int fn, int mode, const float* ent, int64_t nentity, int64
                  emb_range, modulus);
     p.out = scores;
     p.out_ld = scores_ld;
-    if (mode != KGE_SINGLE && nentity < ((int64_t)1 << 31) && use_xcd_order(nentity, N)) {
-        if (step_order(nentity, N) == 2 && tile_plan(fn, p))
+    if (mode != KGE_SINGLE && nentity < ((int64_t)1 << 31) && use_xcd_order(nentity, N, forms)) {
+        if (step_order(nentity, N, forms) == 2 && tile_plan(fn, p, forms))
             return run_score(fn, mode, p, KIND_SCORE_TILE, stream);  // row-group x XCD-slice tiles (§3.0)
         return run_score(fn, mode, p, KIND_SCORE_SHARD_XCD, stream);  // XCD-sliced gather order (§3.0)
     }
@@ -785,6 +790,16 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
                      int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
                      float temperature, int adversarial, float* neg_scores, int64_t ns_ld, float* out_neg,
                      float* pos_scores, float* out_pos, float* cand_stats, void* stream) {
+    return kge_step_forward_ex(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, B, N,
+                               D, gamma, emb_range, modulus, temperature, adversarial, neg_scores, ns_ld, out_neg,
+                               pos_scores, out_pos, cand_stats, nullptr, stream);
+}
+
+int kge_step_forward_ex(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                        int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                        int64_t neg_ld, int64_t B, int64_t N, int64_t D, float gamma, float emb_range, float modulus,
+                        float temperature, int adversarial, float* neg_scores, int64_t ns_ld, float* out_neg,
+                        float* pos_scores, float* out_pos, float* cand_stats, const kge_forms* forms, void* stream) {
     int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
     if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_forward needs a negative mode (0 or 1)");
@@ -803,15 +818,15 @@ int kge_step_forward(int fn, int mode, const float* ent, int64_t nentity, int64_
     p.out_neg = out_neg;
     p.out_pos_raw = pos_scores;
     p.out_pos_ls = out_pos;
-    const int order = step_order(nentity, N);
+    const int order = step_order(nentity, N, forms);
     if (!(cand_stats && fn == KGE_INTERHT) && order != 0) {
         // two launches: the negatives (and the positives) in row-group x XCD-slice tiles or in XCD-sliced
         // ascending-id order, then the rows' self-adversarial reductions
-        if (order == 2 && tile_plan(fn, p)) {
+        if (order == 2 && tile_plan(fn, p, forms)) {
             p.tile_pos = 1;
             rc = run_score(fn, mode, p, KIND_STEP_FWD_TILE, stream);
         } else {
-            p.xcd_phases = xcd_phases(nentity, ent_ld);
+            p.xcd_phases = xcd_phases(nentity, ent_ld, forms);
             rc = run_score(fn, mode, p, KIND_STEP_FWD_XCD, stream);
         }
         if (rc) return rc;
@@ -1044,13 +1059,18 @@ int kge_gemm_nt(const float* A, int64_t lda, const float* Bm, int64_t ldb, float
 
 int kge_gemm_nt_bf16x3(const float* A, int64_t lda, const float* Bm, int64_t ldb, float* C, int64_t ldc, int64_t M,
                       int64_t N, int64_t K, void* stream) {
+    return kge_gemm_nt_bf16x3_ex(A, lda, Bm, ldb, C, ldc, M, N, K, nullptr, stream);
+}
+
+int kge_gemm_nt_bf16x3_ex(const float* A, int64_t lda, const float* Bm, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                          int64_t N, int64_t K, const kge_forms* forms, void* stream) {
     if (M < 0 || N < 0 || K < 0) return fail(KGE_EINVAL, "bad shape");
     if (M == 0 || N == 0) return ok();
     if (!A || !Bm || !C) return fail(KGE_EINVAL, "null pointer");
     if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return fail(KGE_EINVAL, "shape exceeds int32");
     if (K % 4 || lda % 4 || ldb % 4 || !aligned(A, 16) || !aligned(Bm, 16))
         return fail(KGE_ENOTSUP, "kge_gemm_nt_bf16x3 needs K, lda, ldb multiples of 4 and 16-byte aligned A, B");
-    launch_gemm_nt_f32x3(A, Bm, C, (int)M, (int)N, (int)K, lda, ldb, ldc, (hipStream_t)stream);
+    launch_gemm_nt_f32x3(A, Bm, C, (int)M, (int)N, (int)K, lda, ldb, ldc, (hipStream_t)stream, forms ? forms->gemm_form : 0);
     return check_launch("kge_gemm_nt_bf16x3");
 }
 

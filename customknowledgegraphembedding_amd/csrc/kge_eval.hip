@@ -375,7 +375,6 @@ int launch_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K
     const int64_t t128 = tm * ((N + 127) / 128), t64 = tm * ((N + 63) / 64);
     int bn = t128 < 256 ? 64 : 128;
     const int64_t t256 = tm * ((N + 255) / 256);
-    if (const char* env = getenv("KGE_GEMM_BN")) bn = atoi(env) == 64 ? 64 : (atoi(env) == 256 ? 256 : 128);
     if (bn == 256)
         hipLaunchKernelGGL(gemm_nt_f32_kernel<256>, dim3((unsigned)t256), dim3(kBlock), 0, st, A, B, C, M, N, K, lda,
                            ldb, ldc);
@@ -544,11 +543,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
 }  // namespace
 
 int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
-                         int64_t ldc, hipStream_t st) {
+                         int64_t ldc, hipStream_t st, int form) {
     // the split-once kernel when its 32-bit buffer offsets cover both operands and its rows take float4 loads;
-    // KGE_GEMM_X3S=0 keeps gemm_nt_f32x3_kernel (A/B runs; read per call)
-    const char* env = getenv("KGE_GEMM_X3S");
-    if (!(env && env[0] == '0') && (int64_t)M * lda * 4 < (int64_t)XS_OOB && (int64_t)N * ldb * 4 < (int64_t)XS_OOB &&
+    // form 1 (kge_forms.gemm_form) keeps gemm_nt_f32x3_kernel, which splits each fragment in registers
+    if (form == 0 && (int64_t)M * lda * 4 < (int64_t)XS_OOB && (int64_t)N * ldb * 4 < (int64_t)XS_OOB &&
         K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0) {
         static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3s_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;

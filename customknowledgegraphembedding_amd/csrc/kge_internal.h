@@ -221,7 +221,7 @@ int launch_eval_query_any(int fn, bool ch, const ScoreParams& p, hipStream_t st,
 int launch_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
                    int64_t ldc, hipStream_t st);
 int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
-                         int64_t ldc, hipStream_t st);
+                         int64_t ldc, hipStream_t st, int form = 0);
 int launch_rank(const float* S, int64_t M, int64_t N, int64_t ld, const int64_t* truth, const int64_t* fptr,
                 const int64_t* fids, int64_t* ranks, hipStream_t st);
 

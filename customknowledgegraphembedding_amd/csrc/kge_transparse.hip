@@ -91,6 +91,12 @@ struct TsParams {
     float* d_W;
     float* pdw;  // [S, R, d, d] split partials (S > 1)
     int S, T;
+    // ts_fwd_x3g_kernel's column split (kge_transparse_score_ex with a workspace): each block of a row chunk
+    // takes `xsplit` column ranges' one; its per-row sums go to xpart [blocks][XGR] and ts_x3g_finish_kernel adds
+    // them in split order
+    int xsplit;
+    float2* xpart;
+    int form;  // kge_forms.transparse_form: 0 the library's, 1 the forward's operands split per fragment
 };
 
 __device__ __forceinline__ int64_t row_entity(const TsParams& p, int64_t b, int64_t n) {
@@ -1106,36 +1112,51 @@ ts_fwd_x3s_kernel(TsParams p) {
 // The per-row sums over the columns are taken per wave (half-wave shuffles), then over the 8 waves in wave
 // order: the products are ts_rows_kernel's, the column sums in another order (scores within fp32 rounding).
 // ---------------------------------------------------------------------------------------------
+// Column split (round 5): with the whole column range per block only one block per relation works (~12 CUs at
+// C6); ts_fwd_x3g_kernel<4, 1> gives a block 4 waves x 32 columns = 128 columns of its rows, the xsplit blocks of
+// a row chunk together all of them, and writes its per-row sums (over its waves, in wave order) to the
+// workspace; ts_x3g_finish_kernel adds the splits in order: deterministic, scores within fp32 rounding of the
+// one-block form.
 constexpr int XGR = 64, XGC = 512;
 constexpr int kXgAPlane = XGR * 32, kXgBPlane = XGC * 32;
 constexpr int kXgStage = 3 * (kXgAPlane + kXgBPlane);
+// LDS of one pipeline stage for a block of NWV waves x JPW column tiles of 32
+constexpr int xg_bplane(int NWV, int JPW) { return NWV * JPW * 32 * 32; }
+constexpr int xg_stage(int NWV, int JPW) { return 3 * (kXgAPlane + xg_bplane(NWV, JPW)); }
 
+template <int JPW>
 struct XgRegs {
-    float4 a, b[2][2], m[2][2];
+    float4 a, b[JPW][2], m[JPW][2];
 };
 
-__global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(2))) void
+template <int NWV, int JPW>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, NWV * kWave), amdgpu_waves_per_eu(2))) void
 ts_fwd_x3g_kernel(TsParams p) {
+    constexpr int NT = NWV * kWave, CW = NWV * JPW * 32;  // threads, columns per pass
+    constexpr int BPL = xg_bplane(NWV, JPW), STG = xg_stage(NWV, JPW);
+    static_assert(NT >= 4 * XGR, "one A float4 per thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char xg_smem[];  // 2 stages, then u - 1 (d floats)
     __shared__ int rb[XGR], rid[XGR];
-    __shared__ float2 part[kXWaves][XGR];
+    __shared__ float2 part[NWV][XGR];
     __shared__ float2 red[XGR];
-    __shared__ float wsum[kXWaves];
-    __shared__ int wcnt[kXWaves];
-    float* cs = reinterpret_cast<float*>(xg_smem + 2 * kXgStage);
+    __shared__ int wcnt[NWV];
+    float* cs = reinterpret_cast<float*>(xg_smem + 2 * STG);
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int half = lane >> 5, col = lane & 31;
     const int d = p.d;
-    const int64_t r = blockIdx.x / p.nchunk;  // == nrel: the out-of-range bucket
-    const int64_t skip = (int64_t)(blockIdx.x % p.nchunk) * XGR;
+    const int xs = p.xsplit > 1 ? p.xsplit : 1;
+    const int split = (int)(blockIdx.x % xs);            // this block's column range (xsplit > 1)
+    const int64_t rc = blockIdx.x / xs;                  // its (relation, row chunk)
+    const int64_t r = rc / p.nchunk;  // == nrel: the out-of-range bucket
+    const int64_t skip = (int64_t)(rc % p.nchunk) * XGR;
     // this block's rows: the batch rows of relation bucket r, ranks [skip, skip + 64), by an ordered ballot scan
     if (t < XGR) {
         rb[t] = -1;
         red[t] = make_float2(0.f, 0.f);
     }
     int64_t seen = 0;
-    for (int64_t s = 0; s < p.B; s += kXThreads) {
+    for (int64_t s = 0; s < p.B; s += NT) {
         const int64_t b = s + t;
         bool m = false;
         if (b < p.B) {
@@ -1147,7 +1168,7 @@ ts_fwd_x3g_kernel(TsParams p) {
         __syncthreads();
         int before = 0, total = 0;
 #pragma unroll
-        for (int w = 0; w < kXWaves; ++w) {
+        for (int w = 0; w < NWV; ++w) {
             before += (w < wave) ? wcnt[w] : 0;
             total += wcnt[w];
         }
@@ -1160,7 +1181,7 @@ ts_fwd_x3g_kernel(TsParams p) {
         if (seen >= skip + XGR) break;  // uniform
     }
     const int nrows = (int)min<int64_t>(XGR, seen - skip);
-    if (nrows <= 0) return;  // uniform
+    if (nrows <= 0) return;  // uniform (the finish skips a chunk without rows too)
     if (t < XGR) {
         int id = -1;
         if (rb[t] >= 0) {
@@ -1170,21 +1191,29 @@ ts_fwd_x3g_kernel(TsParams p) {
         rid[t] = id;
     }
     const bool rok = r >= 0 && r < p.nrel;
-    {  // u - 1 for the relation row
-        float ss = 0.f;
-        for (int j = t; j < d; j += kXThreads) {
-            const float v = rok ? p.rel[r * p.rel_ld + j] : 0.f;
-            cs[j] = v;
-            ss += v * v;
+    {  // u - 1 for the relation row (the norm summed over 512 threads' strides in the same order at any NWV:
+       // every split of the column-split form sees the same u - 1 as the one-block form)
+        float ss[kXThreads / NT];
+#pragma unroll
+        for (int q = 0; q < kXThreads / NT; ++q) {
+            ss[q] = 0.f;
+            for (int j = t + q * NT; j < d; j += kXThreads) {
+                const float v = rok ? p.rel[r * p.rel_ld + j] : 0.f;
+                cs[j] = v;
+                ss[q] += v * v;
+            }
+            for (int o = 32; o > 0; o >>= 1) ss[q] += __shfl_xor(ss[q], o, kWave);
         }
-        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, kWave);
-        if (lane == 0) wsum[wave] = ss;
+        __shared__ float wsum8[kXWaves];
+#pragma unroll
+        for (int q = 0; q < kXThreads / NT; ++q)
+            if (lane == 0) wsum8[q * NWV + wave] = ss[q];
         __syncthreads();
         float tot = 0.f;
 #pragma unroll
-        for (int w = 0; w < kXWaves; ++w) tot += wsum[w];
+        for (int w = 0; w < kXWaves; ++w) tot += wsum8[w];
         const float rnorm = sqrtf(tot);
-        for (int j = t; j < d; j += kXThreads) cs[j] = cs[j] / rnorm - 1.f;
+        for (int j = t; j < d; j += NT) cs[j] = cs[j] / rnorm - 1.f;
     }
     __syncthreads();
     const rsrc_t ra = make_rsrc(p.ent, (uint32_t)(p.nent * p.ent_ld * 4));
@@ -1194,19 +1223,21 @@ ts_fwd_x3g_kernel(TsParams p) {
     const bool fuse_mask = !p.Mpre;
     const rsrc_t rm = make_rsrc(fuse_mask && rok ? p.mask + r * (int64_t)d * d : p.W, fuse_mask ? mbytes : 0u);
     const int aid = t < 4 * XGR ? rid[t >> 2] : -1, aq = t & 3, bkp = t & 7, bjq = t >> 3;
-    const int nk = (d + 15) / 16, npass = (d + XGC - 1) / XGC, T = nk * npass;
+    // one-block form: every pass of CW columns; split form: the one pass of columns [split CW, split CW + CW)
+    const int nk = (d + 15) / 16, npass = xs > 1 ? 1 : (d + CW - 1) / CW, T = nk * npass;
+    const int col0 = xs > 1 ? split * CW : 0;
 
-    auto gload = [&](XgRegs& R, int g) {
+    auto gload = [&](XgRegs<JPW>& R, int g) {
         const int pc = g / nk, k0 = (g - pc * nk) * 16;
         const int ka = k0 + 4 * aq;
         const uint32_t oa = (aid >= 0 && ka < d) ? (uint32_t)(((int64_t)aid * p.ent_ld + ka) * 4) : kXsOOB;
         const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa, 0, 0);
         R.a = make_float4(__uint_as_float(va[0]), __uint_as_float(va[1]), __uint_as_float(va[2]), __uint_as_float(va[3]));
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < JPW; ++u)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int kb = k0 + 2 * bkp + h, j = pc * XGC + 4 * (bjq + 64 * u);
+                const int kb = k0 + 2 * bkp + h, j = col0 + pc * CW + 4 * (bjq + (NT / 8) * u);
                 const uint32_t ob = (kb < d && j < d) ? (uint32_t)(((int64_t)kb * d + j) * 4) : kXsOOB;
                 const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rw, ob, 0, 0);
                 R.b[u][h] = make_float4(__uint_as_float(vb[0]), __uint_as_float(vb[1]), __uint_as_float(vb[2]),
@@ -1218,8 +1249,8 @@ ts_fwd_x3g_kernel(TsParams p) {
                 }
             }
     };
-    auto sstore = [&](const XgRegs& R, int stage) {
-        unsigned char* A = xg_smem + stage * kXgStage;
+    auto sstore = [&](const XgRegs<JPW>& R, int stage) {
+        unsigned char* A = xg_smem + stage * STG;
         unsigned char* Bp = A + 3 * kXgAPlane;
         if (t < 4 * XGR) {
             const int row = t >> 2;
@@ -1231,7 +1262,7 @@ ts_fwd_x3g_kernel(TsParams p) {
             *reinterpret_cast<bf16x4_t*>(A + 2 * kXgAPlane + o) = s2;
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < JPW; ++u) {
             float4 b0 = R.b[u][0], b1 = R.b[u][1];
             if (fuse_mask) {
                 b0 = mul4(b0, R.m[u][0]);
@@ -1242,25 +1273,25 @@ ts_fwd_x3g_kernel(TsParams p) {
             split3_x4(f32x4_t{b1.x, b1.y, b1.z, b1.w}, o0, o1, o2);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                const int cl = 4 * (bjq + 64 * u) + c;
+                const int cl = 4 * (bjq + (NT / 8) * u) + c;
                 const int o = xs_off(cl, bkp >> 2) + (bkp & 3) * 4;
                 *reinterpret_cast<bf16x2_t*>(Bp + o) = bf16x2_t{e0[c], o0[c]};
-                *reinterpret_cast<bf16x2_t*>(Bp + kXgBPlane + o) = bf16x2_t{e1[c], o1[c]};
-                *reinterpret_cast<bf16x2_t*>(Bp + 2 * kXgBPlane + o) = bf16x2_t{e2[c], o2[c]};
+                *reinterpret_cast<bf16x2_t*>(Bp + BPL + o) = bf16x2_t{e1[c], o1[c]};
+                *reinterpret_cast<bf16x2_t*>(Bp + 2 * BPL + o) = bf16x2_t{e2[c], o2[c]};
             }
         }
     };
-    f32x16 acc[2][2];
+    f32x16 acc[2][JPW];
     auto zero_acc = [&]() {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < JPW; ++j)
 #pragma unroll
                 for (int r2 = 0; r2 < 16; ++r2) acc[i][j][r2] = 0.f;
     };
     auto compute = [&](int stage) {
-        const unsigned char* A = xg_smem + stage * kXgStage;
+        const unsigned char* A = xg_smem + stage * STG;
         const unsigned char* Bp = A + 3 * kXgAPlane;
         bf16x8 a[2][3];
 #pragma unroll
@@ -1270,11 +1301,11 @@ ts_fwd_x3g_kernel(TsParams p) {
             for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * kXgAPlane + o);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int o = xs_off(wave * 64 + j * 32 + col, half);
+        for (int j = 0; j < JPW; ++j) {
+            const int o = xs_off(wave * JPW * 32 + j * 32 + col, half);
             bf16x8 bb[3];
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) bb[pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * kXgBPlane + o);
+            for (int pl = 0; pl < 3; ++pl) bb[pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * BPL + o);
 #pragma unroll
             for (int q = 0; q < 6; ++q)
 #pragma unroll
@@ -1289,8 +1320,8 @@ ts_fwd_x3g_kernel(TsParams p) {
             for (int r2 = 0; r2 < 16; ++r2) {
                 float sq = 0.f, ab = 0.f;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int cg = pc * XGC + wave * 64 + j * 32 + col;
+                for (int j = 0; j < JPW; ++j) {
+                    const int cg = col0 + pc * CW + wave * JPW * 32 + j * 32 + col;
                     const float c = cg < d ? cs[cg] : 0.f;
                     const float v = acc[i][j][r2];
                     sq = fmaf(v, v, sq);
@@ -1307,11 +1338,11 @@ ts_fwd_x3g_kernel(TsParams p) {
         if (t < XGR) {
             float2 x = red[t];
 #pragma unroll
-            for (int w = 0; w < kXWaves; ++w) x = make_float2(x.x + part[w][t].x, x.y + part[w][t].y);
+            for (int w = 0; w < NWV; ++w) x = make_float2(x.x + part[w][t].x, x.y + part[w][t].y);
             red[t] = x;
         }
     };
-    auto step = [&](int g, XgRegs& nxt) {
+    auto step = [&](int g, XgRegs<JPW>& nxt) {
         compute(g & 1);
         if (g + 1 < T) sstore(nxt, (g + 1) & 1);
         if (g + 3 < T) gload(nxt, g + 3);
@@ -1321,7 +1352,7 @@ ts_fwd_x3g_kernel(TsParams p) {
         }
         __syncthreads();
     };
-    XgRegs R0, R1;
+    XgRegs<JPW> R0, R1;
     zero_acc();
     gload(R0, 0);
     if (T > 1) gload(R1, 1);
@@ -1334,8 +1365,58 @@ ts_fwd_x3g_kernel(TsParams p) {
         step(g + 1, R0);
     }
     if (g < T) step(g, R1);
+    if (xs > 1) {  // the split's per-row sums; ts_x3g_finish_kernel adds the splits in order
+        if (t < XGR) p.xpart[blockIdx.x * XGR + t] = red[t];
+        return;
+    }
     if (t < nrows) {
         const float2 x = red[t];
+        const int64_t b = rb[t];
+        p.out[b * p.out_ld] = p.gamma - x.y / sqrtf(x.x);
+        if (p.stats) p.stats[b * p.N] = x;
+    }
+}
+
+// The column-split form's finish: one block per (relation, row chunk), its rows found as the split blocks
+// found them, each row's per-split sums added in split order.
+__global__ __launch_bounds__(kBlock) void ts_x3g_finish_kernel(TsParams p) {
+    __shared__ int rb[XGR];
+    __shared__ int wcnt[kWavesPerBlock];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t rc = blockIdx.x, r = rc / p.nchunk, skip = (rc % p.nchunk) * XGR;
+    if (t < XGR) rb[t] = -1;
+    int64_t seen = 0;
+    for (int64_t s = 0; s < p.B; s += kBlock) {
+        const int64_t b = s + t;
+        bool m = false;
+        if (b < p.B) {
+            const int64_t rr = p.pos[b * 3 + 1];
+            m = (r < p.nrel) ? (rr == r) : !(rr >= 0 && rr < p.nrel);
+        }
+        const uint64_t bal = __ballot(m);
+        if (lane == 0) wcnt[wave] = __popcll(bal);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) {
+            before += (w < wave) ? wcnt[w] : 0;
+            total += wcnt[w];
+        }
+        if (m) {
+            const int64_t k = seen + before + __popcll(bal & ((1ull << lane) - 1ull)) - skip;
+            if (k >= 0 && k < XGR) rb[k] = (int)b;
+        }
+        seen += total;
+        __syncthreads();
+        if (seen >= skip + XGR) break;  // uniform
+    }
+    const int nrows = (int)min<int64_t>(XGR, seen - skip);
+    if (t < nrows) {
+        float2 x = make_float2(0.f, 0.f);
+        for (int sp = 0; sp < p.xsplit; ++sp) {
+            const float2 v = p.xpart[(rc * p.xsplit + sp) * XGR + t];
+            x = make_float2(x.x + v.x, x.y + v.y);
+        }
         const int64_t b = rb[t];
         p.out[b * p.out_ld] = p.gamma - x.y / sqrtf(x.x);
         if (p.stats) p.stats[b * p.N] = x;
@@ -1657,42 +1738,45 @@ void launch_rows(const TsParams& p, hipStream_t st) {
     if constexpr (OP == TS_FWD) {
         // the forward runs the bf16x3 form (fp32 accuracy, 2.67x the fp32 MFMA rate) when rows take float4s;
         // KGE_TS_F32=1 forces the fp32 MFMA form (A/B runs)
-        static const bool f32 = [] {
-            const char* e = getenv("KGE_TS_F32");
-            return e && e[0] == '1';
-        }();
-        if (use_v4(p) && !f32) {
-            // head-batch rows beyond one 128-row block: 256-row blocks that stage each M_r chunk once for all the
-            // batch row's negatives (KGE_TS_BIG=0 keeps the 128-row form, for A/B runs)
-            static const bool big_off = [] {
-                const char* e = getenv("KGE_TS_BIG");
-                return e && e[0] == '0';
-            }();
-            const char* xg_env = getenv("KGE_TS_X3S");
-            if (p.grouped && !(xg_env && xg_env[0] == '0') && p.d <= kXsMaxDim &&
-                p.nent * p.ent_ld * 4 < (int64_t)kXsOOB && (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB) {
-                // single / tail-batch rows: 64 rows of one relation x all columns per block (ts_fwd_x3g_kernel)
+        // the bf16x3 forms (fp32 accuracy, 2.67x the fp32 MFMA rate) when rows take float4s, operands split once at
+        // staging where the 32-bit buffer offsets reach (form 1: the forms that split each fragment in registers,
+        // for the bitwise / rounding cross-checks)
+        if (use_v4(p)) {
+            const bool xs_ok = p.form == 0 && p.d <= kXsMaxDim && p.nent * p.ent_ld * 4 < (int64_t)kXsOOB &&
+                               (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB;
+            if (p.grouped && xs_ok) {
+                // single / tail-batch rows: 64 rows of one relation per block (ts_fwd_x3g_kernel), all columns, or
+                // with a workspace (xpart) one of xsplit 128-column ranges, then the splits' finish
                 TsParams q = p;
                 q.nchunk = (int)((p.B + XGR - 1) / XGR);
+                const int64_t chunks = (p.nrel + 1) * q.nchunk;
+                if (p.xpart && p.xsplit > 1) {
+                    constexpr int ST = xg_stage(4, 1);
+                    const size_t lds = 2 * (size_t)ST + (size_t)p.d * 4;
+                    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3g_kernel<4, 1>),
+                                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                                 2 * ST + kXsMaxDim * 4) == hipSuccess;
+                    (void)attr;
+                    hipLaunchKernelGGL((ts_fwd_x3g_kernel<4, 1>), dim3((unsigned)(chunks * p.xsplit)), dim3(4 * kWave), lds,
+                                       st, q);
+                    hipLaunchKernelGGL(ts_x3g_finish_kernel, dim3((unsigned)chunks), dim3(kBlock), 0, st, q);
+                    return;
+                }
+                q.xsplit = 0;
                 const size_t lds = 2 * (size_t)kXgStage + (size_t)p.d * 4;
-                static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3g_kernel),
+                static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3g_kernel<8, 2>),
                                                              hipFuncAttributeMaxDynamicSharedMemorySize,
                                                              2 * kXgStage + kXsMaxDim * 4) == hipSuccess;
                 (void)attr;
-                hipLaunchKernelGGL(ts_fwd_x3g_kernel, dim3((unsigned)((p.nrel + 1) * q.nchunk)), dim3(kXThreads), lds, st,
-                                   q);
+                hipLaunchKernelGGL((ts_fwd_x3g_kernel<8, 2>), dim3((unsigned)chunks), dim3(kXThreads), lds, st, q);
                 return;
             }
-            if (!p.grouped && p.N > TBM && p.d <= kTsBigMaxDim && !big_off) {
+            if (!p.grouped && p.N > TBM && p.d <= kTsBigMaxDim) {
+                // head-batch rows beyond one 128-row block: 256-row blocks that stage each M_r chunk once for all
+                // the batch row's negatives
                 TsParams q = p;
                 q.nchunk = (int)((p.N + XBR - 1) / XBR);
-                // operands split once at staging (ts_fwd_x3s_kernel, bitwise the same scores) when its buffer
-                // offsets fit 32 bits; KGE_TS_X3S=0 keeps ts_fwd_x3_kernel (A/B runs; read per call, so a test
-                // can compare the two in one process)
-                const char* xs_env = getenv("KGE_TS_X3S");
-                const bool xs_off = xs_env && xs_env[0] == '0';
-                if (!xs_off && p.d <= kXsMaxDim && p.nent * p.ent_ld * 4 < (int64_t)kXsOOB &&
-                    (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB) {
+                if (xs_ok) {  // operands split once at staging (ts_fwd_x3s_kernel, bitwise ts_fwd_x3_kernel's scores)
                     const size_t lds = 2 * (size_t)kXsStage + (size_t)p.d * 4;
                     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel),
                                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1770,9 +1854,32 @@ int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_l
                          int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
                          int64_t neg_ld, int64_t B, int64_t N, int64_t d, float gamma, float* out, int64_t out_ld,
                          float* stats, void* stream) {
+    return kge_transparse_score_ex(mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d,
+                                   gamma, out, out_ld, stats, nullptr, nullptr, 0, stream);
+}
+
+size_t kge_transparse_score_workspace_size(int mode, int64_t nrel, int64_t B, int64_t d) {
+    if (mode == KGE_HEAD_BATCH || B <= 0 || d <= 0 || nrel < 0) return 0;  // only the grouped rows split columns
+    const int64_t chunks = (nrel + 1) * ((B + XGR - 1) / XGR), xsplit = (d + 127) / 128;
+    return xsplit > 1 ? (size_t)(chunks * xsplit * XGR) * sizeof(float2) : 0;
+}
+
+int kge_transparse_score_ex(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
+                            int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
+                            int64_t neg_ld, int64_t B, int64_t N, int64_t d, float gamma, float* out, int64_t out_ld,
+                            float* stats, const kge_forms* forms, void* workspace, size_t workspace_bytes,
+                            void* stream) {
     TsParams p;
     int rc = fill(p, mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d, gamma);
     if (rc) return rc;
+    p.form = forms ? forms->transparse_form : 0;
+    const size_t need = kge_transparse_score_workspace_size(mode, nrel, B, d);
+    if (workspace && need) {
+        if (workspace_bytes < need) return set_error(KGE_EINVAL, "kge_transparse_score_ex: workspace too small");
+        if ((uintptr_t)workspace & 15) return set_error(KGE_EINVAL, "kge_transparse_score_ex: workspace not 16-B aligned");
+        p.xsplit = (int)((d + 127) / 128);
+        p.xpart = reinterpret_cast<float2*>(workspace);
+    }
     if (B == 0 || (!p.grouped && N == 0)) return 0;
     if (!ent || !rel || !W || !pos || !out || (!p.grouped && !neg))
         return set_error(KGE_EINVAL, "kge_transparse_score: null pointer");

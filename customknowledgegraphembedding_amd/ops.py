@@ -75,8 +75,18 @@ def mode_id(mode) -> int:
 # ----------------------------------------------------------------------------------------------
 # raw launches (no autograd)
 # ----------------------------------------------------------------------------------------------
+def _forms_ptr(forms):
+    """A kge_forms for the _ex entry points (None: the library's choice) -> (ctypes pointer, keep-alive)."""
+    import ctypes
+    if forms is None:
+        return None, None
+    if isinstance(forms, dict):
+        forms = _lib.forms(**forms)
+    return ctypes.addressof(forms), forms
+
+
 def score_indexed_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus=0.0,
-                      out=None):
+                      out=None, forms=None):
     _need_gpu(ent, rel, pos, neg)
     _fp32(ent, "entity_embedding")
     _fp32(rel, "relation_embedding")
@@ -93,10 +103,11 @@ def score_indexed_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range
         N, neg_ld, neg_p = neg.shape[1], neg.stride(0), neg.data_ptr()
     if out is None:
         out = torch.empty((B, N), dtype=torch.float32, device=ent.device)
-    rc = _lib.load().kge_score_indexed(
+    fp, _keep = _forms_ptr(forms)
+    rc = _lib.load().kge_score_indexed_ex(
         fn, mode, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0],
         rel.stride(0), rel_off, pos.data_ptr(), neg_p, neg_ld, B, N, D, float(gamma),
-        float(emb_range), float(modulus), out.data_ptr(), out.stride(0), _stream(ent.device))
+        float(emb_range), float(modulus), out.data_ptr(), out.stride(0), fp, _stream(ent.device))
     check(rc, "kge_score_indexed")
     return out
 
@@ -118,7 +129,7 @@ def score_indexed_bwd_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_r
 
 
 def step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range, modulus=0.0,
-                     temperature=1.0, adversarial=True, neg_scores=None, cand_stats=None):
+                     temperature=1.0, adversarial=True, neg_scores=None, cand_stats=None, forms=None):
     """Both model calls of supervisor.py:17-18 in one launch -> (out_neg [B], out_pos [B],
     neg_scores [B, N], pos_scores [B]). `cand_stats` ([B*N, 2] fp32, optional) receives InterHT's
     per-candidate inverse half-norms for the streaming backward."""
@@ -140,12 +151,13 @@ def step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range,
     out_neg = torch.empty((B,), dtype=torch.float32, device=dev)
     out_pos = torch.empty((B,), dtype=torch.float32, device=dev)
     pos_scores = torch.empty((B,), dtype=torch.float32, device=dev)
-    rc = _lib.load().kge_step_forward(
+    fp, _keep = _forms_ptr(forms)
+    rc = _lib.load().kge_step_forward_ex(
         fn, mode, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0],
         rel.stride(0), rel_off, pos.data_ptr(), neg.data_ptr(), neg.stride(0), B, N, D,
         float(gamma), float(emb_range), float(modulus), float(temperature), int(bool(adversarial)),
         neg_scores.data_ptr(), neg_scores.stride(0), out_neg.data_ptr(), pos_scores.data_ptr(),
-        out_pos.data_ptr(), None if cand_stats is None else cand_stats.data_ptr(), _stream(dev))
+        out_pos.data_ptr(), None if cand_stats is None else cand_stats.data_ptr(), fp, _stream(dev))
     check(rc, "kge_step_forward")
     return out_neg, out_pos, neg_scores, pos_scores
 
@@ -340,10 +352,29 @@ def _want_premul(W, pos, neg, mode):
     return W.shape[0] * 4 <= max(1, rows // 128)
 
 
-def transparse_score_raw(mode, ent, rel, W, mask, pos, neg, gamma, stats=None, out=None, M=None):
+_WS_CACHE = {}
+
+
+def _workspace(device, nbytes):
+    """A scratch buffer of at least nbytes on `device`, reused across calls on torch's current stream (the
+    library's workspaces carry nothing between calls)."""
+    if nbytes <= 0:
+        return None
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    ws = _WS_CACHE.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _WS_CACHE[key] = ws
+    return ws
+
+
+def transparse_score_raw(mode, ent, rel, W, mask, pos, neg, gamma, stats=None, out=None, M=None, forms=None,
+                         split=True):
     """TranSparse raw scores (model.py:226-235): [B, N] for head-batch, [B, 1] for single and
     tail-batch (Q9). `stats` (optional [rows, 2] fp32) receives the per-row backward statistics.
-    `M` (optional) = transparse_premul(W, mask), used instead of forming mask * W in the loads."""
+    `M` (optional) = transparse_premul(W, mask), used instead of forming mask * W in the loads.
+    `split` (single / tail-batch): the projection split over the columns through a workspace
+    (kge_transparse_score_ex), else one block per relation's row chunk."""
     _need_gpu(ent, rel, W, mask, pos, neg)
     for t, n in ((ent, "ent"), (rel, "rel"), (W, "W"), (mask, "mask")):
         _fp32(t, n)
@@ -364,10 +395,16 @@ def transparse_score_raw(mode, ent, rel, W, mask, pos, neg, gamma, stats=None, o
             neg = neg.contiguous()
     if out is None:
         out = torch.empty((B, N), dtype=torch.float32, device=ent.device)
-    rc = _lib.load().kge_transparse_score(
-        m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), W.data_ptr(),
-        mask.data_ptr(), pos.data_ptr(), neg.data_ptr() if head else None, neg.stride(0) if head else 0, B, N, d,
-        float(gamma), out.data_ptr(), out.stride(0), None if stats is None else stats.data_ptr(), _stream(ent.device))
+    lib = _lib.load()
+    nbytes = int(lib.kge_transparse_score_workspace_size(m, rel.shape[0], B, d)) if split else 0
+    ws = _workspace(ent.device, nbytes)
+    fp, _keep = _forms_ptr(forms)
+    Wp, maskp = (M.data_ptr(), None) if M is not None else (W.data_ptr(), mask.data_ptr())
+    rc = lib.kge_transparse_score_ex(
+        m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), Wp, maskp,
+        pos.data_ptr(), neg.data_ptr() if head else None, neg.stride(0) if head else 0, B, N, d, float(gamma),
+        out.data_ptr(), out.stride(0), None if stats is None else stats.data_ptr(), fp,
+        None if ws is None else ws.data_ptr(), nbytes, _stream(ent.device))
     check(rc, "kge_transparse_score")
     return out
 

@@ -40,10 +40,15 @@ def timed(f, n=50, warm=20):
 res = {}
 plain = bench.StepRunner(m, batches, fn, planned=False)
 res["unplanned"] = timed(plain)
+# one mode only (the same kernel object every step) against alternating modes (the default above): what a
+# mode switch costs per step
+res["unplanned_head_only"] = timed(lambda i: plain(i, 0))
+res["unplanned_tail_only"] = timed(lambda i: plain(i, 1))
 for at in ("tail", "rows"):
     os.environ["KGE_PLAN_AT"] = at
     r = bench.StepRunner(m, batches, fn, planned=True)
     res["planned_" + at] = timed(r)
+    res["planned_" + at + "_head_only"] = timed(lambda i: r(i, 0))
 os.environ.pop("KGE_PLAN_AT")
 sp = bench.StepRunner(m, batches, fn, planned=True).planner
 

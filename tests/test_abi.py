@@ -141,16 +141,14 @@ def test_sharded_exchange_rejects_bad_arguments():
     assert lib.kge_shard_gather_queries(d, 10, 4, 0, d, 8, 3, 0, 4, 2, 0, 0, 0, d, d, d, d, d, None) == -22
 
 
-def test_step_forward_order_choice_and_override(monkeypatch):
-    """kge_step_forward_order (host-only): the tile form (2) for N >= 128, one launch (0) below; KGE_STEP_ORDER
-    switches it per call (read at every call), and tables past the sort keys' range take the one-launch form."""
+def test_step_forward_order_choice_reads_no_environment(monkeypatch):
+    """kge_step_forward_order (host-only): the tile form (2) for N >= 128, one launch (0) below, and tables past
+    the sort keys' range take the one-launch form. The library reads no environment: a form is chosen only
+    through the _ex entry points' kge_forms."""
     lib = kge.load()
-    monkeypatch.delenv("KGE_STEP_ORDER", raising=False)
-    assert lib.kge_step_forward_order(40943, 256) == 2    # C2
+    for name in ("row", "xcd", "tile"):
+        monkeypatch.setenv("KGE_STEP_ORDER", name)  # the old A/B knob: ignored
+        assert lib.kge_step_forward_order(40943, 256) == 2    # C2
     assert lib.kge_step_forward_order(123182, 1024) == 2  # C4
     assert lib.kge_step_forward_order(40943, 127) == 0
-    for name, code in (("row", 0), ("xcd", 1), ("tile", 2)):
-        monkeypatch.setenv("KGE_STEP_ORDER", name)
-        assert lib.kge_step_forward_order(40943, 256) == code
-    monkeypatch.setenv("KGE_STEP_ORDER", "tile")
     assert lib.kge_step_forward_order(8 << 25, 256) == 0

@@ -119,30 +119,16 @@ def test_c2_xcd_phases_bitwise():
     pos, neg = pos.to(DEV), neg.to(DEV)
     ent, rel = m.entity_embedding.detach(), m.relation_embedding.detach()
     fn = FN_IDS[name]
-    old = os.environ.get("KGE_XCD_PHASES")
-    old_order = os.environ.get("KGE_STEP_ORDER")
-    os.environ["KGE_STEP_ORDER"] = "xcd"  # the phases belong to the XCD-sliced form (the default is the tile form)
-    try:
-        for mode in (0, 1):
-            outs = []
-            for ph in ("1", "2", "3", "4", "8"):
-                os.environ["KGE_XCD_PHASES"] = ph
-                outs.append(ops.step_forward_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f,
-                                                 m._range_f)[:3])
-            want_s = ops.score_indexed_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
-            torch.cuda.synchronize()
-            for o in outs:
-                assert all(torch.equal(x, y) for x, y in zip(o, outs[0])), mode
-            assert torch.equal(outs[0][2], want_s), mode
-    finally:
-        if old is None:
-            os.environ.pop("KGE_XCD_PHASES", None)
-        else:
-            os.environ["KGE_XCD_PHASES"] = old
-        if old_order is None:
-            os.environ.pop("KGE_STEP_ORDER", None)
-        else:
-            os.environ["KGE_STEP_ORDER"] = old_order
+    for mode in (0, 1):
+        outs = []
+        for ph in (1, 2, 3, 4, 8):  # the phases belong to the XCD-sliced form (the default is the tile form)
+            outs.append(ops.step_forward_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f,
+                                             forms=dict(step_order="xcd", xcd_phases=ph))[:3])
+        want_s = ops.score_indexed_raw(fn, mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
+        torch.cuda.synchronize()
+        for o in outs:
+            assert all(torch.equal(x, y) for x, y in zip(o, outs[0])), mode
+        assert torch.equal(outs[0][2], want_s), mode
 
 
 def test_c3_fb15k237_rotate_full_size():

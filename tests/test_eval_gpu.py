@@ -1,5 +1,7 @@
 """GPU tests of the all-entity evaluation path (upstream test_step): the fp32 MFMA GEMM, exact
 filtered ranks vs the oracle's argsort-based restatement, and the metrics."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -164,10 +166,11 @@ def test_gemm_split_once_is_bitwise_the_register_split_kernel(monkeypatch, M, N,
     lib = _lib.load()
     st = torch.cuda.current_stream().cuda_stream
     out = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("KGE_GEMM_X3S", flag)
+    for form in (1, 0):  # 1: split per fragment in registers (gemm_nt_f32x3_kernel), 0: split once (x3s)
         C = torch.full((M, N + 3), -7.0, device=DEV)
-        assert lib.kge_gemm_nt_bf16x3(A.data_ptr(), lda, Bm.data_ptr(), K, C.data_ptr(), N + 3, M, N, K, st) == 0
+        f = _lib.forms(gemm_form=form)
+        assert lib.kge_gemm_nt_bf16x3_ex(A.data_ptr(), lda, Bm.data_ptr(), K, C.data_ptr(), N + 3, M, N, K,
+                                         ctypes.addressof(f), st) == 0
         torch.cuda.synchronize()
         out.append(C.cpu())
     assert torch.equal(out[0], out[1])

@@ -1,12 +1,9 @@
-"""kge_step_forward's row-group x XCD-slice tile form (step_fwd_tile_kernel, KGE_STEP_ORDER=tile, the default
+"""kge_step_forward's row-group x XCD-slice tile form (step_fwd_tile_kernel, forms step_order=tile, the default
 for N >= 128): every candidate and positive goes through the same cand_score as the batch-row-major form
 (step_fwd_kernel) and the XCD-sliced form (step_fwd_xcd_kernel), so all four outputs must be BITWISE equal
 across the three orders, for every score function, both negative modes, any rows-per-block cap, ragged
 batches, out-of-range ids, skewed id distributions and the full C2 size (reference: model.py:114-205,
 supervisor.py:17-18). The fp64 oracle check of the default (tile) order is in test_configs_gpu.py."""
-import contextlib
-import os
-
 import pytest
 import torch
 
@@ -19,35 +16,19 @@ DEV = "cuda"
 FNS = ["TransE", "DistMult", "ComplEx", "RotatE", "pRotatE", "InterHT"]
 
 
-@contextlib.contextmanager
-def _env(**kv):
-    old = {k: os.environ.get(k) for k in kv}
-    try:
-        for k, v in kv.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = str(v)
-        yield
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
 def _model(name, E, R, d, seed=0):
     return kge.TFKGEModel(name, E, R, d, 12.0, double_entity_embedding=name in ("ComplEx", "RotatE", "InterHT"),
                           double_relation_embedding=name == "ComplEx", triple_relation_embedding=name == "InterHT",
                           device=DEV, seed=seed)
 
 
-def _run(m, mode, pos, neg, order, rows=None):
-    with _env(KGE_STEP_ORDER=order, KGE_TILE_ROWS=rows):
-        out = ops.step_forward_raw(FN_IDS[m.model_name], mode, m.entity_embedding.detach(),
-                                   m.relation_embedding.detach(), m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f,
-                                   modulus=float(m.modulus.detach().reshape(-1)[0]) if m.model_name == "pRotatE" else 0.0)
+def _run(m, mode, pos, neg, order, rows=None, q2slots=None):
+    """kge_step_forward_ex with an explicit form (kge_forms: the order, the tile kernel's row cap and InterHT
+    relation slots)."""
+    out = ops.step_forward_raw(FN_IDS[m.model_name], mode, m.entity_embedding.detach(),
+                               m.relation_embedding.detach(), m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f,
+                               modulus=float(m.modulus.detach().reshape(-1)[0]) if m.model_name == "pRotatE" else 0.0,
+                               forms=dict(step_order=order, tile_rows=rows, tile_q2slots=q2slots))
     torch.cuda.synchronize()
     return out
 
@@ -59,11 +40,8 @@ def _same(a, b):
 
 def test_order_query_reports_tile_for_large_n():
     lib = kge.load()
-    with _env(KGE_STEP_ORDER=None):
-        assert lib.kge_step_forward_order(40943, 256) == 2
-        assert lib.kge_step_forward_order(40943, 64) == 0
-    with _env(KGE_STEP_ORDER="xcd"):
-        assert lib.kge_step_forward_order(40943, 256) == 1
+    assert lib.kge_step_forward_order(40943, 256) == 2
+    assert lib.kge_step_forward_order(40943, 64) == 0
 
 
 @pytest.mark.parametrize("name", FNS)
@@ -103,10 +81,9 @@ def test_score_indexed_tile_bitwise(name, mode):
     mod = float(m.modulus.detach().reshape(-1)[0]) if name == "pRotatE" else 0.0
     outs = []
     for order in ("row", "tile", "xcd"):
-        with _env(KGE_STEP_ORDER=order):
-            outs.append(ops.score_indexed_raw(FN_IDS[name], mode, m.entity_embedding.detach(),
-                                              m.relation_embedding.detach(), m._rel_off, pos, neg, m._D, m._gamma_f,
-                                              m._range_f, mod))
+        outs.append(ops.score_indexed_raw(FN_IDS[name], mode, m.entity_embedding.detach(),
+                                          m.relation_embedding.detach(), m._rel_off, pos, neg, m._D, m._gamma_f,
+                                          m._range_f, mod, forms=dict(step_order=order)))
         torch.cuda.synchronize()
     assert _same([outs[1]], [outs[0]]) and _same([outs[2]], [outs[0]])
 
@@ -139,8 +116,7 @@ def test_tile_interht_relation_slots(mode):
                            torch.randint(0, E, (B,), generator=g)], 1).to(DEV)
         neg = torch.randint(0, E, (B, N), generator=g).to(DEV)
         want = _run(m, mode, pos, neg, "row")
-        with _env(KGE_TILE_Q2SLOTS=slots):
-            assert _same(_run(m, mode, pos, neg, "tile"), want), (R, B, slots)
+        assert _same(_run(m, mode, pos, neg, "tile", q2slots=slots), want), (R, B, slots)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -175,16 +151,16 @@ def test_tile_step_forward_graph_capture_replays_bitwise(mode):
         sc = ops.score_indexed_raw(FN_IDS[name], mode, ent, rel, m._rel_off, pos, neg, m._D, m._gamma_f, m._range_f)
         return list(fwd) + [sc]
 
-    with _env(KGE_STEP_ORDER="tile"):
-        want = call()
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            call()  # warm-up on a side stream before capture, as torch.cuda.graph expects
-        torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            got = call()
-        graph.replay()
-        torch.cuda.synchronize()
+    assert kge.load().kge_step_forward_order(E, N) == 2  # the tile form, the default at N >= 128
+    want = call()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        call()  # warm-up on a side stream before capture, as torch.cuda.graph expects
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        got = call()
+    graph.replay()
+    torch.cuda.synchronize()
     assert _same(got, want)

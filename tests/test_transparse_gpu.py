@@ -191,10 +191,10 @@ def test_split_once_forward_is_bitwise_the_register_split_one(monkeypatch, d, N,
     ed, rd, Wd, md = ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV)
     M = ops.transparse_premul(Wd, md) if premul else None
     outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("KGE_TS_X3S", flag)
+    for form in (1, 0):  # 1: split per fragment in registers (ts_fwd_x3_kernel), 0: split once (ts_fwd_x3s_kernel)
         st = torch.empty((B * N, 2), dtype=torch.float32, device=DEV)
-        s = ops.transparse_score_raw(0, ed, rd, Wd, md, pos.to(DEV), neg.to(DEV), gamma, stats=st, M=M)
+        s = ops.transparse_score_raw(0, ed, rd, Wd, md, pos.to(DEV), neg.to(DEV), gamma, stats=st, M=M,
+                                     forms=dict(transparse_form=form))
         torch.cuda.synchronize()
         outs.append((s.cpu(), st.cpu()))
     assert np.array_equal(outs[0][0].numpy(), outs[1][0].numpy(), equal_nan=True)
@@ -210,9 +210,11 @@ def test_split_once_forward_is_bitwise_the_register_split_one(monkeypatch, d, N,
                                           (516, 90, 4, False)])
 @pytest.mark.parametrize("mode", [1, 3])
 def test_grouped_forward_all_columns_per_block(monkeypatch, d, B, R, premul, mode):
-    """Single / tail-batch rows (one relation's rows per block, all columns at once: ts_fwd_x3g_kernel): within
-    1e-4 of the fp64 oracle, within fp32 rounding of ts_rows_kernel's column order (KGE_TS_X3S=0), with rows of
-    out-of-range relations and heads (NaN), more than 64 rows per relation and d past one 512-column pass."""
+    """Single / tail-batch rows: one relation's row chunk per block over all columns (ts_fwd_x3g_kernel<8, 2>),
+    and split over 128-column ranges through a workspace (ts_fwd_x3g_kernel<4, 1> + the ordered finish):
+    within 1e-4 of the fp64 oracle, within fp32 rounding of ts_rows_kernel's column order (form 1) and of each
+    other, bitwise run to run, with rows of out-of-range relations and heads (NaN), more than 64 rows per
+    relation and d past one 512-column pass."""
     E, gamma = 400, 12.0
     ent, rel, W, mask = _tables(E, R, d, seed=5)
     pos, neg = _batch(E, R, B, 3, seed=11)
@@ -221,17 +223,22 @@ def test_grouped_forward_all_columns_per_block(monkeypatch, d, B, R, premul, mod
     ed, rd, Wd, md = ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV)
     M = ops.transparse_premul(Wd, md) if premul else None
     got = {}
-    for flag in ("0", "1"):
-        monkeypatch.setenv("KGE_TS_X3S", flag)
+    for key, form, split in (("old", 1, False), ("one", 0, False), ("split", 0, True), ("split2", 0, True)):
         st = torch.empty((B, 2), dtype=torch.float32, device=DEV)
-        s = ops.transparse_score_raw(mode, ed, rd, Wd, md, pos.to(DEV), neg.to(DEV), gamma, stats=st, M=M)
+        s = ops.transparse_score_raw(mode, ed, rd, Wd, md, pos.to(DEV), neg.to(DEV), gamma, stats=st, M=M,
+                                     forms=dict(transparse_form=form), split=split)
         torch.cuda.synchronize()
-        got[flag] = (s.cpu().numpy(), st.cpu().numpy())
+        got[key] = (s.cpu().numpy(), st.cpu().numpy())
     bad = np.zeros(B, dtype=bool)
     bad[[3, 5]] = True
-    new, old = got["1"][0][:, 0], got["0"][0][:, 0]
-    assert np.isnan(new[bad]).all() and np.isnan(old[bad]).all()
-    assert np.abs(new[~bad] - old[~bad]).max() <= 1e-5 * max(1.0, np.abs(old[~bad]).max())
+    old = got["old"][0][:, 0]
+    assert np.array_equal(got["split"][0], got["split2"][0], equal_nan=True)  # deterministic
+    assert np.array_equal(got["split"][1], got["split2"][1], equal_nan=True)
+    for key in ("one", "split"):
+        new = got[key][0][:, 0]
+        assert np.isnan(new[bad]).all() and np.isnan(old[bad]).all()
+        assert np.abs(new[~bad] - old[~bad]).max() <= 1e-5 * max(1.0, np.abs(old[~bad]).max()), key
+    new = got["split"][0][:, 0]
     ok_pos = pos.clone()
     ok_pos[3, 1], ok_pos[5, 0] = 0, 0
     ref, _ = _oracle(ent, rel, W, mask, ok_pos, neg, mode, gamma)

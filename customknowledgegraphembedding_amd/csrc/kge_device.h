@@ -65,38 +65,8 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
 constexpr int kAuxNT = 2, kAuxSC1 = 16;
 // cache policy of bwd_ent_stream_kernel's streamed table row and Adam moments: nt loads AND nt
 // stores (either alone measured no faster; together the C2 train step drops 0.636 -> 0.606 ms,
-// scripts/ab_cache_policy.sh). Overridable with -D for A/B builds.
-#ifndef KGE_ENT_LD_AUX
-#define KGE_ENT_LD_AUX kAuxNT
-#endif
-#ifndef KGE_ENT_ST_AUX
-#define KGE_ENT_ST_AUX kAuxNT
-#endif
-// bwd_ent_stream_kernel: a small bucket's codes requested ahead of the row, the row's norms taken
-// after the first events' loads are issued (0: the earlier order, for A/B builds)
-#ifndef KGE_ENT_EARLY
-#define KGE_ENT_EARLY 1
-#endif
-#ifndef KGE_ENT_UMAX
-#define KGE_ENT_UMAX 2
-#endif
-#ifndef KGE_ENT_WPE
-#define KGE_ENT_WPE 0
-#endif
-#ifndef KGE_ENT_LATE_MV
-#define KGE_ENT_LATE_MV 1
-#endif
-// step_fwd_grad_kernel: InterHT's per-element Jacobian signs kept from the score pass, under a 2-waves/SIMD
-// bound (256 VGPRs, 36 B/lane spilled; 191 -> 175 us at C2 same box). 0: recomputed, 229 VGPRs
-#ifndef KGE_FG_KEEPSGN
-#define KGE_FG_KEEPSGN 1
-#endif
-// step_fwd_grad_kernel's query pass: gradient weights on the hardware exp / log / rcp, InterHT's Jacobian
-// sums on packed fp32 pairs with the sign recomputed and RotatE's on the hardware rsq (KGE_FG_FAST = 1),
-// or the libm-accurate weights and scalar sums with the score pass's kept signs (0, the round-2 form)
-#ifndef KGE_FG_FAST
-#define KGE_FG_FAST 1
-#endif
+// scripts/ab_cache_policy.sh)
+constexpr int kEntLdAux = kAuxNT, kEntStAux = kAuxNT;
 
 template <int V, int AUX = 0>
 __device__ __forceinline__ vecf<V> bload(rsrc_t r, uint32_t off) {
@@ -904,9 +874,6 @@ step_fwd_xcd_kernel(ScoreParams p) {
 // bucket counts / cursors [kTileBuckets], the item count, the sorted list [R (N + 1)] of (row << 16 | column)
 // (column N: the row's positive).
 // ---------------------------------------------------------------------------------------------
-#ifndef KGE_TILE_EXP
-#define KGE_TILE_EXP 0  // A/B experiments on the setup only (scripts/gpu_r04_l.sh); 0 in every shipped build
-#endif
 template <int V, int G>
 struct TileQueryIH {  // InterHT: q0, q1 from LDS, the relation third in registers
     LdsOperand<V> q0, q1;
@@ -1290,11 +1257,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     // once (C4 tail-batch 94.5 -> 88 us); 16 at fewer waves, where the 17th slot measured ~1 us slower at C3
     constexpr int TPI = NWV >= 16 ? 17 : 16;
     int wbk[TPI], wcd[TPI];
-#if KGE_TILE_EXP == 1
-    const bool in_regs = false;  // experiment: the walk made after the query build (the two-pass form)
-#else
     const bool in_regs = !pl && nf <= (int64_t)TPI * NT;  // block-uniform
-#endif
     // (their loads are issued here, before the query build, so both latencies overlap)
     if (in_regs) {
 #pragma unroll
@@ -1313,9 +1276,6 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         ri = rrow[r];  // the raw relation id until put() replaces it with the checked one
         bool qok = qi >= 0 && qi < p.q_rows;
         rok = ri >= 0 && ri < p.r_rows;
-#if KGE_TILE_EXP == 2
-        qok = rok = false;  // experiment: the query rows read as zeros (no memory traffic)
-#endif
         q.build(p.qent + (qok ? qi : 0) * p.q_ld, qok, p.rel + (rok ? ri : 0) * p.r_ld + p.r_off, rok, p.D, lane, p);
     };
     auto put = [&](int r, const Query<FN, CH, V, G>& q, int64_t ri, bool rok) {
@@ -1429,7 +1389,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     const int cnt = pl ? pcnt : cntp[0];
 
     if (p.tile_dry) return;
-    // 3. the sweep: wave w takes items w, w + NWV, w + 2 NWV, ...; with KGE_TILE_DEPTH = 2 the next item's
+    // 3. the sweep: wave w takes items w, w + NWV, w + 2 NWV, ...; the next item's
     // candidate row (and InterHT's relation third) is in flight while this one is scored
     struct Item {
         Cand<FN, V, G> c;
@@ -1485,14 +1445,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             }
         };
         float my_score = 0.f;
-        if constexpr (KGE_TILE_DEPTH == 1) {
-            for (int j = 0; j < nc; ++j) {
-                Item it;
-                load(it, j);
-                const float s = score(it, j);
-                if (lane == j) my_score = s;
-            }
-        } else {
+        {
             Item x0, x1;
             load(x0, 0);
             for (int j = 0; j < nc; j += 2) {
@@ -1594,14 +1547,11 @@ score_sharded_xcd_kernel(ScoreParams p) {
 // step_fwd_xcd_kernel, every gather of a shard row is issued by one XCD and each XCD's waves sweep their
 // slice together (3.9 MB at the north star's 8-way YAGO3-10 split: the XCD's L2 holds it). A wave reads its
 // ~N / 64 entries with one load per 64 (no walk over the row's ids), sorts them by row, gathers and scores
-// them KGE_SHARD_DEPTH rows deep and writes each score at the row's compact run start + its rank: the send
+// them two rows deep and writes each score at the row's compact run start + its rank: the send
 // block of the score all-to-all. Head-batch positives: the exchanged block holds the TAIL (the negatives'
 // query entity), so the wave of the head's slice on the head's owner scores query (h, r), built from its
 // shard row, against the tail row (the single-mode formula, bitwise every other positive's).
 // ---------------------------------------------------------------------------------------------
-#ifndef KGE_SHARD_DEPTH
-#define KGE_SHARD_DEPTH 2
-#endif
 template <int FN, bool CH, int V, int G>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock), amdgpu_waves_per_eu(G <= 4 ? 4 : 1))) void
 shard_bucket_kernel(ScoreParams p) {
@@ -1637,7 +1587,7 @@ shard_bucket_kernel(ScoreParams p) {
                 const int src = key & (kWave - 1);
                 const int row = lane_pull(e.x, src), k = lane_pull(e.y, src);
                 float2 st;
-                const float sc = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, (FN == KGE_INTERHT ? 1 : KGE_SHARD_DEPTH)>(
+                const float sc = score_lanes<FN, CH, V, G, false, std::decay_t<decltype(qq)>, (FN == KGE_INTERHT ? 1 : 2)>(
                     p, qq, (int64_t)row + p.c_base, cnt, lane, st);
                 if (lane < cnt) p.out[off + k] = sc;
             }
@@ -1927,19 +1877,13 @@ __device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcp
 __device__ __forceinline__ float flog_sigmoid(float x) { return fminf(x, 0.f) - __logf(1.f + __expf(-fabsf(x))); }
 
 // (xr, xi) / |(xr, xi)| and 0 at (and, fast form, within FLT_MIN of) the origin: the derivative of RotatE's
-// modulus, in every gradient path. KGE_FG_FAST: one hardware reciprocal square root for both components
+// modulus, in every gradient path. One hardware reciprocal square root for both components
 // instead of a square root and two IEEE divisions (the RotatE fused forward 340 -> 193 us at C3).
 __device__ __forceinline__ void rot_unit(float xr, float xi, float& fr, float& fi) {
-#if KGE_FG_FAST
     const float s2 = xr * xr + xi * xi;
     const float im = s2 >= 1.17549435e-38f ? __builtin_amdgcn_rsqf(s2) : 0.f;
     fr = xr * im;
     fi = xi * im;
-#else
-    const float m = sqrtf(xr * xr + xi * xi);
-    fr = (m > 0.f) ? xr / m : 0.f;
-    fi = (m > 0.f) ? xi / m : 0.f;
-#endif
 }
 
 template <int FN, bool CH, int V, bool TWO>
@@ -1993,23 +1937,8 @@ __device__ __forceinline__ void group_jac(const vecf<V>& ca, const vecf<V>& cb, 
     }
 }
 
-#if KGE_FG_FAST
-#undef KGE_FG_KEEPSGN
-#define KGE_FG_KEEPSGN 0
-#endif
-#ifndef KGE_FG_WPE
-#define KGE_FG_WPE 2
-#endif
-#ifndef KGE_FG_DEPTH
-#define KGE_FG_DEPTH 2
-#endif
-#if KGE_FG_KEEPSGN || KGE_FG_FAST
-#define KGE_FG_ATTR __attribute__((amdgpu_waves_per_eu(KGE_FG_WPE)))
-#else
-#define KGE_FG_ATTR
-#endif
 template <int FN, bool CH, int V, int G, int RED>
-__global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(ScoreParams p) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void step_fwd_grad_kernel(ScoreParams p) {
     static_assert(FN != KGE_PROTATE, "pRotatE's modulus gradient is not part of the fused query pass");
     constexpr bool TWO = RED == 2;
     constexpr int W = G * kWave;  // vecf<V> per operand per wave image
@@ -2049,15 +1978,9 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
         // one candidate's contribution (s is wave-uniform)
         auto accumulate = [&](const Cand<FN, V, G>& c, const LdsQuery<V>& q, float s, float2 nst,
                               const vecf<V>* nsg) {
-#if KGE_FG_FAST
             auto xexp = [](float x) { return fexp(x); };
             auto xsig = [](float x) { return fsigmoid(x); };
             auto xlogsig = [](float x) { return flog_sigmoid(x); };
-#else
-            auto xexp = [](float x) { return expf(x); };
-            auto xsig = [](float x) { return sigmoidf(x); };
-            auto xlogsig = [](float x) { return log_sigmoid(x); };
-#endif
             float wa, wb = 0.f;
             if constexpr (RED == 0) {
                 wa = -xsig(s);
@@ -2092,7 +2015,6 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
                     wb = e;
                 }
             }
-#if KGE_FG_FAST
             if constexpr (FN == KGE_INTERHT && V % 2 == 0) {
 #pragma unroll
                 for (int k = 0; k < G; ++k)
@@ -2100,7 +2022,6 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
                                              a1[k], a2[k], b0[k], b1[k], b2[k]);
                 return;
             }
-#endif
 #pragma unroll
             for (int k = 0; k < G; ++k)
                 group_jac<FN, CH, V, TWO>(c.ca[k], c.cb[k], q.q0[k], q.q1[k], q.q2[k], (lane + k * kWave) < DV, nst.x,
@@ -2139,33 +2060,13 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
                 asm volatile("" : "+v"(li));
                 const LdsQuery<V> q{{qimg[0], li}, {qimg[1], li}, {qimg[2], li}};
                 float2 nst = make_float2(0.f, 0.f);
-#if KGE_FG_KEEPSGN
-                // InterHT: the score pass leaves each element's -sgn for the Jacobian sums (16 VGPRs
-                // instead of recomputing the element's term)
-                vecf<V> nsg[G];
-                const float s = cand_score<FN, CH, V, G>(c, q, p, &nst, FN == KGE_INTERHT ? nsg : nullptr);
-#else
                 const float s = cand_score<FN, CH, V, G>(c, q, p, &nst);
-#endif
                 if (lane == jj) my_score = s;
                 // opaque copies of the half-norms: the gradient recomputes the candidate's terms
                 // instead of keeping the score's per-element values alive across the reductions
                 asm volatile("" : "+v"(nst.x), "+v"(nst.y));
-#if KGE_FG_KEEPSGN
-                accumulate(c, q, s, nst, FN == KGE_INTERHT ? nsg : nullptr);
-#else
                 accumulate(c, q, s, nst, nullptr);
-#endif
             };
-#if KGE_FG_DEPTH == 1
-            // one row in registers at a time (more waves per SIMD hide the gather latency instead)
-            for (int j = 0; j < nc; ++j) {
-                x0.load(cand_row(p, readlane64(my_id, j), ok0), ok0, p.D, lane);
-                one(x0, j);
-            }
-            (void)x1;
-            (void)ok1;
-#else
             // software pipeline (as score_run): row j + 1 is in flight while row j is reduced
             x0.load(cand_row(p, readlane64(my_id, 0), ok0), ok0, p.D, lane);
             int j = 0;
@@ -2182,7 +2083,6 @@ __global__ __launch_bounds__(kBlock) KGE_FG_ATTR void step_fwd_grad_kernel(Score
             } else {
                 one(x0, j);
             }
-#endif
             if (lane < nc) p.out[b * p.out_ld + c0 + src] = my_score;
         }
     }
@@ -3292,17 +3192,12 @@ constexpr int kEntSortMax = 2048;
 // the relation row, is read from the relation table instead: it stays in L2)
 constexpr int ent_nq(int fn) { return (fn == KGE_COMPLEX || fn == KGE_ROTATE || fn == KGE_INTERHT) ? 2 : 1; }
 
-#if KGE_ENT_WPE > 0
-#define KGE_ENT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(KGE_ENT_WPE)))
-#else
-#define KGE_ENT_WPE_ATTR
-#endif
 template <int FN, bool CH, int V, int G>
-__global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel(ScoreParams p) {
+__global__ __launch_bounds__(kBlock) void bwd_ent_stream_kernel(ScoreParams p) {
     static_assert(G % kWavesPerBlock == 0, "the streaming phase 2 needs a multiple of 4 groups per lane");
     constexpr int GW = G / kWavesPerBlock;
     constexpr int U0 = GW == 1 ? 4 : (GW == 2 ? 2 : 1);  // events whose query slices are in flight
-    constexpr int U = U0 < KGE_ENT_UMAX ? U0 : KGE_ENT_UMAX;
+    constexpr int U = U0 < 2 ? U0 : 2;  // 2 events in flight (4: 398-400 us against 369-374 at C2, 93 VGPRs)
     constexpr bool SPLIT = is_split(FN);
     constexpr int NH = SPLIT ? 2 : 1;
     constexpr int NQ = ent_nq(FN);
@@ -3322,19 +3217,17 @@ __global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel
         goffs[gg] = goff<V>(lane, k);
         gin[gg] = (lane + k * kWave) < DV;
     }
-    // streamed (read-once) operands: the table row and its Adam moments, nontemporal (KGE_ENT_LD_AUX)
-    auto sload = [&](rsrc_t r, uint32_t off) { return bload<V, KGE_ENT_LD_AUX>(r, off); };
+    // streamed (read-once) operands: the table row and its Adam moments, nontemporal (kEntLdAux)
+    auto sload = [&](rsrc_t r, uint32_t off) { return bload<V, kEntLdAux>(r, off); };
     // bucket bounds and codes are validated against the event count: a corrupted bucket table (a
     // workspace that was not zero-filled) gives wrong gradients, never an out-of-range access
     const int ntot = (int)(p.Bn * p.Nn + 3 * p.Bn);
     const int lo = min(max(p.ev_off[e], 0), ntot), hi = min(max(p.ev_off[e + 1], lo), ntot);
     const int n = hi - lo;
-#if KGE_ENT_EARLY
     // a small bucket's codes are requested before the row and its moments: the vector-memory counter
     // retires in order, so the code -> relation index -> event-slice chain then runs under the row's
     // HBM latency instead of after it
     int code0 = (n <= kWave && lane < n) ? p.ev_code[lo + lane] : INT32_MAX;
-#endif
     // the row slice, and the Adam moments requested up front so their latency overlaps the walk
     vecf<V> ca[GW], cb[GW], mm[NH][GW], vv[NH][GW];
     {
@@ -3361,9 +3254,6 @@ __global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel
             }
         }
     };
-#if !KGE_ENT_LATE_MV
-    load_mv();
-#endif
     vecf<V> sa[GW], sb[GW], ra[GW], rb[GW];  // candidate terms (normalised space), row events
 #pragma unroll
     for (int gg = 0; gg < GW; ++gg) sa[gg] = sb[gg] = ra[gg] = rb[gg] = vzero<V>();
@@ -3386,9 +3276,6 @@ __global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel
                 ib = rsqrt_f(s.y);
             }
         };
-#if !KGE_ENT_EARLY
-        norms();
-#endif
         // one event: its slice of the slot's stored query (candidate event) or of the slot's
         // query-entity gradient (row event)
         auto load_ev = [&](int code, vecf<V>(&x0)[GW], vecf<V>(&x1)[GW], vecf<V>(&x2)[GW]) {
@@ -3444,11 +3331,7 @@ __global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel
             }
         };
         if (n <= kWave) {
-#if KGE_ENT_EARLY
             int code = code0;
-#else
-            int code = lane < n ? p.ev_code[lo + lane] : INT32_MAX;
-#endif
             if ((unsigned)code >= (unsigned)ntot) code = INT32_MAX;  // never index with a stray code
             const int nv = __popcll(__ballot(code != INT32_MAX));
             code = wave_sort_asc(code, lane);
@@ -3457,18 +3340,14 @@ __global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (j + u < nv) load_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
-#if KGE_ENT_EARLY
                 // the norms after the first events' loads are issued (nv is block-uniform)
                 if (j == 0) norms();
-#endif
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (j + u < nv) apply_ev(__builtin_amdgcn_readlane(code, j + u), x0[u], x1[u], x2[u]);
             }
         } else if (n <= kEntSortMax) {
-#if KGE_ENT_EARLY
             norms();
-#endif
             // large bucket (a hub entity, or a small table): one block-wide bitonic sort of its codes in LDS,
             // then the same ordered walk, U events in flight (n is block-uniform: every barrier is reached)
             int np2 = 2 * kWave;
@@ -3506,9 +3385,7 @@ __global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel
                     if (j + u < nv) apply_ev(srt[j + u], x0[u], x1[u], x2[u]);
             }
         } else {
-#if KGE_ENT_EARLY
             norms();
-#endif
             // larger still: extract codes in ascending order (O(n^2 / 64))
             int last = -1;
             for (int it = 0; it < n; ++it) {
@@ -3525,9 +3402,7 @@ __global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel
                 last = m;
             }
         }
-#if KGE_ENT_LATE_MV
         load_mv();  // the moments' latency overlaps the row's closing dot
-#endif
         if constexpr (FN == KGE_INTERHT) {
             // any_cand is block-uniform (every wave walks the same events)
             if (any_cand) {
@@ -3557,10 +3432,8 @@ __global__ __launch_bounds__(kBlock) KGE_ENT_WPE_ATTR void bwd_ent_stream_kernel
                 sb[gg].a[i] += rb[gg].a[i];
             }
     }
-#if KGE_ENT_LATE_MV
     if (n <= 0) load_mv();
-#endif
-    auto sstore = [&](rsrc_t r, uint32_t off, const vecf<V>& v) { bstore<V, KGE_ENT_ST_AUX>(r, off, v); };
+    auto sstore = [&](rsrc_t r, uint32_t off, const vecf<V>& v) { bstore<V, kEntStAux>(r, off, v); };
     if (p.adam.on) {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {

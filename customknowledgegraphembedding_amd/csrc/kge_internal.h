@@ -38,9 +38,6 @@ enum Kind {
                                // entity-sorted sweep per block (queries in LDS)
     KIND_SCORE_TILE = 20,      // kge_score_indexed in the same order (no positives)
 };
-#ifndef KGE_TILE_DEPTH
-#define KGE_TILE_DEPTH 2
-#endif
 constexpr int kTileBuckets = 256;  // entity buckets of a slice (the block's counting sort)
 constexpr int kTileMaxRows = 16;
 constexpr int kTileLdsMax = 160 * 1024;

@@ -103,13 +103,11 @@ __global__ __launch_bounds__(kBlock) void shard_fwd_grad_kernel(ScoreParams p) {
     float mrun = -INFINITY, Z = 0.f, Ln = 0.f;
     {
         auto accumulate = [&](const Cand<FN, V, G>& c, const LdsQuery<V>& q, float s, float2 nst) {
-#if KGE_FG_FAST
             // the hardware exp / log / rcp, as the single-GPU fused forward (per candidate these were most of
             // a DistMult wave's VALU work); the merged stats stay within fp32 rounding of the libm ones
             auto expf = [](float x) { return fexp(x); };
             auto sigmoidf = [](float x) { return fsigmoid(x); };
             auto log_sigmoid = [](float x) { return flog_sigmoid(x); };
-#endif
             float wa, wb = 0.f;
             if constexpr (RED == 0) {
                 wa = -sigmoidf(s);

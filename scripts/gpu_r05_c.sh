@@ -15,5 +15,7 @@ done
 cat $O/probe.json
 timeout -k 10 300 python -u bench.py --workload c6 --steps 20 --warmup 3 > $O/bench_c6.json 2> $O/bench_c6.err || { tail -20 $O/bench_c6.err; exit 1; }
 cat $O/bench_c6.json
+timeout -k 10 200 python -u scripts/stagger_probe.py > $O/stagger.json 2>> $O/probe.err || exit 1
+cat $O/stagger.json
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- python3 $GRAFT_REPO_ROOT/scripts/plan_probe.py c2 > $GRAFT_REPO_ROOT/$O/prof.log 2>&1 || exit 1
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_c6 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload c6 --steps 20 --warmup 3 > $GRAFT_REPO_ROOT/$O/prof_c6.log 2>&1 || exit 1

@@ -217,6 +217,7 @@ struct kge_shard_exec {
     static constexpr int kTimingEvents = 4 + 6 * kMaxChunks;
     hipEvent_t t[kTimingEvents] = {};
     bool timed = false;  // the last step recorded them
+    bool broken = false;  // a step failed part-way: its plan slots and (under RCCL) its peers are in an unknown state
 
     int* slot_i(int s, size_t off) { return reinterpret_cast<int*>(ws + s * L.slot + off); }
 };
@@ -564,6 +565,16 @@ int kge_shard_exec_plan(kge_shard_exec* x, const int64_t* pos, const int64_t* ne
     return rc;
 }
 
+static int exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld, int64_t shard_lo, const float* rel,
+                     int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                     int64_t neg_ld, int mode, float gamma, float emb_range, float modulus, float temperature,
+                     int adversarial, const int64_t* next_pos, const int64_t* next_neg, int next_mode, float* scores,
+                     int64_t ns_ld, float* out_neg, float* pos_scores, float* out_pos, void* stream);
+
+// An error part-way through a step (a failed launch or collective, an inline plan) leaves the plan slots and,
+// under RCCL, the other ranks (blocked in the collective) in an unknown state: the executor is marked broken and
+// every later call fails at once. Argument errors found before any work (null pointers, the waiting plan made
+// for another batch) leave it usable.
 int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld, int64_t shard_lo, const float* rel,
                         int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
                         int64_t neg_ld, int mode, float gamma, float emb_range, float modulus, float temperature,
@@ -572,6 +583,26 @@ int kge_shard_exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld,
                         void* stream) {
     if (!x || !shard || !rel || !pos || !neg || !scores || !out_neg || !pos_scores || !out_pos)
         return set_error(KGE_EINVAL, "kge_shard_exec_step: null pointer");
+    if (x->broken)
+        return set_error(KGE_EHIP, "kge_shard_exec_step: an earlier step of this executor failed part-way; an exec "
+                                   "error is fatal to the executor and its communicator");
+    if (x->nplanned > 0) {
+        const kge_shard_exec::Slot& sl = x->slot[x->cur];
+        if (sl.pos != pos || sl.neg != neg || sl.neg_ld != neg_ld || sl.mode != mode)
+            return set_error(KGE_EINVAL, "kge_shard_exec_step: the waiting plan was made for another batch or mode");
+    }
+    const int rc = exec_step(x, shard, shard_ld, shard_lo, rel, nrelation, rel_ld, rel_off, pos, neg, neg_ld, mode,
+                             gamma, emb_range, modulus, temperature, adversarial, next_pos, next_neg, next_mode, scores,
+                             ns_ld, out_neg, pos_scores, out_pos, stream);
+    if (rc) x->broken = true;
+    return rc;
+}
+
+static int exec_step(kge_shard_exec* x, const float* shard, int64_t shard_ld, int64_t shard_lo, const float* rel,
+                     int64_t nrelation, int64_t rel_ld, int64_t rel_off, const int64_t* pos, const int64_t* neg,
+                     int64_t neg_ld, int mode, float gamma, float emb_range, float modulus, float temperature,
+                     int adversarial, const int64_t* next_pos, const int64_t* next_neg, int next_mode, float* scores,
+                     int64_t ns_ld, float* out_neg, float* pos_scores, float* out_pos, void* stream) {
     const hipStream_t st = (hipStream_t)stream;
     int s = x->cur;
     kge_shard_exec::Slot* sl = &x->slot[s];

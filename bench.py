@@ -290,6 +290,8 @@ class StepRunner:
             self.planner = ops.StepPlanner(fn, ent, rel, m._rel_off, m._D, B, N, m._gamma_f, m._range_f,
                                            modulus=mod)
         self.next_i = None  # the step the pending plan is for
+        # two output sets, alternating (a training loop double-buffers what the next step overwrites)
+        self.outs = [self.planner.outputs() for _ in range(2)] if self.planner is not None else None
 
     def batch(self, i):
         return self.batches[i % len(self.batches)]
@@ -304,7 +306,7 @@ class StepRunner:
             self.planner.plan(pos, neg, md)  # the chain starts here (a run's first step, or a new chain)
         npos, nneg = self.batch(i + 1)
         nmd = (i + 1) % 2 if mode is None else mode
-        out = self.planner.step(nxt=(npos, nneg, nmd))
+        out = self.planner.step(nxt=(npos, nneg, nmd), out=self.outs[i % 2])
         self.next_i = (i + 1, nmd)
         return out
 
@@ -1358,12 +1360,15 @@ def main(argv=None):
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_us = []  # host time of each step's calls (the loop is host-bound if these reach the device step)
     for i in range(a.steps):
         g, r = divmod(i, ev_group)
         if g % 2 == 0 and r == 0 and i + ev_group <= a.steps:
             evs[g] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             evs[g][0].record()
+        h0 = time.perf_counter()
         runner(a.warmup + i)  # continues the warmup's plan chain: one plan per timed step, made inside it
+        host_us.append((time.perf_counter() - h0) * 1e6)
         if g in evs and r == ev_group - 1:
             evs[g][1].record()
     torch.cuda.synchronize()
@@ -1450,6 +1455,7 @@ def main(argv=None):
                        "lists) made by the previous step's tail blocks; one plan per timed step"
                        if runner.planner is not None else "none (kge_step_forward)"),
             unplanned_step_us=unplanned_us,
+            host_us_per_step_median=statistics.median(host_us), event_group_step_us=[x * 1e3 for x in kern_ms],
             unique_row_bytes_per_step=uniq * ent_dim_ * 4, row_reuse=(B * N + 2 * B) / max(1, uniq)),
         "build": kge.build_id(),
     }

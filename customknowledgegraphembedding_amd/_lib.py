@@ -86,6 +86,13 @@ SIGNATURES = {
         [_c_i, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f,
          _c_f, _c_i, _c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p],
     ),
+    "kge_step_planner_create": (
+        _c_i, [_c_p, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f,
+               _c_f, _c_i, _c_p, _c_p, _c_i64, _c_p]),
+    "kge_step_planner_set_modulus": (_c_i, [_c_p, _c_f]),
+    "kge_step_planner_plan": (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i]),
+    "kge_step_planner_step": (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p, _c_p, _c_p]),
+    "kge_step_planner_destroy": (_c_i, [_c_p]),
     "kge_step_finish": (
         _c_i,
         [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_i64,

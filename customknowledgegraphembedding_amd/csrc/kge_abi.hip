@@ -36,22 +36,6 @@ __global__ __launch_bounds__(kBlock) void neg_rows_kernel(ScoreParams p) {
     if (lane == 0) p.out_neg[b] = r;
 }
 
-// ... and, with p.tile_next.plan set, blocks past the rows' make the next batch's step plan (kge_step_forward_planned:
-// the row reductions use few CUs, the plan blocks run beside them)
-__global__ __launch_bounds__(kBlock) void neg_rows_plan_kernel(ScoreParams p) {
-    __shared__ int sm[plan_lds_ints(kBlock)];
-    const int rb = (int)((p.B + kWavesPerBlock - 1) / kWavesPerBlock);
-    if ((int)blockIdx.x >= rb) {
-        tile_plan_group<kWavesPerBlock>(p.tile_next, (int)blockIdx.x - rb, sm);
-        return;
-    }
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (b >= p.B) return;
-    const int lane = threadIdx.x & 63;
-    const float r = row_reduce_fast(p.out + b * p.out_ld, p.N, p.temperature, p.adversarial, lane);
-    if (lane == 0) p.out_neg[b] = r;
-}
-
 // With `ps` set it also writes the positive branch's d_ps[b] = d_out_pos[b] * sigmoid(-ps[b])
 // (logsigmoid backward, model.py:145), saving the separate launch in the train step.
 __global__ __launch_bounds__(kBlock) void neg_reduce_bwd_kernel(const float* __restrict__ s, int64_t B, int64_t N,
@@ -906,27 +890,110 @@ int kge_step_forward_planned(int fn, int mode, const float* ent, int64_t nentity
     p.out_pos_ls = out_pos;
     p.tile_pos = 1;
     p.tile_plan = reinterpret_cast<const int*>(plan);
-    // where the next batch's plan is made: the tile launch's tail blocks, or beside the row reductions
-    const char* at = getenv("KGE_PLAN_AT");  // A/B of the placement (temporary)
-    const bool at_rows = at && strcmp(at, "rows") == 0;
-    PlanArgs nx{};
-    if (next_plan)
-        nx = plan_args(tp, next_mode, nentity, nrelation, next_pos, next_neg, next_neg_ld, B, N, next_plan);
-    if (next_plan && !at_rows) {
-        p.tile_next = nx;
+    // the next batch's plan: the scoring launch's tail blocks, on the CUs its scoring blocks free up at its end
+    // (C2 device time per step, alternating modes: 93.6 us; made beside the row reductions 99.5 us, as a launch
+    // of its own 101.6 us, not planned 101.9 us; scripts/plan_probe.py, profiles/r05_plan_ab.txt)
+    if (next_plan) {
+        p.tile_next = plan_args(tp, next_mode, nentity, nrelation, next_pos, next_neg, next_neg_ld, B, N, next_plan);
         p.tile_lds = std::max(p.tile_lds, plan_lds_ints(p.tile_waves * kWave) * 4);
     }
     rc = run_score(fn, mode, p, KIND_STEP_FWD_TILE, stream);
     if (rc) return rc;
     const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (next_plan && at_rows) {
-        p.tile_next = nx;
-        hipLaunchKernelGGL(neg_rows_plan_kernel, dim3((unsigned)(blocks + plan_groups(B, tp.tile_rows))), dim3(kBlock),
-                           0, (hipStream_t)stream, p);
-    } else {
-        hipLaunchKernelGGL(neg_rows_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, p);
-    }
+    hipLaunchKernelGGL(neg_rows_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, p);
     return check_launch("kge_step_forward_planned row reductions");
+}
+
+// The planned step loop as a handle (kge_step_planner_*): the tables, shapes and the two plan buffers are given
+// once; a step then passes only the next batch and the outputs (9 arguments instead of 29: at C2 the device
+// step is ~93 us and the host issues one step per step, so its per-call cost is part of the loop's rate).
+struct kge_step_planner {
+    int fn = 0, adversarial = 1;
+    const float* ent = nullptr;
+    const float* rel = nullptr;
+    int64_t nentity = 0, ent_ld = 0, nrelation = 0, rel_ld = 0, rel_off = 0, B = 0, N = 0, D = 0;
+    float gamma = 0.f, emb_range = 0.f, modulus = 0.f, temperature = 1.f;
+    void* plans[2] = {nullptr, nullptr};
+    int cur = -1;  // the buffer holding the next step's plan (-1: none)
+    int mode = 0;  // that plan's batch mode
+    void* stream = nullptr;
+};
+
+int kge_step_planner_create(kge_step_planner** out, int fn, const float* ent, int64_t nentity, int64_t ent_ld,
+                            const float* rel, int64_t nrelation, int64_t rel_ld, int64_t rel_off, int64_t B, int64_t N,
+                            int64_t D, float gamma, float emb_range, float modulus, float temperature, int adversarial,
+                            void* plan0, void* plan1, int64_t plan_bytes, void* stream) {
+    if (!out) return fail(KGE_EINVAL, "kge_step_planner_create: null pointer");
+    *out = nullptr;
+    const int64_t need = kge_step_plan_size(fn, nentity, ent_ld, nrelation, rel_ld, rel_off, B, N, D);
+    if (need <= 0) return fail(KGE_ENOTSUP, "kge_step_planner_create: the tile form does not apply to this shape");
+    if (!ent || !rel || !plan0 || !plan1 || plan0 == plan1) return fail(KGE_EINVAL, "kge_step_planner_create: bad pointers");
+    if (plan_bytes < need || !aligned(plan0, 16) || !aligned(plan1, 16))
+        return fail(KGE_EINVAL, "kge_step_planner_create: plan buffers too small or not 16-B aligned");
+    kge_step_planner* sp = new kge_step_planner;
+    sp->fn = fn;
+    sp->ent = ent;
+    sp->nentity = nentity;
+    sp->ent_ld = ent_ld;
+    sp->rel = rel;
+    sp->nrelation = nrelation;
+    sp->rel_ld = rel_ld;
+    sp->rel_off = rel_off;
+    sp->B = B;
+    sp->N = N;
+    sp->D = D;
+    sp->gamma = gamma;
+    sp->emb_range = emb_range;
+    sp->modulus = modulus;
+    sp->temperature = temperature;
+    sp->adversarial = adversarial;
+    sp->plans[0] = plan0;
+    sp->plans[1] = plan1;
+    sp->stream = stream;
+    *out = sp;
+    return ok();
+}
+
+int kge_step_planner_set_modulus(kge_step_planner* sp, float modulus) {
+    if (!sp) return fail(KGE_EINVAL, "kge_step_planner_set_modulus: null pointer");
+    sp->modulus = modulus;
+    return ok();
+}
+
+int kge_step_planner_plan(kge_step_planner* sp, const int64_t* pos, const int64_t* neg, int64_t neg_ld, int mode) {
+    if (!sp) return fail(KGE_EINVAL, "kge_step_planner_plan: null pointer");
+    const int buf = sp->cur < 0 ? 0 : sp->cur;
+    const int rc = kge_step_plan(sp->fn, mode, sp->nentity, sp->ent_ld, sp->nrelation, sp->rel_ld, sp->rel_off, pos, neg,
+                                 neg_ld, sp->B, sp->N, sp->D, sp->plans[buf], sp->stream);
+    if (rc) return rc;
+    sp->cur = buf;
+    sp->mode = mode;
+    return ok();
+}
+
+int kge_step_planner_step(kge_step_planner* sp, const int64_t* next_pos, const int64_t* next_neg, int64_t next_neg_ld,
+                          int next_mode, float* neg_scores, float* out_neg, float* pos_scores, float* out_pos) {
+    if (!sp) return fail(KGE_EINVAL, "kge_step_planner_step: null pointer");
+    if (sp->cur < 0) return fail(KGE_EINVAL, "kge_step_planner_step: no batch planned (kge_step_planner_plan first)");
+    const bool nxt = next_pos && next_neg;
+    const int rc = kge_step_forward_planned(
+        sp->fn, sp->mode, sp->ent, sp->nentity, sp->ent_ld, sp->rel, sp->nrelation, sp->rel_ld, sp->rel_off, sp->B,
+        sp->N, sp->D, sp->gamma, sp->emb_range, sp->modulus, sp->temperature, sp->adversarial, sp->plans[sp->cur],
+        next_pos, next_neg, next_neg_ld, next_mode, nxt ? sp->plans[1 - sp->cur] : nullptr, neg_scores, sp->N, out_neg,
+        pos_scores, out_pos, sp->stream);
+    if (rc) return rc;
+    if (nxt) {
+        sp->cur = 1 - sp->cur;
+        sp->mode = next_mode;
+    } else {
+        sp->cur = -1;
+    }
+    return ok();
+}
+
+int kge_step_planner_destroy(kge_step_planner* sp) {
+    delete sp;
+    return ok();
 }
 
 int kge_score_sharded(int fn, int mode, const float* qent, int64_t q_ld, const float* rel, int64_t nrelation,

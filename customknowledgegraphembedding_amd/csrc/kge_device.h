@@ -993,6 +993,14 @@ __device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
     constexpr int TPI = 17;  // C2's 16 x 257 items over 768 threads walked once; larger groups twice
     const bool in_regs = nf <= TPI * NT;
     int ky[TPI], ic[TPI], cd[TPI];
+    // the rows' positives (b, h, r, t), loaded with the walk's ids (one round trip), stored at the end
+    int64_t ph = -1, pr = -1, pt = -1;
+    if (t < nr) {
+        const int64_t b = brow[t];
+        ph = a.pos[b * 3];
+        pr = a.pos[b * 3 + 1];
+        pt = a.pos[b * 3 + 2];
+    }
     if (in_regs) {
         int64_t idv[TPI];
         int rr[TPI];
@@ -1013,26 +1021,6 @@ __device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
             item(f, k, i, c);
             atomicAdd(&hist[k], 1);
         }
-    }
-    // the rows' (b, h, r, t), ids checked (-1: out of range); the header
-    auto chk = [](int64_t id, int64_t n) { return (id >= 0 && id < n) ? (int)id : -1; };
-    if (t < R) {
-        int4 m = make_int4(-1, -1, -1, -1);
-        if (t < nr) {
-            const int64_t b = brow[t];
-            m = make_int4((int)b, chk(a.pos[b * 3], a.nent), chk(a.pos[b * 3 + 1], a.nrel), chk(a.pos[b * 3 + 2], a.nent));
-        }
-        reinterpret_cast<int4*>(a.plan + kPlanHdr)[(int64_t)g * R + t] = m;
-    }
-    if (g == 0 && t == 0) {
-        int* h = a.plan;
-        h[0] = kPlanMagic;
-        h[1] = (int)a.B;
-        h[2] = (int)a.N;
-        h[3] = a.mode;
-        h[4] = R;
-        h[5] = (int)a.nent;
-        h[6] = a.sort;
     }
     __syncthreads();
     if (w == 0) {  // exclusive scan of the 8 x 256 counts, 32 per lane; the slice starts
@@ -1074,6 +1062,21 @@ __device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
             item(f, k, i, c);
             list[atomicAdd(&hist[k], 1)] = make_int2(i, c);
         }
+    }
+    // the rows' (b, h, r, t), ids checked (-1: out of range); the header
+    auto chk = [](int64_t id, int64_t n) { return (id >= 0 && id < n) ? (int)id : -1; };
+    if (t < R)
+        reinterpret_cast<int4*>(a.plan + kPlanHdr)[(int64_t)g * R + t] =
+            t < nr ? make_int4(brow[t], chk(ph, a.nent), chk(pr, a.nrel), chk(pt, a.nent)) : make_int4(-1, -1, -1, -1);
+    if (g == 0 && t == 0) {
+        int* h = a.plan;
+        h[0] = kPlanMagic;
+        h[1] = (int)a.B;
+        h[2] = (int)a.N;
+        h[3] = a.mode;
+        h[4] = R;
+        h[5] = (int)a.nent;
+        h[6] = a.sort;
     }
 }
 

@@ -421,12 +421,6 @@ struct XsGemmRegs {
     float4 a[2], b[2];
 };
 
-// STAG (round 5): the two waves of a SIMD (w and w + 4) run the same step at the same time — both multiply, then
-// both split and store the next chunk — so the SIMD's matrix core idles while they convert. Waves 4-7 store
-// first and multiply second (the two are independent within a step: they touch different LDS stages), so one
-// wave of each SIMD converts while the other multiplies (MI355X_MICROARCH.md: stagger SIMD partners by wave
-// number >= 4). The products and their order are unchanged: C is bitwise the same.
-template <bool STAG>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2))) void gemm_nt_x3s_kernel(
     const float* __restrict__ A, const float* __restrict__ Bm, float* __restrict__ C, int M, int N, int K, int64_t lda,
     int64_t ldb, int64_t ldc) {
@@ -516,13 +510,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
         }
     };
     auto step = [&](int g, XsGemmRegs& nxt) {
-        if (!STAG || wave < 4) {
-            compute(g & 1);
-            if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-        } else {
-            if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-            compute(g & 1);
-        }
+        compute(g & 1);
+        if (g + 1 < T) sstore(nxt, (g + 1) & 1);
         if (g + 3 < T) gload(nxt, g + 3);
         __syncthreads();
     };
@@ -556,23 +545,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
 int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
                          int64_t ldc, hipStream_t st, int form) {
     // the split-once kernel when its 32-bit buffer offsets cover both operands and its rows take float4 loads;
-    // form 1 (kge_forms.gemm_form) keeps gemm_nt_f32x3_kernel, which splits each fragment in registers; form 2
-    // the split-once kernel without the SIMD-partner stagger (A/B)
+    // form 1 (kge_forms.gemm_form) keeps gemm_nt_f32x3_kernel, which splits each fragment in registers (a
+    // SIMD-partner stagger, waves 4-7 storing before multiplying, measured no faster: profiles/r05_stagger_ab.txt)
     if (form != 1 && (int64_t)M * lda * 4 < (int64_t)XS_OOB && (int64_t)N * ldb * 4 < (int64_t)XS_OOB &&
         K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0) {
-        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3s_kernel<true>),
+        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3s_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
-        static const bool attr2 = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3s_kernel<false>),
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
         (void)attr;
-        (void)attr2;
         const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
-        if (form == 2)
-            hipLaunchKernelGGL(gemm_nt_x3s_kernel<false>, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st, A, B, C, M,
-                               N, K, lda, ldb, ldc);
-        else
-            hipLaunchKernelGGL(gemm_nt_x3s_kernel<true>, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st, A, B, C, M,
-                               N, K, lda, ldb, ldc);
+        hipLaunchKernelGGL(gemm_nt_x3s_kernel, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st, A, B, C, M, N, K, lda,
+                           ldb, ldc);
         return 0;
     }
     const int64_t tiles = (int64_t)((M + XBM - 1) / XBM) * ((N + XBM - 1) / XBM);

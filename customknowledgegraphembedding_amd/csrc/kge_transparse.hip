@@ -886,9 +886,6 @@ struct XsRegs {
     float4 a[2], b[2], m[2];
 };
 
-// STAG: waves 4-7 split and store the next chunk before multiplying this one (the eval GEMM's stagger,
-// gemm_nt_x3s_kernel): bitwise the same scores
-template <bool STAG>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(2))) void
 ts_fwd_x3s_kernel(TsParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char xs_smem[];  // 2 stages, then u - 1 (d floats)
@@ -1071,13 +1068,8 @@ ts_fwd_x3s_kernel(TsParams p) {
     // one chunk step: multiply stage g % 2, store chunk g + 1 (held in `nxt`) into the other stage, load chunk
     // g + 3 into `nxt` (chunk g + 2 is in flight in the other set), fold at the end of a column super-tile
     auto step = [&](int g, XsRegs& nxt) {
-        if (!STAG || wave < 4) {
-            compute(g & 1);
-            if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-        } else {
-            if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-            compute(g & 1);
-        }
+        compute(g & 1);
+        if (g + 1 < T) sstore(nxt, (g + 1) & 1);
         if (g + 3 < T) gload(nxt, g + 3);
         if ((g + 1) % nk == 0) {
             fold(g / nk);
@@ -1351,13 +1343,8 @@ ts_fwd_x3g_kernel(TsParams p) {
         }
     };
     auto step = [&](int g, XgRegs<JPW>& nxt) {
-        if (NWV < 8 || wave < 4) {  // 8 waves: waves 4-7 store first (the stagger of ts_fwd_x3s_kernel)
-            compute(g & 1);
-            if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-        } else {
-            if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-            compute(g & 1);
-        }
+        compute(g & 1);
+        if (g + 1 < T) sstore(nxt, (g + 1) & 1);
         if (g + 3 < T) gload(nxt, g + 3);
         if ((g + 1) % nk == 0) {
             fold(g / nk);
@@ -1755,7 +1742,7 @@ void launch_rows(const TsParams& p, hipStream_t st) {
         // staging where the 32-bit buffer offsets reach (form 1: the forms that split each fragment in registers,
         // for the bitwise / rounding cross-checks)
         if (use_v4(p)) {
-            const bool xs_ok = (p.form == 0 || (p.form == 2 && p.grouped)) && p.d <= kXsMaxDim && p.nent * p.ent_ld * 4 < (int64_t)kXsOOB &&
+            const bool xs_ok = p.form == 0 && p.d <= kXsMaxDim && p.nent * p.ent_ld * 4 < (int64_t)kXsOOB &&
                                (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB;
             if (p.grouped && xs_ok) {
                 // single / tail-batch rows: 64 rows of one relation per block (ts_fwd_x3g_kernel), all columns, or
@@ -1789,25 +1776,13 @@ void launch_rows(const TsParams& p, hipStream_t st) {
                 // the batch row's negatives
                 TsParams q = p;
                 q.nchunk = (int)((p.N + XBR - 1) / XBR);
-                if (xs_ok || (p.form == 2 && p.d <= kXsMaxDim && p.nent * p.ent_ld * 4 < (int64_t)kXsOOB &&
-                              (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB)) {
-                    // operands split once at staging (ts_fwd_x3s_kernel, bitwise ts_fwd_x3_kernel's scores); form 2:
-                    // without the SIMD-partner stagger (A/B)
+                if (xs_ok) {  // operands split once at staging (ts_fwd_x3s_kernel, bitwise ts_fwd_x3_kernel's scores)
                     const size_t lds = 2 * (size_t)kXsStage + (size_t)p.d * 4;
-                    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel<true>),
+                    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel),
                                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                                  2 * kXsStage + kXsMaxDim * 4) == hipSuccess;
-                    static const bool attr2 = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel<false>),
-                                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                                  2 * kXsStage + kXsMaxDim * 4) == hipSuccess;
                     (void)attr;
-                    (void)attr2;
-                    if (p.form == 2)
-                        hipLaunchKernelGGL(ts_fwd_x3s_kernel<false>, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds,
-                                           st, q);
-                    else
-                        hipLaunchKernelGGL(ts_fwd_x3s_kernel<true>, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds,
-                                           st, q);
+                    hipLaunchKernelGGL(ts_fwd_x3s_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);
                     return;
                 }
                 hipLaunchKernelGGL(ts_fwd_x3_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);

@@ -163,10 +163,10 @@ def step_forward_raw(fn, mode, ent, rel, rel_off, pos, neg, D, gamma, emb_range,
 
 
 class StepPlanner:
-    """step_forward_raw with the tile scorer's id-only setup made one step AHEAD (kge_step_plan /
-    kge_step_forward_planned): a step loop that knows its next batch (run.py's prefetching input pipeline,
-    run.py:40-66) hands it to the current step, whose launch's tail blocks plan it, so the next step's blocks
-    start on their sorted candidates at once. Outputs are bitwise step_forward_raw's.
+    """step_forward_raw with the tile scorer's id-only setup made one step AHEAD (kge_step_planner_*: the handle
+    form of kge_step_plan / kge_step_forward_planned): a step loop that knows its next batch (run.py's prefetching
+    input pipeline, run.py:40-66) hands it to the current step, whose launch's tail blocks plan it, so the next
+    step's blocks start on their sorted candidates at once. Outputs are bitwise step_forward_raw's.
 
         sp = StepPlanner(fn, ent, rel, rel_off, D, B, N, gamma, emb_range)
         sp.plan(pos0, neg0, mode0)                    # the first batch's plan: one launch
@@ -176,25 +176,36 @@ class StepPlanner:
     A plan is a snapshot of its batch's ids (the planned step reads no id but the plan's). The planner keeps
     the tensors of the batch being planned until the step that consumes the plan, and two plan buffers
     (the step reads one while its tail blocks write the other). The tables may change between steps (they are
-    read at step time). `available(...)` is False when the tile form does not apply (use step_forward_raw)."""
+    read at step time); the launch stream is torch's current stream when the planner is made. `available(...)`
+    is False when the tile form does not apply (use step_forward_raw). A step costs the host one 9-argument
+    C call: the tables, shapes and buffers live in the library's handle."""
 
     def __init__(self, fn, ent, rel, rel_off, D, B, N, gamma, emb_range, modulus=0.0, temperature=1.0,
                  adversarial=True):
+        import ctypes
         _need_gpu(ent, rel)
         _fp32(ent, "entity_embedding")
         _fp32(rel, "relation_embedding")
         self.fn, self.ent, self.rel, self.rel_off, self.D = fn, ent, rel, rel_off, D
         self.B, self.N = B, N
-        self.gamma, self.emb_range, self.modulus = float(gamma), float(emb_range), float(modulus)
-        self.temperature, self.adversarial = float(temperature), int(bool(adversarial))
+        lib = _lib.load()
         nbytes = self.plan_size(fn, ent, rel, rel_off, D, B, N)
         if nbytes <= 0:
             raise _lib.KGEHipError("kge_step_plan_size is 0: the tile form does not apply to this shape "
                                    "(use step_forward_raw)")
         self._bufs = [torch.empty(nbytes, dtype=torch.uint8, device=ent.device) for _ in range(2)]
-        self._cur = None       # index of the buffer holding the next step's plan
-        self._mode = None      # that plan's batch mode
-        self._held = None      # the tensors that plan was made from (kept alive until its step)
+        h = ctypes.c_void_p()
+        check(lib.kge_step_planner_create(
+            ctypes.addressof(h), fn, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0],
+            rel.stride(0), rel_off, B, N, D, float(gamma), float(emb_range), float(modulus), float(temperature),
+            int(bool(adversarial)), self._bufs[0].data_ptr(), self._bufs[1].data_ptr(), nbytes,
+            _stream(ent.device)), "kge_step_planner_create")
+        self._h = h.value
+        self._lib = lib
+        self._step_fn = lib.kge_step_planner_step
+        self._planned = False
+        self._held = None      # the tensors the waiting plan was made from (kept alive until its step)
+        self._pshape, self._nshape = (B, 3), (B, N)
 
     @staticmethod
     def plan_size(fn, ent, rel, rel_off, D, B, N):
@@ -206,57 +217,64 @@ class StepPlanner:
         return cls.plan_size(fn, ent, rel, rel_off, D, B, N) > 0
 
     def _check_batch(self, pos, neg, mode):
-        _need_gpu(pos, neg)
-        _i64(pos, "positive_sample")
-        _i64(neg, "negative_sample")
         if mode not in (HEAD_BATCH, TAIL_BATCH):
             raise ValueError("a planned step needs a negative mode (0 head-batch or 1 tail-batch)")
-        if tuple(pos.shape) != (self.B, 3) or not pos.is_contiguous():
-            raise ValueError(f"positive_sample must be a contiguous [{self.B}, 3] int64 tensor")
-        if tuple(neg.shape) != (self.B, self.N) or neg.stride(1) != 1:
-            raise ValueError(f"negative_sample must be a row-contiguous [{self.B}, {self.N}] int64 tensor")
+        if pos.shape != self._pshape or neg.shape != self._nshape:
+            raise ValueError(f"a planned batch must be pos [{self.B}, 3] and neg [{self.B}, {self.N}]")
+        if pos.dtype != torch.int64 or neg.dtype != torch.int64 or pos.device != self.ent.device or \
+                neg.device != self.ent.device:
+            raise TypeError("a planned batch must be int64 tensors on the tables' device")
+        if pos.stride() != (3, 1) or neg.stride(1) != 1:
+            raise ValueError("pos must be contiguous and neg row-contiguous")
+
+    def set_modulus(self, modulus):
+        check(self._lib.kge_step_planner_set_modulus(self._h, float(modulus)), "kge_step_planner_set_modulus")
 
     def plan(self, pos, neg, mode):
         """The plan of the batch the next step() scores (a run's first batch; later ones come from step)."""
         self._check_batch(pos, neg, mode)
-        buf = 0 if self._cur is None else self._cur
-        rc = _lib.load().kge_step_plan(self.fn, mode, self.ent.shape[0], self.ent.stride(0), self.rel.shape[0],
-                                       self.rel.stride(0), self.rel_off, pos.data_ptr(), neg.data_ptr(),
-                                       neg.stride(0), self.B, self.N, self.D, self._bufs[buf].data_ptr(),
-                                       _stream(self.ent.device))
-        check(rc, "kge_step_plan")
-        self._cur, self._mode, self._held = buf, mode, (pos, neg)
+        check(self._lib.kge_step_planner_plan(self._h, pos.data_ptr(), neg.data_ptr(), neg.stride(0), mode),
+              "kge_step_planner_plan")
+        self._planned, self._held = True, (pos, neg)
+
+    def outputs(self):
+        """A set of output tensors for step(out=...): (out_neg [B], out_pos [B], neg_scores [B, N], pos_scores [B])."""
+        dev = self.ent.device
+        return (torch.empty((self.B,), dtype=torch.float32, device=dev),
+                torch.empty((self.B,), dtype=torch.float32, device=dev),
+                torch.empty((self.B, self.N), dtype=torch.float32, device=dev),
+                torch.empty((self.B,), dtype=torch.float32, device=dev))
 
     def step(self, nxt=None, out=None):
         """Both model calls on the planned batch -> (out_neg [B], out_pos [B], neg_scores [B, N],
-        pos_scores [B]); with nxt = (pos, neg, mode) the same launch plans that batch for the next step."""
-        if self._cur is None:
+        pos_scores [B]); with nxt = (pos, neg, mode) the same launch plans that batch for the next step.
+        `out`: outputs to write (from outputs(); neg_scores contiguous), else fresh tensors."""
+        if not self._planned:
             raise RuntimeError("StepPlanner.step: no batch planned (call plan() first, or pass nxt to step)")
-        dev = self.ent.device
-        if out is None:
-            out = (torch.empty((self.B,), dtype=torch.float32, device=dev),
-                   torch.empty((self.B,), dtype=torch.float32, device=dev),
-                   torch.empty((self.B, self.N), dtype=torch.float32, device=dev),
-                   torch.empty((self.B,), dtype=torch.float32, device=dev))
-        out_neg, out_pos, neg_scores, pos_scores = out
-        nbuf, npos, nneg, nmode = None, None, None, 0
-        if nxt is not None:
+        out_neg, out_pos, neg_scores, pos_scores = out if out is not None else self.outputs()
+        if nxt is None:
+            rc = self._step_fn(self._h, None, None, 0, 0, neg_scores.data_ptr(), out_neg.data_ptr(),
+                               pos_scores.data_ptr(), out_pos.data_ptr())
+        else:
             npos, nneg, nmode = nxt
             self._check_batch(npos, nneg, nmode)
-            nbuf = 1 - self._cur
-        rc = _lib.load().kge_step_forward_planned(
-            self.fn, self._mode, self.ent.data_ptr(), self.ent.shape[0], self.ent.stride(0), self.rel.data_ptr(),
-            self.rel.shape[0], self.rel.stride(0), self.rel_off, self.B, self.N, self.D, self.gamma,
-            self.emb_range, self.modulus, self.temperature, self.adversarial, self._bufs[self._cur].data_ptr(),
-            ctypes_ptr(npos), ctypes_ptr(nneg), 0 if nneg is None else nneg.stride(0), nmode,
-            None if nbuf is None else self._bufs[nbuf].data_ptr(), neg_scores.data_ptr(), neg_scores.stride(0),
-            out_neg.data_ptr(), pos_scores.data_ptr(), out_pos.data_ptr(), _stream(dev))
-        check(rc, "kge_step_forward_planned")
+            rc = self._step_fn(self._h, npos.data_ptr(), nneg.data_ptr(), nneg.stride(0), nmode,
+                               neg_scores.data_ptr(), out_neg.data_ptr(), pos_scores.data_ptr(), out_pos.data_ptr())
+        check(rc, "kge_step_planner_step")
         if nxt is None:
-            self._cur, self._mode, self._held = None, None, None
+            self._planned, self._held = False, None
         else:
-            self._cur, self._mode, self._held = nbuf, nmode, (npos, nneg)
+            self._held = (nxt[0], nxt[1])
         return out_neg, out_pos, neg_scores, pos_scores
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                self._lib.kge_step_planner_destroy(h)
+            except Exception:  # noqa: BLE001 (interpreter teardown)
+                pass
+            self._h = None
 
 
 def step_finish_raw(fn, ent, rel, rel_off, pos, D, gamma, emb_range, neg_scores, modulus=0.0,

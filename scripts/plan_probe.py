@@ -1,8 +1,7 @@
 """Round-5 probe: the C2 step with and without its plan made ahead, and where the plan is made.
 Device time per step (events around 50 steps after 20 warmup), same batches as bench.py's C2 line:
   unplanned           kge_step_forward (setup inside the tile kernel)
-  planned_tail        kge_step_forward_planned, next plan in the tile launch's tail blocks (KGE_PLAN_AT=tail)
-  planned_rows        the same, next plan beside the row reductions (KGE_PLAN_AT=rows)
+  planned_tail        kge_step_forward_planned, next plan in the tile launch's tail blocks
   planned_standalone  kge_step_plan as its own launch, then the planned step without a next plan
 Usage: python scripts/plan_probe.py [workload]"""
 import json
@@ -44,12 +43,9 @@ res["unplanned"] = timed(plain)
 # mode switch costs per step
 res["unplanned_head_only"] = timed(lambda i: plain(i, 0))
 res["unplanned_tail_only"] = timed(lambda i: plain(i, 1))
-for at in ("tail", "rows"):
-    os.environ["KGE_PLAN_AT"] = at
-    r = bench.StepRunner(m, batches, fn, planned=True)
-    res["planned_" + at] = timed(r)
-    res["planned_" + at + "_head_only"] = timed(lambda i: r(i, 0))
-os.environ.pop("KGE_PLAN_AT")
+r = bench.StepRunner(m, batches, fn, planned=True)
+res["planned_tail"] = timed(r)
+res["planned_tail_head_only"] = timed(lambda i: r(i, 0))
 sp = bench.StepRunner(m, batches, fn, planned=True).planner
 
 

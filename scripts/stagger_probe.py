@@ -1,7 +1,8 @@
 """Round-5 A/B: the SIMD-partner stagger (waves 4-7 store the next chunk before multiplying) in the eval GEMM
 (gemm_nt_x3s_kernel, C5 shape 4096 x 14951 x 1000) and the TranSparse head-batch forward (ts_fwd_x3s_kernel, c6
 shape); the TranSparse single-mode rows split over 128-column ranges (ts_fwd_x3g_kernel<4, 1> + finish) against
-one block per relation chunk. Device time per launch, forms interleaved, 3 rounds of 10 launches each."""
+one block per relation chunk. Device time per launch, forms interleaved, 3 rounds of 10 launches each.
+(The no-stagger forms 2 it compared were removed after this A/B: profiles/r05_stagger_ab.txt.)"""
 import ctypes
 import json
 import os

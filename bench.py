@@ -828,10 +828,20 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
     ent = m.entity_embedding.detach()
     Q = torch.empty((Bq, K), dtype=torch.float32, device=device)
     lib = __import__("customknowledgegraphembedding_amd._lib", fromlist=["load"]).load()
+    split = os.environ.get("KGE_BENCH_EVAL_SPLIT", "planes")  # planes (default) | staging (the round-4 form)
+    qp = torch.empty(int(lib.kge_split_bf16x3_bytes(Bq, K)), dtype=torch.uint8, device=device)
+    ep = torch.empty(int(lib.kge_split_bf16x3_bytes(E, K)), dtype=torch.uint8, device=device)
+
+    def entity_pass():
+        """The start of an evaluation pass: the entity table's bf16 planes (evaluate.entity_planes), once per pass."""
+        if split == "planes":
+            lib.kge_split_bf16x3(ent.data_ptr(), E, K, ent.stride(0), ep.data_ptr(), E,
+                                 torch.cuda.current_stream().cuda_stream)
 
     def step(b, ev=None):
-        """One query batch: Q = h*r or r*t (kge_eval_query), S = Q . E^T (kge_gemm_nt_bf16x3, events around
-        it), exact filtered ranks."""
+        """One query batch: Q = h*r or r*t (kge_eval_query), S = Q . E^T (the query's bf16 planes and
+        kge_gemm_nt_bf16x3_planes on the pass's entity planes, events around both; or kge_gemm_nt_bf16x3), exact
+        filtered ranks."""
         pos, mode, truth, fptr, fids = b
         st = torch.cuda.current_stream().cuda_stream
         lib.kge_eval_query(FN_IDS[w["fn"]], 0 if mode == "head-batch" else 1, ent.data_ptr(), E, ent.stride(0),
@@ -839,11 +849,16 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                            m._D, Q.data_ptr(), K, st)
         if ev is not None:
             ev[0].record()
-        lib.kge_gemm_nt_bf16x3(Q.data_ptr(), K, ent.data_ptr(), ent.stride(0), S.data_ptr(), E, Bq, E, K, st)
+        if split == "planes":
+            lib.kge_split_bf16x3(Q.data_ptr(), Bq, K, K, qp.data_ptr(), Bq, st)
+            lib.kge_gemm_nt_bf16x3_planes(qp.data_ptr(), Bq, ep.data_ptr(), E, K, S.data_ptr(), E, Bq, E, st)
+        else:
+            lib.kge_gemm_nt_bf16x3(Q.data_ptr(), K, ent.data_ptr(), ent.stride(0), S.data_ptr(), E, Bq, E, K, st)
         if ev is not None:
             ev[1].record()
         return evaluate.rank_filtered(S, truth, fptr, fids)
 
+    entity_pass()
     for i in range(a.warmup):
         step(batches[i % 4])
     torch.cuda.synchronize()
@@ -854,6 +869,7 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ranks = []
+    entity_pass()  # the timed region is one evaluation pass: its entity planes are made inside it
     for i in range(a.steps):
         ranks.append(step(batches[i % 4], evs[i]))
     torch.cuda.synchronize()
@@ -884,8 +900,10 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                        "parallelism": f"replicas{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": mfma_flops / gemm_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                          "frac": mfma_flops / gemm_s / 1e12 / 2500.0, "traffic": None,
-                         "kernel": ("gemm_nt_f32x3_kernel (v_mfma_f32_32x32x16_bf16, six products per 16 k, operands "
-                                    "split per fragment)" if os.environ.get("KGE_GEMM_X3S", "1") == "0" else
+                         "kernel": ("split3_planes_kernel (the query block's bf16 planes) + gemm_nt_x3p_kernel (256 x "
+                                    "256 tiles from the query and entity bf16 planes, no conversion in the loop, six "
+                                    "products per 16 k on v_mfma_f32_32x32x16_bf16; the entity planes made once per "
+                                    "evaluation pass, inside the timed region)" if split == "planes" else
                                     "gemm_nt_x3s_kernel (256 x 256 tiles, operands split once at staging into bf16 "
                                     "planes, six products per 16 k on v_mfma_f32_32x32x16_bf16)"),
                          "kernel_avg_us": gemm_s * 1e6,

@@ -1124,6 +1124,37 @@ int kge_gemm_nt(const float* A, int64_t lda, const float* Bm, int64_t ldb, float
     return check_launch("kge_gemm_nt");
 }
 
+int64_t kge_split_bf16x3_bytes(int64_t rows, int64_t cols) {
+    if (rows < 0 || cols <= 0) return 0;
+    return 3 * rows * ((cols + 15) / 16 * 16) * 2;
+}
+
+int kge_split_bf16x3(const float* X, int64_t rows, int64_t cols, int64_t ld, void* planes, int64_t plane_rows,
+                     void* stream) {
+    if (rows < 0 || cols <= 0 || ld < cols || plane_rows < rows) return fail(KGE_EINVAL, "kge_split_bf16x3: bad shape");
+    if (rows == 0) return ok();
+    if (!X || !planes) return fail(KGE_EINVAL, "kge_split_bf16x3: null pointer");
+    if (!aligned(planes, 16)) return fail(KGE_EINVAL, "kge_split_bf16x3: planes must be 16-B aligned");
+    if (kge_split_bf16x3_bytes(plane_rows, cols) >= ((int64_t)1 << 32) - 16)
+        return fail(KGE_ENOTSUP, "kge_split_bf16x3: planes past 4 GB (the GEMM's 32-bit buffer offsets)");
+    launch_split3_planes(X, rows, cols, ld, planes, plane_rows, (hipStream_t)stream);
+    return check_launch("kge_split_bf16x3");
+}
+
+int kge_gemm_nt_bf16x3_planes(const void* A_planes, int64_t a_rows, const void* B_planes, int64_t b_rows, int64_t K,
+                              float* C, int64_t ldc, int64_t M, int64_t N, void* stream) {
+    if (M < 0 || N < 0 || K <= 0 || M > a_rows || N > b_rows) return fail(KGE_EINVAL, "bad shape");
+    if (M == 0 || N == 0) return ok();
+    if (!A_planes || !B_planes || !C) return fail(KGE_EINVAL, "null pointer");
+    if (M > INT32_MAX || N > INT32_MAX || !aligned(A_planes, 16) || !aligned(B_planes, 16))
+        return fail(KGE_EINVAL, "kge_gemm_nt_bf16x3_planes: int32 shapes and 16-B aligned planes");
+    if (kge_split_bf16x3_bytes(a_rows, K) >= ((int64_t)1 << 32) - 16 ||
+        kge_split_bf16x3_bytes(b_rows, K) >= ((int64_t)1 << 32) - 16)
+        return fail(KGE_ENOTSUP, "kge_gemm_nt_bf16x3_planes: planes past 4 GB");
+    launch_gemm_nt_x3p(A_planes, a_rows, B_planes, b_rows, K, C, ldc, (int)M, (int)N, (hipStream_t)stream);
+    return check_launch("kge_gemm_nt_bf16x3_planes");
+}
+
 int kge_gemm_nt_bf16x3(const float* A, int64_t lda, const float* Bm, int64_t ldb, float* C, int64_t ldc, int64_t M,
                       int64_t N, int64_t K, void* stream) {
     return kge_gemm_nt_bf16x3_ex(A, lda, Bm, ldb, C, ldc, M, N, K, nullptr, stream);

@@ -540,6 +540,149 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same GEMM on operands split BEFORE it (round 5): gemm_nt_x3s_kernel spends ~190 VALU instructions per wave
+// and 16-k chunk splitting its fp32 loads into bf16 terms and computing their addresses, against 48 MFMAs
+// (PMC, profiles/r05_pmc_c5.json: the matrix cores busy 0.60 of the kernel, co-issuing with that VALU work 20 %
+// of the time). The operands of the all-entity scores are reused: the entity table across every query batch of
+// an evaluation pass, the query block across the 59 entity tiles. split3_planes_kernel writes each fp32 matrix as
+// three bf16 planes [3][rows][kp] (xs_split3's arithmetic, kp = K rounded up to 16, zero padded), and
+// gemm_nt_x3p_kernel stages the planes' 16-B pieces into the same LDS images with no conversion: the products,
+// their order and C are bitwise gemm_nt_x3s_kernel's.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void split3_planes_kernel(const float* __restrict__ X, int64_t rows, int cols,
+                                                               int64_t ld, int kp, __bf16* __restrict__ P,
+                                                               int64_t plane) {
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // one k quad of one row
+    const int kq = kp / 4;
+    if (q >= rows * kq) return;
+    const int64_t r = q / kq;
+    const int k = (int)(q - r * kq) * 4;
+    xs_f32x4 v;
+    if (k + 3 < cols && (ld & 3) == 0 && ((uintptr_t)X & 15) == 0) {
+        const float4 x = *reinterpret_cast<const float4*>(X + r * ld + k);
+        v = xs_f32x4{x.x, x.y, x.z, x.w};
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = k + i < cols ? X[r * ld + k + i] : 0.f;
+    }
+    xs_bf16x4 s0, s1, s2;
+    xs_split3(v, s0, s1, s2);
+    __bf16* d = P + r * kp + k;
+    *reinterpret_cast<xs_bf16x4*>(d) = s0;
+    *reinterpret_cast<xs_bf16x4*>(d + plane) = s1;
+    *reinterpret_cast<xs_bf16x4*>(d + 2 * plane) = s2;
+}
+
+struct XpGemmRegs {
+    int4 a[3], b[3];
+};
+
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2))) void gemm_nt_x3p_kernel(
+    const __bf16* __restrict__ Ap, int64_t a_plane, const __bf16* __restrict__ Bp, int64_t b_plane, int kp,
+    float* __restrict__ C, int M, int N, int64_t ldc) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char gp_smem[];  // 2 stages
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int half = lane >> 5, col = lane & 31;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int ntn = (N + XS_T - 1) / XS_T, ntm = (M + XS_T - 1) / XS_T;
+    const int nblk = ntn * ntm;
+    int bid = blockIdx.x;
+    {  // XCD-aware bijective remap (gemm_nt_x3s_kernel's)
+        const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    }
+    const int tn = bid / ntm, tm = bid % ntm;
+    const int m0 = tm * XS_T, n0 = tn * XS_T;
+    const rsrc_t ra = make_rsrc(Ap, (uint32_t)(3 * a_plane * 2));
+    const rsrc_t rb = make_rsrc(Bp, (uint32_t)(3 * b_plane * 2));
+    // thread t stages row t >> 1, k half t & 1 of every plane: its byte offsets advance 32 B per chunk
+    const int srow = t >> 1, sh = t & 1;
+    const uint32_t oa0 = m0 + srow < M ? (uint32_t)(((int64_t)(m0 + srow) * kp + 8 * sh) * 2) : XS_OOB;
+    const uint32_t ob0 = n0 + srow < N ? (uint32_t)(((int64_t)(n0 + srow) * kp + 8 * sh) * 2) : XS_OOB;
+    const uint32_t pa = (uint32_t)(a_plane * 2), pb = (uint32_t)(b_plane * 2);
+    const int so = xs_off(srow, sh);
+    const int T = kp / 16;
+    auto gload = [&](XpGemmRegs& R, int g) {
+        const uint32_t dk = (uint32_t)g * 32u;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa0 == XS_OOB ? XS_OOB : oa0 + p * pa + dk, 0, 0);
+            const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rb, ob0 == XS_OOB ? XS_OOB : ob0 + p * pb + dk, 0, 0);
+            R.a[p] = make_int4(va[0], va[1], va[2], va[3]);
+            R.b[p] = make_int4(vb[0], vb[1], vb[2], vb[3]);
+        }
+    };
+    auto sstore = [&](const XpGemmRegs& R, int stage) {
+        unsigned char* As = gp_smem + stage * XS_STAGE;
+        unsigned char* Bs = As + 3 * XS_PLANE;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            *reinterpret_cast<int4*>(As + p * XS_PLANE + so) = R.a[p];
+            *reinterpret_cast<int4*>(Bs + p * XS_PLANE + so) = R.b[p];
+        }
+    };
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) acc[i][j][r2] = 0.f;
+    auto compute = [&](int stage) {  // gemm_nt_x3s_kernel's
+        const unsigned char* As = gp_smem + stage * XS_STAGE;
+        const unsigned char* Bs = As + 3 * XS_PLANE;
+        bf16x8 a[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int o = xs_off(wr * 64 + i * 32 + col, half);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * XS_PLANE + o);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int o = xs_off(wc * 128 + j * 32 + col, half);
+            bf16x8 bb[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) bb[pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * XS_PLANE + o);
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0, 0, 0);
+        }
+    };
+    auto step = [&](int g, XpGemmRegs& nxt) {
+        compute(g & 1);
+        if (g + 1 < T) sstore(nxt, (g + 1) & 1);
+        if (g + 3 < T) gload(nxt, g + 3);
+        __syncthreads();
+    };
+    XpGemmRegs R0, R1;
+    gload(R0, 0);
+    if (T > 1) gload(R1, 1);
+    sstore(R0, 0);
+    if (T > 2) gload(R0, 2);
+    __syncthreads();
+    int g = 0;
+    for (; g + 1 < T; g += 2) {
+        step(g, R1);
+        step(g + 1, R0);
+    }
+    if (g < T) step(g, R1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int gn = n0 + wc * 128 + j * 32 + col;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = m0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (gm < M && gn < N) C[(int64_t)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
 }  // namespace
 
 int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
@@ -560,6 +703,28 @@ int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N,
     const int64_t tiles = (int64_t)((M + XBM - 1) / XBM) * ((N + XBM - 1) / XBM);
     hipLaunchKernelGGL(gemm_nt_f32x3_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, st, A, B, C, M, N, K, lda, ldb,
                        ldc);
+    return 0;
+}
+
+int launch_split3_planes(const float* X, int64_t rows, int64_t cols, int64_t ld, void* planes, int64_t plane_rows,
+                         hipStream_t st) {
+    const int kp = (int)((cols + 15) / 16 * 16);
+    const int64_t q = rows * (kp / 4);
+    hipLaunchKernelGGL(split3_planes_kernel, dim3((unsigned)((q + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, X, rows,
+                       (int)cols, ld, kp, static_cast<__bf16*>(planes), plane_rows * kp);
+    return 0;
+}
+
+int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, float* C, int64_t ldc,
+                       int M, int N, hipStream_t st) {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
+    (void)attr;
+    const int kp = (int)((K + 15) / 16 * 16);
+    const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
+    hipLaunchKernelGGL(gemm_nt_x3p_kernel, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st,
+                       static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp, C, M,
+                       N, ldc);
     return 0;
 }
 

@@ -219,6 +219,10 @@ int launch_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K
                    int64_t ldc, hipStream_t st);
 int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
                          int64_t ldc, hipStream_t st, int form = 0);
+int launch_split3_planes(const float* X, int64_t rows, int64_t cols, int64_t ld, void* planes, int64_t plane_rows,
+                         hipStream_t st);
+int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, float* C, int64_t ldc,
+                       int M, int N, hipStream_t st);
 int launch_rank(const float* S, int64_t M, int64_t N, int64_t ld, const int64_t* truth, const int64_t* fptr,
                 const int64_t* fids, int64_t* ranks, hipStream_t st);
 

@@ -47,8 +47,36 @@ def build_filter(queries: np.ndarray, mode: str, all_true_triples) -> tuple[np.n
     return ptr, ids
 
 
-def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor | None = None) -> torch.Tensor:
-    """[B, E] scores of every entity as the candidate (head-batch or tail-batch)."""
+def split_planes(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """x [rows, K] fp32 as three bf16 planes (kge_split_bf16x3: uint8 storage of [3][rows][K rounded to 16]),
+    the operand form of kge_gemm_nt_bf16x3_planes."""
+    lib = _lib.load()
+    rows, K = x.shape
+    nbytes = int(lib.kge_split_bf16x3_bytes(rows, K))
+    if out is None or out.numel() < nbytes:
+        out = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
+    check(lib.kge_split_bf16x3(x.data_ptr(), rows, K, x.stride(0), out.data_ptr(), rows,
+                               torch.cuda.current_stream(x.device).cuda_stream), "kge_split_bf16x3")
+    return out
+
+
+def entity_planes(model) -> torch.Tensor | None:
+    """The entity table's bf16 planes for one evaluation pass (DistMult / ComplEx), made once and passed to
+    every score_all call of the pass: the table does not change while it is evaluated. None for the other
+    score functions."""
+    if model.model_name not in MFMA_FNS:
+        return None
+    return split_planes(model.entity_embedding.detach())
+
+
+_Q_PLANES = {}
+
+
+def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor | None = None,
+              planes: torch.Tensor | None = None) -> torch.Tensor:
+    """[B, E] scores of every entity as the candidate (head-batch or tail-batch). DistMult / ComplEx: pass
+    `planes` = entity_planes(model), made once per evaluation pass (without it the call splits the table
+    itself: kge_gemm_nt_bf16x3, the operands split at staging)."""
     m = ops.mode_id(mode)
     ent, rel = model.entity_embedding.detach(), model.relation_embedding.detach()
     B, E = positive_sample.shape[0], ent.shape[0]
@@ -74,9 +102,16 @@ def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor
         check(lib.kge_eval_query(FN_IDS[model.model_name], m, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(),
                                  rel.shape[0], rel.stride(0), positive_sample.data_ptr(), B, model._D, Q.data_ptr(),
                                  Q.stride(0), st), "kge_eval_query")
-        # S = Q . E^T at fp32 accuracy on the bf16 matrix cores (bf16x3 split in registers, six products)
-        check(lib.kge_gemm_nt_bf16x3(Q.data_ptr(), Q.stride(0), ent.data_ptr(), ent.stride(0), out.data_ptr(),
-                                     out.stride(0), B, E, K, st), "kge_gemm_nt_bf16x3")
+        # S = Q . E^T at fp32 accuracy on the bf16 matrix cores (bf16x3 terms, six products): from the pass's
+        # entity planes and the batch's query planes, or with the operands split at staging
+        if planes is not None:
+            key = (str(dev), st)
+            qp = _Q_PLANES[key] = split_planes(Q, _Q_PLANES.get(key))
+            check(lib.kge_gemm_nt_bf16x3_planes(qp.data_ptr(), B, planes.data_ptr(), E, K, out.data_ptr(),
+                                                out.stride(0), B, E, st), "kge_gemm_nt_bf16x3_planes")
+        else:
+            check(lib.kge_gemm_nt_bf16x3(Q.data_ptr(), Q.stride(0), ent.data_ptr(), ent.stride(0), out.data_ptr(),
+                                         out.stride(0), B, E, K, st), "kge_gemm_nt_bf16x3")
         return out
     cand = torch.arange(E, device=dev, dtype=torch.int64).unsqueeze(0).expand(B, E)  # row stride 0
     modulus = float(model.modulus.detach().reshape(-1)[0]) if model.model_name == "pRotatE" else 0.0
@@ -161,13 +196,14 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
         triples = triples[dist.get_rank()::world]
     all_ranks = []
     with torch.no_grad():
+        planes = entity_planes(model)  # once per evaluation pass (DistMult / ComplEx)
         for mode in ("head-batch", "tail-batch"):
             col = 0 if mode == "head-batch" else 2
             ptr, ids = build_filter(triples, mode, all_true_triples)
             for s in range(0, len(triples), bs):
                 q = triples[s:s + bs]
                 pos = torch.from_numpy(q).to(dev)
-                S = score_all(model, pos, mode)
+                S = score_all(model, pos, mode, planes=planes)
                 p = ptr[s:s + len(q) + 1]
                 fptr = torch.from_numpy(p - p[0]).to(dev)
                 fids = torch.from_numpy(ids[p[0]:p[-1]]).to(dev)
@@ -180,5 +216,5 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
     return metrics_from_ranks(ranks)
 
 
-__all__ = ["build_filter", "score_all", "rank_filtered", "metrics_from_ranks", "test_step", "HEAD_BATCH",
-           "TAIL_BATCH"]
+__all__ = ["build_filter", "score_all", "rank_filtered", "metrics_from_ranks", "test_step", "entity_planes",
+           "split_planes", "HEAD_BATCH", "TAIL_BATCH"]

@@ -50,7 +50,7 @@ def _run_test_step_with_oracle():
     test = true[:9]
     ent, rel = m.entity_embedding.detach().double(), m.relation_embedding.detach().double()
 
-    def score_all(model, pos, mode, out=None):
+    def score_all(model, pos, mode, out=None, planes=None):
         cand = torch.arange(E, dtype=torch.int64).unsqueeze(0).expand(pos.shape[0], E)
         return O.score("TransE", ent, rel, pos, cand, mode, 6.0)
 

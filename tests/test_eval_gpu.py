@@ -175,3 +175,42 @@ def test_gemm_split_once_is_bitwise_the_register_split_kernel(monkeypatch, M, N,
         out.append(C.cpu())
     assert torch.equal(out[0], out[1])
     assert bool((out[1][:, N:] == -7.0).all())  # nothing written past N
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 4), (37, 300, 64), (257, 513, 1000), (300, 131, 12), (64, 14951, 1000),
+                                   (129, 77, 37)])
+def test_gemm_on_presplit_planes_is_bitwise_the_staging_split(M, N, K):
+    """kge_split_bf16x3 + kge_gemm_nt_bf16x3_planes (operands split before the GEMM into three bf16 planes, K padded
+    to 16 with zeros; no conversion in the GEMM's loop) against kge_gemm_nt_bf16x3 (split at staging): C bitwise
+    equal, partial tiles in M and N, K not a multiple of 16 (and of 4: the staging form's register-split fallback),
+    a padded leading dimension of C; nothing written past N."""
+    g = torch.Generator().manual_seed(M + 7 * N + K)
+    A = (torch.randn(M, K, generator=g) * torch.logspace(-2, 2, K)).to(DEV)
+    Bm = torch.randn(N, K, generator=g).to(DEV)
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    want = torch.full((M, N + 3), -7.0, device=DEV)
+    assert lib.kge_gemm_nt_bf16x3(A.data_ptr(), K, Bm.data_ptr(), K, want.data_ptr(), N + 3, M, N, K, st) == 0
+    ap, bp = evaluate.split_planes(A), evaluate.split_planes(Bm)
+    got = torch.full((M, N + 3), -7.0, device=DEV)
+    assert lib.kge_gemm_nt_bf16x3_planes(ap.data_ptr(), M, bp.data_ptr(), N, K, got.data_ptr(), N + 3, M, N, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    assert bool((got[:, N:] == -7.0).all())
+
+
+def test_score_all_with_entity_planes_is_bitwise_the_per_call_split():
+    """evaluate.score_all with the pass's entity planes (evaluate.entity_planes, made once per test_step) gives the
+    scores of the call that splits the operands itself, bitwise, for DistMult and ComplEx in both modes."""
+    for name, de in (("DistMult", False), ("ComplEx", True)):
+        m = kge.KGEModel(name, 900, 7, 96, 12.0, double_entity_embedding=de, double_relation_embedding=de,
+                         device=DEV, seed=3)
+        g = torch.Generator().manual_seed(1)
+        pos = torch.stack([torch.randint(0, 900, (70,), generator=g), torch.randint(0, 7, (70,), generator=g),
+                           torch.randint(0, 900, (70,), generator=g)], 1).to(DEV)
+        planes = evaluate.entity_planes(m)
+        for mode in ("head-batch", "tail-batch"):
+            a = evaluate.score_all(m, pos, mode).clone()
+            b = evaluate.score_all(m, pos, mode, planes=planes)
+            torch.cuda.synchronize()
+            assert torch.equal(a, b), (name, mode)

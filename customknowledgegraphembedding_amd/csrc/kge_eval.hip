@@ -546,10 +546,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
 // (PMC, profiles/r05_pmc_c5.json: the matrix cores busy 0.60 of the kernel, co-issuing with that VALU work 20 %
 // of the time). The operands of the all-entity scores are reused: the entity table across every query batch of
 // an evaluation pass, the query block across the 59 entity tiles. split3_planes_kernel writes each fp32 matrix as
-// three bf16 planes [3][rows][kp] (xs_split3's arithmetic, kp = K rounded up to 16, zero padded), and
-// gemm_nt_x3p_kernel stages the planes' 16-B pieces into the same LDS images with no conversion: the products,
-// their order and C are bitwise gemm_nt_x3s_kernel's.
+// three bf16 planes (xs_split3's arithmetic, K rounded up to 16 with zeros), each plane k-chunk-major
+// [K / 16][rows][16]: a block's 16-k chunk of 256 rows is 8 KB contiguous per plane, loaded in whole lines (a
+// row-major [rows][K] plane gave each row's 32 B of a chunk its own 128-B line: 4x the L2 traffic, slower than
+// staging from fp32). gemm_nt_x3p_kernel stages the pieces into the same LDS images with no conversion: the
+// products, their order and C are bitwise gemm_nt_x3s_kernel's.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t rows_pad(int64_t plane, int kp) { return plane / kp; }
+
 __global__ __launch_bounds__(kBlock) void split3_planes_kernel(const float* __restrict__ X, int64_t rows, int cols,
                                                                int64_t ld, int kp, __bf16* __restrict__ P,
                                                                int64_t plane) {
@@ -568,7 +572,7 @@ __global__ __launch_bounds__(kBlock) void split3_planes_kernel(const float* __re
     }
     xs_bf16x4 s0, s1, s2;
     xs_split3(v, s0, s1, s2);
-    __bf16* d = P + r * kp + k;
+    __bf16* d = P + ((int64_t)(k >> 4) * rows_pad(plane, kp) + r) * 16 + (k & 15);
     *reinterpret_cast<xs_bf16x4*>(d) = s0;
     *reinterpret_cast<xs_bf16x4*>(d + plane) = s1;
     *reinterpret_cast<xs_bf16x4*>(d + 2 * plane) = s2;
@@ -596,19 +600,20 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
     const int m0 = tm * XS_T, n0 = tn * XS_T;
     const rsrc_t ra = make_rsrc(Ap, (uint32_t)(3 * a_plane * 2));
     const rsrc_t rb = make_rsrc(Bp, (uint32_t)(3 * b_plane * 2));
-    // thread t stages row t >> 1, k half t & 1 of every plane: its byte offsets advance 32 B per chunk
+    // thread t stages row t >> 1, k half t & 1 of every plane; a plane is [K / 16][plane rows][16], so chunk g of
+    // the block's rows is contiguous and the offsets advance one chunk slab (plane rows x 32 B) per chunk
     const int srow = t >> 1, sh = t & 1;
-    const uint32_t oa0 = m0 + srow < M ? (uint32_t)(((int64_t)(m0 + srow) * kp + 8 * sh) * 2) : XS_OOB;
-    const uint32_t ob0 = n0 + srow < N ? (uint32_t)(((int64_t)(n0 + srow) * kp + 8 * sh) * 2) : XS_OOB;
+    const uint32_t oa0 = m0 + srow < M ? (uint32_t)(((int64_t)(m0 + srow) * 16 + 8 * sh) * 2) : XS_OOB;
+    const uint32_t ob0 = n0 + srow < N ? (uint32_t)(((int64_t)(n0 + srow) * 16 + 8 * sh) * 2) : XS_OOB;
     const uint32_t pa = (uint32_t)(a_plane * 2), pb = (uint32_t)(b_plane * 2);
+    const uint32_t sa = (uint32_t)(a_plane / kp * 32), sb = (uint32_t)(b_plane / kp * 32);  // one chunk slab
     const int so = xs_off(srow, sh);
     const int T = kp / 16;
     auto gload = [&](XpGemmRegs& R, int g) {
-        const uint32_t dk = (uint32_t)g * 32u;
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-            const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa0 == XS_OOB ? XS_OOB : oa0 + p * pa + dk, 0, 0);
-            const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rb, ob0 == XS_OOB ? XS_OOB : ob0 + p * pb + dk, 0, 0);
+            const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa0 == XS_OOB ? XS_OOB : oa0 + p * pa + g * sa, 0, 0);
+            const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rb, ob0 == XS_OOB ? XS_OOB : ob0 + p * pb + g * sb, 0, 0);
             R.a[p] = make_int4(va[0], va[1], va[2], va[3]);
             R.b[p] = make_int4(vb[0], vb[1], vb[2], vb[3]);
         }

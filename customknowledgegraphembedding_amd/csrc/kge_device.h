@@ -960,6 +960,7 @@ __device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
     const int Np = a.mode == KGE_HEAD_BATCH ? (int)a.N : (int)a.N + 1;
     const int nf = nr * Np;
     const int64_t S = (a.nent + 7) / 8;
+    const int S32 = (int)S;  // nent < 2^31 (kge_step_plan_size): slice math in 32 bits
     const float invS = 1.f / (float)S, bscale = (float)kTileBuckets / (float)S, inv_np = 1.f / (float)Np;
     // an item's id, by address select and one load (no branch: a walk's loads all go out together)
     auto item_row = [&](int f, int& r) {
@@ -974,13 +975,12 @@ __device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
     auto classify = [&](int f, int r, int64_t id, int& key, int& idc, int& code) {
         const int n = f - r * Np;
         const bool valid = id >= 0 && id < a.nent;
-        int x = 0, bk = 0;
-        if (valid) {
-            x = min(7, (int)((float)id * invS));
-            if ((int64_t)x * S > id) --x;
-            if ((int64_t)(x + 1) * S <= id) ++x;
-            bk = min(kTileBuckets - 1, (int)((float)(int)(id - (int64_t)x * S) * bscale));
-        }
+        const int i32 = valid ? (int)id : 0;
+        int x = min(7, (int)((float)i32 * invS));  // the products below stay <= 7 S < 2^31
+        if (x * S32 > i32) --x;
+        if (x < 7 && (x + 1) * S32 <= i32) ++x;
+        const int bk = valid ? min(kTileBuckets - 1, (int)((float)(i32 - x * S32) * bscale)) : 0;
+        if (!valid) x = 0;
         key = x * kTileBuckets + bk;
         idc = valid ? (int)id : -1;
         code = (r << 16) | n;

@@ -56,5 +56,13 @@ def standalone(i):
 
 
 res["planned_standalone"] = timed(standalone)
+
+
+def plan_only(i):
+    pos, neg = batches[i % len(batches)]
+    sp.plan(pos, neg, i % 2)
+
+
+res["plan_kernel_alone"] = timed(plan_only)
 res["workload"] = w["name"]
 print(json.dumps(res), flush=True)

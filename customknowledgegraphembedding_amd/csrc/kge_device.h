@@ -992,7 +992,7 @@ __device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
     };
     constexpr int TPI = 17;  // C2's 16 x 257 items over 768 threads walked once; larger groups twice
     const bool in_regs = nf <= TPI * NT;
-    int ky[TPI], ic[TPI], cd[TPI];
+    int ky[TPI], ic[TPI], cd[TPI], rk[TPI];
     // the rows' positives (b, h, r, t), loaded with the walk's ids (one round trip), stored at the end
     int64_t ph = -1, pr = -1, pt = -1;
     if (t < nr) {
@@ -1012,9 +1012,10 @@ __device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
             ky[u] = -1;
             if (f < nf) classify(f, rr[u], idv[u], ky[u], ic[u], cd[u]);
         }
+        // the counting atomic's old value is the item's rank in its bin: the scatter then needs no second atomic
 #pragma unroll
         for (int u = 0; u < TPI; ++u)
-            if (ky[u] >= 0) atomicAdd(&hist[ky[u]], 1);
+            if (ky[u] >= 0) rk[u] = atomicAdd(&hist[ky[u]], 1);
     } else {
         for (int f = t; f < nf; f += NT) {
             int k, i, c;
@@ -1050,12 +1051,9 @@ __device__ void tile_plan_group(const PlanArgs& a, int g, int* sm) {
     __syncthreads();
     int2* list = reinterpret_cast<int2*>(a.plan + plan_list(a.B, R)) + (int64_t)g * R * (a.N + 1);
     if (in_regs) {
-        int at[TPI];
-#pragma unroll
-        for (int u = 0; u < TPI; ++u) at[u] = ky[u] >= 0 ? atomicAdd(&hist[ky[u]], 1) : -1;
 #pragma unroll
         for (int u = 0; u < TPI; ++u)
-            if (at[u] >= 0) list[at[u]] = make_int2(ic[u], cd[u]);
+            if (ky[u] >= 0) list[hist[ky[u]] + rk[u]] = make_int2(ic[u], cd[u]);
     } else {
         for (int f = t; f < nf; f += NT) {
             int k, i, c;
@@ -1328,11 +1326,12 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
             }
         }
     }
+    int wrk[TPI];  // the item's rank in its bucket, from the counting atomic (no second atomic in the scatter)
     if (pl) {
     } else if (in_regs) {
 #pragma unroll
         for (int u = 0; u < TPI; ++u)
-            if (wbk[u] >= 0) atomicAdd(&hist[wbk[u]], 1);
+            if (wbk[u] >= 0) wrk[u] = atomicAdd(&hist[wbk[u]], 1);
     } else {
         for (int64_t f = t; f < nf; f += NT) {
             int bk, code;
@@ -1376,12 +1375,9 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     __syncthreads();
     if (pl) {
     } else if (in_regs) {
-        int at[TPI];
-#pragma unroll
-        for (int u = 0; u < TPI; ++u) at[u] = wbk[u] >= 0 ? atomicAdd(&hist[wbk[u]], 1) : -1;
 #pragma unroll
         for (int u = 0; u < TPI; ++u)
-            if (at[u] >= 0) list[at[u]] = wcd[u];
+            if (wbk[u] >= 0) list[hist[wbk[u]] + wrk[u]] = wcd[u];
     } else {
         for (int64_t f = t; f < nf; f += NT) {
             int bk, code;

@@ -1288,7 +1288,7 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         }
         if (lane == 0) rrow[r] = rok ? ri : -1;
     };
-    if constexpr (NWV <= 12) {  // waves with two rows build both side by side (one load latency; at 16 waves it spills)
+    if constexpr (2 * NWV <= kTileMaxRows) {
         for (int r = w; r < nr; r += 2 * NWV) {
             const int r2 = r + NWV < nr ? r + NWV : r;
             Query<FN, CH, V, G> qa, qb;

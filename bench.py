@@ -951,8 +951,8 @@ def transparse_bench(w, a, device):
     dt = time.perf_counter() - t0
     k_s = statistics.mean(e0.elapsed_time(e1) for e0, e1 in evs) / 1e3
     flops = 2.0 * B * N * d * d
-    # the forward runs the bf16x3 form unless KGE_TS_F32=1 (float4 rows: d % 4 == 0, aligned tables)
-    x3 = os.environ.get("KGE_TS_F32") != "1" and d % 4 == 0
+    # the default forms run the bf16x3 forward (float4 rows: d % 4 == 0, aligned tables)
+    x3 = d % 4 == 0
     dp = (d + 127) // 128 * 128  # columns in 128-wide tiles, K in 32-deep chunks: both padded to 128 here
     mfma_flops = 6 * 2.0 * B * N * dp * ((d + 31) // 32 * 32)
     train = None
@@ -994,13 +994,8 @@ def transparse_bench(w, a, device):
 
 
 def ts_kernel_name():
-    """The head-batch TranSparse forward kernel launch_rows<TS_FWD> picks (kge_transparse.hip) under the A/B
-    knobs KGE_TS_BIG and KGE_TS_X3S."""
-    if os.environ.get("KGE_TS_BIG", "1") == "0":
-        return "ts_rows_kernel<TS_FWD, 4, true> (128-row blocks, bf16x3 on the bf16 MFMA)"
-    if os.environ.get("KGE_TS_X3S", "1") == "0":
-        return ("ts_fwd_x3_kernel (256 negatives of one batch row per block; bf16x3 split in registers, six products "
-                "on v_mfma_f32_32x32x16_bf16)")
+    """The head-batch TranSparse forward kernel the default forms select (kge_transparse.hip launch_rows<TS_FWD>:
+    d % 4 == 0, aligned tables, d <= 1024)."""
     return ("ts_fwd_x3s_kernel (256 negatives of one batch row per block, M_r chunks staged once for all of them; "
             "operands split once at staging into bf16 planes, six products on v_mfma_f32_32x32x16_bf16, fp32 "
             "accumulation)")

@@ -509,17 +509,20 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0, 0, 0);
         }
     };
+    // the loads are issued unconditionally (a chunk past K reads zeros through the out-of-range offset): with no
+    // branch around a load, the wait before a store to LDS leaves the younger set's loads in flight (a
+    // conditional load made it wait for every load, the pipeline one chunk deep)
     auto step = [&](int g, XsGemmRegs& nxt) {
         compute(g & 1);
         if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-        if (g + 3 < T) gload(nxt, g + 3);
+        gload(nxt, g + 3);
         __syncthreads();
     };
     XsGemmRegs R0, R1;
     gload(R0, 0);
-    if (T > 1) gload(R1, 1);
+    gload(R1, 1);
     sstore(R0, 0);
-    if (T > 2) gload(R0, 2);
+    gload(R0, 2);
     __syncthreads();
     int g = 0;
     for (; g + 1 < T; g += 2) {
@@ -609,11 +612,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
     const uint32_t sa = (uint32_t)(a_plane / kp * 32), sb = (uint32_t)(b_plane / kp * 32);  // one chunk slab
     const int so = xs_off(srow, sh);
     const int T = kp / 16;
-    auto gload = [&](XpGemmRegs& R, int g) {
+    auto gload = [&](XpGemmRegs& R, int g) {  // unconditional (gemm_nt_x3s_kernel's): a chunk past K reads zeros
+        const bool ina = oa0 != XS_OOB && g < T, inb = ob0 != XS_OOB && g < T;
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-            const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa0 == XS_OOB ? XS_OOB : oa0 + p * pa + g * sa, 0, 0);
-            const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rb, ob0 == XS_OOB ? XS_OOB : ob0 + p * pb + g * sb, 0, 0);
+            const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, ina ? oa0 + p * pa + g * sa : XS_OOB, 0, 0);
+            const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rb, inb ? ob0 + p * pb + g * sb : XS_OOB, 0, 0);
             R.a[p] = make_int4(va[0], va[1], va[2], va[3]);
             R.b[p] = make_int4(vb[0], vb[1], vb[2], vb[3]);
         }
@@ -660,14 +664,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
     auto step = [&](int g, XpGemmRegs& nxt) {
         compute(g & 1);
         if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-        if (g + 3 < T) gload(nxt, g + 3);
+        gload(nxt, g + 3);
         __syncthreads();
     };
     XpGemmRegs R0, R1;
     gload(R0, 0);
-    if (T > 1) gload(R1, 1);
+    gload(R1, 1);
     sstore(R0, 0);
-    if (T > 2) gload(R0, 2);
+    gload(R0, 2);
     __syncthreads();
     int g = 0;
     for (; g + 1 < T; g += 2) {

@@ -886,6 +886,7 @@ struct XsRegs {
     float4 a[2], b[2], m[2];
 };
 
+template <bool MASK>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(2))) void
 ts_fwd_x3s_kernel(TsParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char xs_smem[];  // 2 stages, then u - 1 (d floats)
@@ -942,10 +943,10 @@ ts_fwd_x3s_kernel(TsParams p) {
     __syncthreads();
     // buffer descriptors: the entity table (rows by per-lane offset) and the relation's d x d matrix
     const rsrc_t ra = make_rsrc(p.ent, (uint32_t)(p.nent * p.ent_ld * 4));
-    const float* Wr = rok ? (p.Mpre ? p.Mpre : p.W) + r * (int64_t)d * d : p.W;
+    const float* Wr = rok ? (MASK ? p.W : p.Mpre) + r * (int64_t)d * d : p.W;
     const uint32_t mbytes = rok ? (uint32_t)((int64_t)d * d * 4) : 0u;
     const rsrc_t rw = make_rsrc(Wr, mbytes);
-    const bool fuse_mask = !p.Mpre;
+    constexpr bool fuse_mask = MASK;  // M_r = W_r * mask_r formed at staging (else p.Mpre holds the products)
     const rsrc_t rm = make_rsrc(fuse_mask && rok ? p.mask + r * (int64_t)d * d : p.W, fuse_mask ? mbytes : 0u);
     // this thread's staging slots: A rows (t >> 2) + 128 u, k quad t & 3; B k pair t & 7 (+u), columns 4 (t >> 3)
     int aid[2];
@@ -954,16 +955,19 @@ ts_fwd_x3s_kernel(TsParams p) {
     const int aq = t & 3, bkp = t & 7, bjq = t >> 3;
     const int nk = (d + 15) / 16, nct = (d + XBC - 1) / XBC, T = nk * nct;
 
+    // every load is issued unconditionally (a chunk past the end reads zeros through the out-of-range offset):
+    // with no branch around a load the wait before a store to LDS counts exactly the younger set's loads
     auto gload = [&](XsRegs& R, int g) {
+        const bool in = g < T;
         const int ct = g / nk, k0 = (g - ct * nk) * 16;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int ka = k0 + 4 * aq;
+            const int ka = in ? k0 + 4 * aq : d;
             const uint32_t oa = (aid[u] >= 0 && ka < d) ? (uint32_t)(((int64_t)aid[u] * p.ent_ld + ka) * 4) : kXsOOB;
             const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa, 0, 0);
             R.a[u] = make_float4(__uint_as_float(va[0]), __uint_as_float(va[1]), __uint_as_float(va[2]),
                                  __uint_as_float(va[3]));
-            const int kb = k0 + 2 * bkp + u, j = ct * XBC + 4 * bjq;
+            const int kb = in ? k0 + 2 * bkp + u : d, j = ct * XBC + 4 * bjq;
             const uint32_t ob = (kb < d && j < d) ? (uint32_t)(((int64_t)kb * d + j) * 4) : kXsOOB;
             const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rw, ob, 0, 0);
             R.b[u] = make_float4(__uint_as_float(vb[0]), __uint_as_float(vb[1]), __uint_as_float(vb[2]),
@@ -1070,7 +1074,7 @@ ts_fwd_x3s_kernel(TsParams p) {
     auto step = [&](int g, XsRegs& nxt) {
         compute(g & 1);
         if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-        if (g + 3 < T) gload(nxt, g + 3);
+        gload(nxt, g + 3);
         if ((g + 1) % nk == 0) {
             fold(g / nk);
             zero_acc();
@@ -1080,9 +1084,9 @@ ts_fwd_x3s_kernel(TsParams p) {
     XsRegs R0, R1;
     zero_acc();
     gload(R0, 0);
-    if (T > 1) gload(R1, 1);
+    gload(R1, 1);
     sstore(R0, 0);
-    if (T > 2) gload(R0, 2);
+    gload(R0, 2);
     __syncthreads();
     int g = 0;
     for (; g + 1 < T; g += 2) {
@@ -1113,7 +1117,7 @@ ts_fwd_x3s_kernel(TsParams p) {
 // order: the products are ts_rows_kernel's, the column sums in another order (scores within fp32 rounding).
 // ---------------------------------------------------------------------------------------------
 // Column split (round 5): with the whole column range per block only one block per relation works (~12 CUs at
-// C6); ts_fwd_x3g_kernel<4, 1> gives a block 4 waves x 32 columns = 128 columns of its rows, the xsplit blocks of
+// C6); ts_fwd_x3g_kernel<4, 1, 2, MASK> gives a block 4 waves x 32 columns = 128 columns of its rows, the xsplit blocks of
 // a row chunk together all of them, and writes its per-row sums (over its waves, in wave order) to the
 // workspace; ts_x3g_finish_kernel adds the splits in order: deterministic, scores within fp32 rounding of the
 // one-block form.
@@ -1124,17 +1128,24 @@ constexpr int kXgStage = 3 * (kXgAPlane + kXgBPlane);
 constexpr int xg_bplane(int NWV, int JPW) { return NWV * JPW * 32 * 32; }
 constexpr int xg_stage(int NWV, int JPW) { return 3 * (kXgAPlane + xg_bplane(NWV, JPW)); }
 
-template <int JPW>
+// the column-split form's block: 4 waves x 32 columns, two register sets (chunks loaded two steps ahead). Deeper
+// prefetch (4 / 6 sets) and 2-wave 64-column blocks measured no faster (profiles/r05_ts_xg_ab.txt): a step costs
+// ~1.3 us whatever its width, with or without the loads' latency exposed.
+constexpr int kXgSplitWaves = 4, kXgSplitCols = 32 * kXgSplitWaves, kXgSplitDepth = 2;
+
+template <int JPW, int AP>
 struct XgRegs {
-    float4 a, b[JPW][2], m[JPW][2];
+    float4 a[AP], b[JPW][2], m[JPW][2];
 };
 
-template <int NWV, int JPW>
+template <int NWV, int JPW, int DEP, bool MASK>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, NWV * kWave), amdgpu_waves_per_eu(2))) void
 ts_fwd_x3g_kernel(TsParams p) {
     constexpr int NT = NWV * kWave, CW = NWV * JPW * 32;  // threads, columns per pass
     constexpr int BPL = xg_bplane(NWV, JPW), STG = xg_stage(NWV, JPW);
-    static_assert(NT >= 4 * XGR, "one A float4 per thread");
+    constexpr int AP = NT >= 4 * XGR ? 1 : 4 * XGR / NT;  // A float4 per thread per step
+    static_assert(AP * NT == 4 * XGR || NT >= 4 * XGR, "A tile staging");
+    using Regs = XgRegs<JPW, AP>;
     extern __shared__ __attribute__((aligned(16))) unsigned char xg_smem[];  // 2 stages, then u - 1 (d floats)
     __shared__ int rb[XGR], rid[XGR];
     __shared__ float2 part[NWV][XGR];
@@ -1217,27 +1228,38 @@ ts_fwd_x3g_kernel(TsParams p) {
     }
     __syncthreads();
     const rsrc_t ra = make_rsrc(p.ent, (uint32_t)(p.nent * p.ent_ld * 4));
-    const float* Wr = rok ? (p.Mpre ? p.Mpre : p.W) + r * (int64_t)d * d : p.W;
+    const float* Wr = rok ? (MASK ? p.W : p.Mpre) + r * (int64_t)d * d : p.W;
     const uint32_t mbytes = rok ? (uint32_t)((int64_t)d * d * 4) : 0u;
     const rsrc_t rw = make_rsrc(Wr, mbytes);
-    const bool fuse_mask = !p.Mpre;
+    constexpr bool fuse_mask = MASK;  // M_r = W_r * mask_r formed at staging (else p.Mpre holds the products)
     const rsrc_t rm = make_rsrc(fuse_mask && rok ? p.mask + r * (int64_t)d * d : p.W, fuse_mask ? mbytes : 0u);
-    const int aid = t < 4 * XGR ? rid[t >> 2] : -1, aq = t & 3, bkp = t & 7, bjq = t >> 3;
+    int aid[AP];
+#pragma unroll
+    for (int u = 0; u < AP; ++u) aid[u] = t + u * NT < 4 * XGR ? rid[(t + u * NT) >> 2] : -1;
+    const int aq = t & 3, bkp = t & 7, bjq = t >> 3;
     // one-block form: every pass of CW columns; split form: the one pass of columns [split CW, split CW + CW)
     const int nk = (d + 15) / 16, npass = xs > 1 ? 1 : (d + CW - 1) / CW, T = nk * npass;
     const int col0 = xs > 1 ? split * CW : 0;
 
-    auto gload = [&](XgRegs<JPW>& R, int g) {
+    // every load is issued unconditionally (a chunk past the end reads zeros through the out-of-range offset):
+    // with no branch around a load the wait before a store to LDS counts exactly the younger sets' loads
+    auto gload = [&](Regs& R, int g) {
+        const bool in = g < T;
         const int pc = g / nk, k0 = (g - pc * nk) * 16;
-        const int ka = k0 + 4 * aq;
-        const uint32_t oa = (aid >= 0 && ka < d) ? (uint32_t)(((int64_t)aid * p.ent_ld + ka) * 4) : kXsOOB;
-        const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa, 0, 0);
-        R.a = make_float4(__uint_as_float(va[0]), __uint_as_float(va[1]), __uint_as_float(va[2]), __uint_as_float(va[3]));
+        const int ka = in ? k0 + 4 * aq : d;
+#pragma unroll
+        for (int u = 0; u < AP; ++u) {
+            const uint32_t oa =
+                (aid[u] >= 0 && ka < d) ? (uint32_t)(((int64_t)aid[u] * p.ent_ld + ka) * 4) : kXsOOB;
+            const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa, 0, 0);
+            R.a[u] = make_float4(__uint_as_float(va[0]), __uint_as_float(va[1]), __uint_as_float(va[2]),
+                                 __uint_as_float(va[3]));
+        }
 #pragma unroll
         for (int u = 0; u < JPW; ++u)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int kb = k0 + 2 * bkp + h, j = col0 + pc * CW + 4 * (bjq + (NT / 8) * u);
+                const int kb = in ? k0 + 2 * bkp + h : d, j = col0 + pc * CW + 4 * (bjq + (NT / 8) * u);
                 const uint32_t ob = (kb < d && j < d) ? (uint32_t)(((int64_t)kb * d + j) * 4) : kXsOOB;
                 const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rw, ob, 0, 0);
                 R.b[u][h] = make_float4(__uint_as_float(vb[0]), __uint_as_float(vb[1]), __uint_as_float(vb[2]),
@@ -1249,18 +1271,20 @@ ts_fwd_x3g_kernel(TsParams p) {
                 }
             }
     };
-    auto sstore = [&](const XgRegs<JPW>& R, int stage) {
+    auto sstore = [&](const Regs& R, int stage) {
         unsigned char* A = xg_smem + stage * STG;
         unsigned char* Bp = A + 3 * kXgAPlane;
-        if (t < 4 * XGR) {
-            const int row = t >> 2;
-            bf16x4_t s0, s1, s2;
-            split3_x4(f32x4_t{R.a.x, R.a.y, R.a.z, R.a.w}, s0, s1, s2);
-            const int o = xs_off(row, aq >> 1) + (aq & 1) * 8;
-            *reinterpret_cast<bf16x4_t*>(A + o) = s0;
-            *reinterpret_cast<bf16x4_t*>(A + kXgAPlane + o) = s1;
-            *reinterpret_cast<bf16x4_t*>(A + 2 * kXgAPlane + o) = s2;
-        }
+#pragma unroll
+        for (int u = 0; u < AP; ++u)
+            if (t + u * NT < 4 * XGR) {
+                const int row = (t + u * NT) >> 2;
+                bf16x4_t s0, s1, s2;
+                split3_x4(f32x4_t{R.a[u].x, R.a[u].y, R.a[u].z, R.a[u].w}, s0, s1, s2);
+                const int o = xs_off(row, aq >> 1) + (aq & 1) * 8;
+                *reinterpret_cast<bf16x4_t*>(A + o) = s0;
+                *reinterpret_cast<bf16x4_t*>(A + kXgAPlane + o) = s1;
+                *reinterpret_cast<bf16x4_t*>(A + 2 * kXgAPlane + o) = s2;
+            }
 #pragma unroll
         for (int u = 0; u < JPW; ++u) {
             float4 b0 = R.b[u][0], b1 = R.b[u][1];
@@ -1342,29 +1366,33 @@ ts_fwd_x3g_kernel(TsParams p) {
             red[t] = x;
         }
     };
-    auto step = [&](int g, XgRegs<JPW>& nxt) {
+    // DEP register sets: chunk c is held in set c % DEP from its load until its store to LDS, so a chunk's
+    // loads are issued DEP steps before the step that stores it
+    auto step = [&](int g, Regs& nxt) {
         compute(g & 1);
         if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-        if (g + 3 < T) gload(nxt, g + 3);
+        gload(nxt, g + 1 + DEP);
         if ((g + 1) % nk == 0) {
             fold(g / nk);
             zero_acc();
         }
         __syncthreads();
     };
-    XgRegs<JPW> R0, R1;
+    Regs R[DEP];
     zero_acc();
-    gload(R0, 0);
-    if (T > 1) gload(R1, 1);
-    sstore(R0, 0);
-    if (T > 2) gload(R0, 2);
+#pragma unroll
+    for (int c = 0; c < DEP; ++c) gload(R[c], c);
+    sstore(R[0], 0);
+    gload(R[0], DEP);
     __syncthreads();
     int g = 0;
-    for (; g + 1 < T; g += 2) {
-        step(g, R1);
-        step(g + 1, R0);
+    for (; g + DEP <= T; g += DEP) {
+#pragma unroll
+        for (int c = 0; c < DEP; ++c) step(g + c, R[(c + 1) % DEP]);
     }
-    if (g < T) step(g, R1);
+#pragma unroll
+    for (int c = 0; c < DEP - 1; ++c)
+        if (g + c < T) step(g + c, R[(c + 1) % DEP]);
     if (xs > 1) {  // the split's per-row sums; ts_x3g_finish_kernel adds the splits in order
         if (t < XGR) p.xpart[blockIdx.x * XGR + t] = red[t];
         return;
@@ -1421,6 +1449,23 @@ __global__ __launch_bounds__(kBlock) void ts_x3g_finish_kernel(TsParams p) {
         p.out[b * p.out_ld] = p.gamma - x.y / sqrtf(x.x);
         if (p.stats) p.stats[b * p.N] = x;
     }
+}
+
+template <bool MASK>
+void launch_x3s(const TsParams& q, unsigned grid, size_t lds, hipStream_t st) {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel<MASK>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 2 * kXsStage + kXsMaxDim * 4) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL(ts_fwd_x3s_kernel<MASK>, dim3(grid), dim3(kXThreads), lds, st, q);
+}
+
+template <int NWV, int JPW, int DEP, bool MASK>
+void launch_x3g(const TsParams& q, unsigned grid, size_t lds, size_t lds_max, hipStream_t st) {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3g_kernel<NWV, JPW, DEP, MASK>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL((ts_fwd_x3g_kernel<NWV, JPW, DEP, MASK>), dim3(grid), dim3(NWV * kWave), lds, st, q);
 }
 
 __global__ __launch_bounds__(kBlock) void ts_premul_kernel(const float4* __restrict__ W, const float4* __restrict__ mask,
@@ -1736,8 +1781,6 @@ void launch_rows(const TsParams& p, hipStream_t st) {
     const unsigned blocks = (unsigned)row_blocks(p);
     const size_t lds = OP == TS_DH ? 0 : (size_t)p.d * sizeof(float);
     if constexpr (OP == TS_FWD) {
-        // the forward runs the bf16x3 form (fp32 accuracy, 2.67x the fp32 MFMA rate) when rows take float4s;
-        // KGE_TS_F32=1 forces the fp32 MFMA form (A/B runs)
         // the bf16x3 forms (fp32 accuracy, 2.67x the fp32 MFMA rate) when rows take float4s, operands split once at
         // staging where the 32-bit buffer offsets reach (form 1: the forms that split each fragment in registers,
         // for the bitwise / rounding cross-checks)
@@ -1751,24 +1794,24 @@ void launch_rows(const TsParams& p, hipStream_t st) {
                 q.nchunk = (int)((p.B + XGR - 1) / XGR);
                 const int64_t chunks = (p.nrel + 1) * q.nchunk;
                 if (p.xpart && p.xsplit > 1) {
-                    constexpr int ST = xg_stage(4, 1);
+                    constexpr int ST = xg_stage(kXgSplitWaves, 1);
                     const size_t lds = 2 * (size_t)ST + (size_t)p.d * 4;
-                    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3g_kernel<4, 1>),
-                                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                                 2 * ST + kXsMaxDim * 4) == hipSuccess;
-                    (void)attr;
-                    hipLaunchKernelGGL((ts_fwd_x3g_kernel<4, 1>), dim3((unsigned)(chunks * p.xsplit)), dim3(4 * kWave), lds,
-                                       st, q);
+                    const unsigned grid = (unsigned)(chunks * p.xsplit);
+                    const size_t lmax = 2 * (size_t)ST + kXsMaxDim * 4;
+                    if (q.Mpre)
+                        launch_x3g<kXgSplitWaves, 1, kXgSplitDepth, false>(q, grid, lds, lmax, st);
+                    else
+                        launch_x3g<kXgSplitWaves, 1, kXgSplitDepth, true>(q, grid, lds, lmax, st);
                     hipLaunchKernelGGL(ts_x3g_finish_kernel, dim3((unsigned)chunks), dim3(kBlock), 0, st, q);
                     return;
                 }
                 q.xsplit = 0;
                 const size_t lds = 2 * (size_t)kXgStage + (size_t)p.d * 4;
-                static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3g_kernel<8, 2>),
-                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                             2 * kXgStage + kXsMaxDim * 4) == hipSuccess;
-                (void)attr;
-                hipLaunchKernelGGL((ts_fwd_x3g_kernel<8, 2>), dim3((unsigned)chunks), dim3(kXThreads), lds, st, q);
+                const size_t lmax = 2 * (size_t)kXgStage + kXsMaxDim * 4;
+                if (q.Mpre)
+                    launch_x3g<8, 2, 2, false>(q, (unsigned)chunks, lds, lmax, st);
+                else
+                    launch_x3g<8, 2, 2, true>(q, (unsigned)chunks, lds, lmax, st);
                 return;
             }
             if (!p.grouped && p.N > TBM && p.d <= kTsBigMaxDim) {
@@ -1778,11 +1821,10 @@ void launch_rows(const TsParams& p, hipStream_t st) {
                 q.nchunk = (int)((p.N + XBR - 1) / XBR);
                 if (xs_ok) {  // operands split once at staging (ts_fwd_x3s_kernel, bitwise ts_fwd_x3_kernel's scores)
                     const size_t lds = 2 * (size_t)kXsStage + (size_t)p.d * 4;
-                    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel),
-                                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                                 2 * kXsStage + kXsMaxDim * 4) == hipSuccess;
-                    (void)attr;
-                    hipLaunchKernelGGL(ts_fwd_x3s_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);
+                    if (q.Mpre)
+                        launch_x3s<false>(q, (unsigned)(p.B * q.nchunk), lds, st);
+                    else
+                        launch_x3s<true>(q, (unsigned)(p.B * q.nchunk), lds, st);
                     return;
                 }
                 hipLaunchKernelGGL(ts_fwd_x3_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);
@@ -1860,7 +1902,7 @@ int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_l
 
 size_t kge_transparse_score_workspace_size(int mode, int64_t nrel, int64_t B, int64_t d) {
     if (mode == KGE_HEAD_BATCH || B <= 0 || d <= 0 || nrel < 0) return 0;  // only the grouped rows split columns
-    const int64_t chunks = (nrel + 1) * ((B + XGR - 1) / XGR), xsplit = (d + 127) / 128;
+    const int64_t chunks = (nrel + 1) * ((B + XGR - 1) / XGR), xsplit = (d + kXgSplitCols - 1) / kXgSplitCols;
     return xsplit > 1 ? (size_t)(chunks * xsplit * XGR) * sizeof(float2) : 0;
 }
 
@@ -1877,7 +1919,7 @@ int kge_transparse_score_ex(int mode, const float* ent, int64_t nent, int64_t en
     if (workspace && need) {
         if (workspace_bytes < need) return set_error(KGE_EINVAL, "kge_transparse_score_ex: workspace too small");
         if ((uintptr_t)workspace & 15) return set_error(KGE_EINVAL, "kge_transparse_score_ex: workspace not 16-B aligned");
-        p.xsplit = (int)((d + 127) / 128);
+        p.xsplit = (int)((d + kXgSplitCols - 1) / kXgSplitCols);
         p.xpart = reinterpret_cast<float2*>(workspace);
     }
     if (B == 0 || (!p.grouped && N == 0)) return 0;

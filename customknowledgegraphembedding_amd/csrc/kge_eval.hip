@@ -661,10 +661,28 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0, 0, 0);
         }
     };
+    // one step: multiply stage g % 2, store chunk g + 1 into the other stage, load chunk g + 3. The stores and
+    // loads are placed among the MFMAs (one store + one load per 4 MFMAs after the first B fragment's 12): 596 ->
+    // 568 us at C5 against the compiler's order (MFMAs first, then the stores and loads; profiles/r05_x3p_sched_ab.txt;
+    // an s_setprio(1) around the step on top measured the same). The last step's store lands in a stage nothing
+    // reads again.
     auto step = [&](int g, XpGemmRegs& nxt) {
         compute(g & 1);
-        if (g + 1 < T) sstore(nxt, (g + 1) & 1);
+        sstore(nxt, (g + 1) & 1);
         gload(nxt, g + 3);
+        __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);  // DS reads: the A fragments and B fragment 0
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0); // MFMA
+#pragma unroll
+        for (int j = 1; j < 4; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // B fragment j
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
         __syncthreads();
     };
     XpGemmRegs R0, R1;

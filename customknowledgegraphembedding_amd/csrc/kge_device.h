@@ -1410,14 +1410,9 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
                 my_id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
             }
         }
-        // a load past the chunk (valid false) reads zeros through a zero-size descriptor: the candidate loads
-        // are issued unconditionally, so the wait before scoring row j leaves row j + 1's loads in flight (a
-        // conditional load made the compiler wait for every load, the next row's included)
-        auto load = [&](Item& it, int j, bool valid) {
-            j &= kWave - 1;
+        auto load = [&](Item& it, int j) {
             bool ok;
-            const float* row = cand_row(p, readlane64(my_id, j), ok);
-            it.c.load(row, ok && valid, p.D, lane);
+            it.c.load(cand_row(p, readlane64(my_id, j), ok), ok, p.D, lane);
             if constexpr (FN == KGE_INTERHT) {
                 const int r = __builtin_amdgcn_readlane(code, j) >> 16;
                 const int sl = q2slot[r];
@@ -1451,13 +1446,13 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         float my_score = 0.f;
         {
             Item x0, x1;
-            load(x0, 0, true);
+            load(x0, 0);
             for (int j = 0; j < nc; j += 2) {
-                load(x1, j + 1, j + 1 < nc);
+                if (j + 1 < nc) load(x1, j + 1);
                 float s = score(x0, j);
                 if (lane == j) my_score = s;
-                load(x0, j + 2, j + 2 < nc);
                 if (j + 1 < nc) {
+                    if (j + 2 < nc) load(x0, j + 2);
                     s = score(x1, j + 1);
                     if (lane == j + 1) my_score = s;
                 }

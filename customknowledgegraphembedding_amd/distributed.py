@@ -281,10 +281,10 @@ class NativeShardExec:
         if self._fifo:
             p0, n0, m0, v0, w0 = self._fifo[0]
             if p0 is not pos_g or n0 is not neg_g or m0 != mode:
-                raise ValueError("NativeShardExec.step: the oldest batch planned ahead is another batch or mode "
-                                 "(steps must consume the planned batches in order)")
+                raise KGEHipError("NativeShardExec.step: the oldest batch planned ahead is another batch or mode "
+                                  "(steps must consume the planned batches in order)")
             if pos_g._version != v0 or neg_g._version != w0:
-                raise ValueError("NativeShardExec.step: the batch's ids changed in place after it was planned")
+                raise KGEHipError("NativeShardExec.step: the batch's ids changed in place after it was planned")
         sk, B, N = self.sk, self.B, self.N
         out = torch.empty(B * (N + 3), dtype=torch.float32, device=sk.device)
         base = out.data_ptr()

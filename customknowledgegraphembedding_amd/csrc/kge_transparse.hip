@@ -91,11 +91,12 @@ struct TsParams {
     float* d_W;
     float* pdw;  // [S, R, d, d] split partials (S > 1)
     int S, T;
-    // ts_fwd_x3g_kernel's column split (kge_transparse_score_ex with a workspace): each block of a row chunk
-    // takes `xsplit` column ranges' one; its per-row sums go to xpart [blocks][XGR] and ts_x3g_finish_kernel adds
-    // them in split order
-    int xsplit;
-    float2* xpart;
+    // ts_fwd_x3g_kernel's split form (kge_transparse_score_ex with a workspace): each block of a row chunk takes
+    // one of `xsplit` column ranges and one of `ksplit` K ranges and writes its rows' raw projections there to
+    // xk [ksplit][B][xk_ld]; ts_xk_finish_kernel adds the K ranges in order and reduces each row
+    int xsplit, ksplit;
+    float* xk;
+    int64_t xk_ld;
     int form;  // kge_forms.transparse_form: 0 the library's, 1 the forward's operands split per fragment
 };
 
@@ -1116,11 +1117,13 @@ ts_fwd_x3s_kernel(TsParams p) {
 // The per-row sums over the columns are taken per wave (half-wave shuffles), then over the 8 waves in wave
 // order: the products are ts_rows_kernel's, the column sums in another order (scores within fp32 rounding).
 // ---------------------------------------------------------------------------------------------
-// Column split (round 5): with the whole column range per block only one block per relation works (~12 CUs at
-// C6); ts_fwd_x3g_kernel<4, 1, 2, MASK> gives a block 4 waves x 32 columns = 128 columns of its rows, the xsplit blocks of
-// a row chunk together all of them, and writes its per-row sums (over its waves, in wave order) to the
-// workspace; ts_x3g_finish_kernel adds the splits in order: deterministic, scores within fp32 rounding of the
-// one-block form.
+// Split form (round 5): with the whole column range per block only one block per relation works (~12 CUs at
+// C6). With a workspace, ts_fwd_x3g_kernel<4, 1, 2, MASK> gives a block 4 waves x 32 columns = 128 columns of its
+// rows and one K range of 8 chunks (xsplit x ksplit blocks per row chunk: 16 at d = 500) and writes the rows' raw
+// partial projections to the workspace; ts_xk_finish_kernel adds each row's K ranges in order and reduces it:
+// deterministic, scores within fp32 rounding of the one-block form. A step of the K loop costs ~1.25 us whatever
+// the block's width (profiles/r05_ts_xg_ab.txt: 2-wave blocks and deeper prefetch measured no faster), so the
+// K split is what shortens the block: 32 steps -> 8.
 constexpr int XGR = 64, XGC = 512;
 constexpr int kXgAPlane = XGR * 32, kXgBPlane = XGC * 32;
 constexpr int kXgStage = 3 * (kXgAPlane + kXgBPlane);
@@ -1132,6 +1135,10 @@ constexpr int xg_stage(int NWV, int JPW) { return 3 * (kXgAPlane + xg_bplane(NWV
 // prefetch (4 / 6 sets) and 2-wave 64-column blocks measured no faster (profiles/r05_ts_xg_ab.txt): a step costs
 // ~1.3 us whatever its width, with or without the loads' latency exposed.
 constexpr int kXgSplitWaves = 4, kXgSplitCols = 32 * kXgSplitWaves, kXgSplitDepth = 2;
+// the split form's K range per block: 8 chunks of 16 (a 500-wide K in 4 ranges)
+constexpr int kXgKChunks = 8;
+__host__ __device__ constexpr int64_t xg_ksplit(int64_t d) { return ((d + 15) / 16 + kXgKChunks - 1) / kXgKChunks; }
+__host__ __device__ constexpr int64_t xg_xsplit(int64_t d) { return (d + kXgSplitCols - 1) / kXgSplitCols; }
 
 template <int JPW, int AP>
 struct XgRegs {
@@ -1156,11 +1163,16 @@ ts_fwd_x3g_kernel(TsParams p) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int half = lane >> 5, col = lane & 31;
     const int d = p.d;
-    const int xs = p.xsplit > 1 ? p.xsplit : 1;
-    const int split = (int)(blockIdx.x % xs);            // this block's column range (xsplit > 1)
-    const int64_t rc = blockIdx.x / xs;                  // its (relation, row chunk)
-    const int64_t r = rc / p.nchunk;  // == nrel: the out-of-range bucket
-    const int64_t skip = (int64_t)(rc % p.nchunk) * XGR;
+    const bool sf = p.xk != nullptr;  // the split form
+    const int xs = sf ? p.xsplit : 1, ks = sf ? p.ksplit : 1;
+    const int split = (int)(blockIdx.x % xs);  // this block's column range
+    const int64_t q0 = blockIdx.x / xs;
+    const int kidx = (int)(q0 % ks);           // its K range
+    // its (relation, row chunk): one-block form relation-major; split form chunk-major, so that the blocks of
+    // every relation's first chunk (the ones with rows, unless a relation has more than 64) are dispatched first
+    const int64_t q1 = q0 / ks;
+    const int64_t r = sf ? q1 % (p.nrel + 1) : q1 / p.nchunk;  // == nrel: the out-of-range bucket
+    const int64_t skip = (sf ? q1 / (p.nrel + 1) : q1 % p.nchunk) * XGR;
     // this block's rows: the batch rows of relation bucket r, ranks [skip, skip + 64), by an ordered ballot scan
     if (t < XGR) {
         rb[t] = -1;
@@ -1202,8 +1214,8 @@ ts_fwd_x3g_kernel(TsParams p) {
         rid[t] = id;
     }
     const bool rok = r >= 0 && r < p.nrel;
-    {  // u - 1 for the relation row (the norm summed over 512 threads' strides in the same order at any NWV:
-       // every split of the column-split form sees the same u - 1 as the one-block form)
+    if (!sf) {  // u - 1 for the relation row (the norm summed over 512 threads' strides in the same order at any
+                // NWV, as ts_xk_finish_kernel sums it for the split form)
         float ss[kXThreads / NT];
 #pragma unroll
         for (int q = 0; q < kXThreads / NT; ++q) {
@@ -1237,15 +1249,18 @@ ts_fwd_x3g_kernel(TsParams p) {
 #pragma unroll
     for (int u = 0; u < AP; ++u) aid[u] = t + u * NT < 4 * XGR ? rid[(t + u * NT) >> 2] : -1;
     const int aq = t & 3, bkp = t & 7, bjq = t >> 3;
-    // one-block form: every pass of CW columns; split form: the one pass of columns [split CW, split CW + CW)
-    const int nk = (d + 15) / 16, npass = xs > 1 ? 1 : (d + CW - 1) / CW, T = nk * npass;
-    const int col0 = xs > 1 ? split * CW : 0;
+    // one-block form: every pass of CW columns over all of K; split form: the one pass of columns
+    // [split CW, split CW + CW) over K chunks [kidx kXgKChunks, + kXgKChunks)
+    const int nk0 = (d + 15) / 16;
+    const int kc0 = sf ? kidx * kXgKChunks : 0, nk = sf ? min(kXgKChunks, nk0 - kc0) : nk0;
+    const int npass = sf ? 1 : (d + CW - 1) / CW, T = nk * npass;
+    const int col0 = sf ? split * CW : 0;
 
     // every load is issued unconditionally (a chunk past the end reads zeros through the out-of-range offset):
     // with no branch around a load the wait before a store to LDS counts exactly the younger sets' loads
     auto gload = [&](Regs& R, int g) {
         const bool in = g < T;
-        const int pc = g / nk, k0 = (g - pc * nk) * 16;
+        const int pc = g / nk, k0 = (kc0 + g - pc * nk) * 16;
         const int ka = in ? k0 + 4 * aq : d;
 #pragma unroll
         for (int u = 0; u < AP; ++u) {
@@ -1372,7 +1387,7 @@ ts_fwd_x3g_kernel(TsParams p) {
         compute(g & 1);
         if (g + 1 < T) sstore(nxt, (g + 1) & 1);
         gload(nxt, g + 1 + DEP);
-        if ((g + 1) % nk == 0) {
+        if (!sf && (g + 1) % nk == 0) {
             fold(g / nk);
             zero_acc();
         }
@@ -1393,58 +1408,24 @@ ts_fwd_x3g_kernel(TsParams p) {
 #pragma unroll
     for (int c = 0; c < DEP - 1; ++c)
         if (g + c < T) step(g + c, R[(c + 1) % DEP]);
-    if (xs > 1) {  // the split's per-row sums; ts_x3g_finish_kernel adds the splits in order
-        if (t < XGR) p.xpart[blockIdx.x * XGR + t] = red[t];
+    if (sf) {  // the rows' raw projections over this block's columns and K range; ts_xk_finish_kernel reduces them
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) {
+                const int row = i * 32 + (r2 & 3) + 8 * (r2 >> 2) + 4 * half;
+                if (row >= nrows) continue;
+                float* xr = p.xk + ((int64_t)kidx * p.B + rb[row]) * p.xk_ld;
+#pragma unroll
+                for (int j = 0; j < JPW; ++j) {
+                    const int cg = col0 + wave * JPW * 32 + j * 32 + col;
+                    if (cg < d) xr[cg] = acc[i][j][r2];
+                }
+            }
         return;
     }
     if (t < nrows) {
         const float2 x = red[t];
-        const int64_t b = rb[t];
-        p.out[b * p.out_ld] = p.gamma - x.y / sqrtf(x.x);
-        if (p.stats) p.stats[b * p.N] = x;
-    }
-}
-
-// The column-split form's finish: one block per (relation, row chunk), its rows found as the split blocks
-// found them, each row's per-split sums added in split order.
-__global__ __launch_bounds__(kBlock) void ts_x3g_finish_kernel(TsParams p) {
-    __shared__ int rb[XGR];
-    __shared__ int wcnt[kWavesPerBlock];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int64_t rc = blockIdx.x, r = rc / p.nchunk, skip = (rc % p.nchunk) * XGR;
-    if (t < XGR) rb[t] = -1;
-    int64_t seen = 0;
-    for (int64_t s = 0; s < p.B; s += kBlock) {
-        const int64_t b = s + t;
-        bool m = false;
-        if (b < p.B) {
-            const int64_t rr = p.pos[b * 3 + 1];
-            m = (r < p.nrel) ? (rr == r) : !(rr >= 0 && rr < p.nrel);
-        }
-        const uint64_t bal = __ballot(m);
-        if (lane == 0) wcnt[wave] = __popcll(bal);
-        __syncthreads();
-        int before = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < kWavesPerBlock; ++w) {
-            before += (w < wave) ? wcnt[w] : 0;
-            total += wcnt[w];
-        }
-        if (m) {
-            const int64_t k = seen + before + __popcll(bal & ((1ull << lane) - 1ull)) - skip;
-            if (k >= 0 && k < XGR) rb[k] = (int)b;
-        }
-        seen += total;
-        __syncthreads();
-        if (seen >= skip + XGR) break;  // uniform
-    }
-    const int nrows = (int)min<int64_t>(XGR, seen - skip);
-    if (t < nrows) {
-        float2 x = make_float2(0.f, 0.f);
-        for (int sp = 0; sp < p.xsplit; ++sp) {
-            const float2 v = p.xpart[(rc * p.xsplit + sp) * XGR + t];
-            x = make_float2(x.x + v.x, x.y + v.y);
-        }
         const int64_t b = rb[t];
         p.out[b * p.out_ld] = p.gamma - x.y / sqrtf(x.x);
         if (p.stats) p.stats[b * p.N] = x;
@@ -1466,6 +1447,64 @@ void launch_x3g(const TsParams& q, unsigned grid, size_t lds, size_t lds_max, hi
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max) == hipSuccess;
     (void)attr;
     hipLaunchKernelGGL((ts_fwd_x3g_kernel<NWV, JPW, DEP, MASK>), dim3(grid), dim3(NWV * kWave), lds, st, q);
+}
+
+// The split form's finish: one block per batch row. The row's projection is the sum of its K ranges' partial
+// projections in range order (deterministic), reduced over the columns as the one-block form reduces it (u - 1
+// of the row's relation in the same 512-thread order; the column sums in another order: scores within fp32
+// rounding of the one-block form).
+__global__ __launch_bounds__(kBlock) void ts_xk_finish_kernel(TsParams p) {
+    extern __shared__ float xf_cs[];  // u - 1 (d floats)
+    __shared__ float wsum8[kXWaves];
+    __shared__ float2 wred[kWavesPerBlock];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t b = blockIdx.x;
+    const int d = p.d;
+    const int64_t r = p.pos[b * 3 + 1];
+    const bool rok = r >= 0 && r < p.nrel;
+    {
+        float ss[kXThreads / kBlock];
+#pragma unroll
+        for (int q = 0; q < kXThreads / kBlock; ++q) {
+            ss[q] = 0.f;
+            for (int j = t + q * kBlock; j < d; j += kXThreads) {
+                const float v = rok ? p.rel[r * p.rel_ld + j] : 0.f;
+                xf_cs[j] = v;
+                ss[q] += v * v;
+            }
+            for (int o = 32; o > 0; o >>= 1) ss[q] += __shfl_xor(ss[q], o, kWave);
+        }
+#pragma unroll
+        for (int q = 0; q < kXThreads / kBlock; ++q)
+            if (lane == 0) wsum8[q * kWavesPerBlock + wave] = ss[q];
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < kXWaves; ++w) tot += wsum8[w];
+        const float rnorm = sqrtf(tot);
+        for (int j = t; j < d; j += kBlock) xf_cs[j] = xf_cs[j] / rnorm - 1.f;
+    }
+    __syncthreads();
+    float sq = 0.f, ab = 0.f;
+    for (int c = t; c < d; c += kBlock) {
+        float v = 0.f;
+        for (int k = 0; k < p.ksplit; ++k) v += p.xk[((int64_t)k * p.B + b) * p.xk_ld + c];
+        sq = fmaf(v, v, sq);
+        ab += fabsf(v * xf_cs[c]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sq += __shfl_xor(sq, o, kWave);
+        ab += __shfl_xor(ab, o, kWave);
+    }
+    if (lane == 0) wred[wave] = make_float2(sq, ab);
+    __syncthreads();
+    if (t == 0) {
+        float2 x = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) x = make_float2(x.x + wred[w].x, x.y + wred[w].y);
+        p.out[b * p.out_ld] = p.gamma - x.y / sqrtf(x.x);
+        if (p.stats) p.stats[b * p.N] = x;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void ts_premul_kernel(const float4* __restrict__ W, const float4* __restrict__ mask,
@@ -1789,23 +1828,23 @@ void launch_rows(const TsParams& p, hipStream_t st) {
                                (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB;
             if (p.grouped && xs_ok) {
                 // single / tail-batch rows: 64 rows of one relation per block (ts_fwd_x3g_kernel), all columns, or
-                // with a workspace (xpart) one of xsplit 128-column ranges, then the splits' finish
+                // with a workspace (xk) one of xsplit 128-column ranges x one of ksplit K ranges, then the finish
                 TsParams q = p;
                 q.nchunk = (int)((p.B + XGR - 1) / XGR);
                 const int64_t chunks = (p.nrel + 1) * q.nchunk;
-                if (p.xpart && p.xsplit > 1) {
+                if (p.xk) {
                     constexpr int ST = xg_stage(kXgSplitWaves, 1);
                     const size_t lds = 2 * (size_t)ST + (size_t)p.d * 4;
-                    const unsigned grid = (unsigned)(chunks * p.xsplit);
+                    const unsigned grid = (unsigned)(chunks * p.xsplit * p.ksplit);
                     const size_t lmax = 2 * (size_t)ST + kXsMaxDim * 4;
                     if (q.Mpre)
                         launch_x3g<kXgSplitWaves, 1, kXgSplitDepth, false>(q, grid, lds, lmax, st);
                     else
                         launch_x3g<kXgSplitWaves, 1, kXgSplitDepth, true>(q, grid, lds, lmax, st);
-                    hipLaunchKernelGGL(ts_x3g_finish_kernel, dim3((unsigned)chunks), dim3(kBlock), 0, st, q);
+                    hipLaunchKernelGGL(ts_xk_finish_kernel, dim3((unsigned)p.B), dim3(kBlock), (size_t)p.d * 4, st, q);
                     return;
                 }
-                q.xsplit = 0;
+                q.xk = nullptr;
                 const size_t lds = 2 * (size_t)kXgStage + (size_t)p.d * 4;
                 const size_t lmax = 2 * (size_t)kXgStage + kXsMaxDim * 4;
                 if (q.Mpre)
@@ -1901,9 +1940,10 @@ int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_l
 }
 
 size_t kge_transparse_score_workspace_size(int mode, int64_t nrel, int64_t B, int64_t d) {
-    if (mode == KGE_HEAD_BATCH || B <= 0 || d <= 0 || nrel < 0) return 0;  // only the grouped rows split columns
-    const int64_t chunks = (nrel + 1) * ((B + XGR - 1) / XGR), xsplit = (d + kXgSplitCols - 1) / kXgSplitCols;
-    return xsplit > 1 ? (size_t)(chunks * xsplit * XGR) * sizeof(float2) : 0;
+    // only the grouped rows (single / tail-batch) split; the partial projections [ksplit][B][xsplit 128] floats
+    if (mode == KGE_HEAD_BATCH || B <= 0 || d <= 0 || d > kXsMaxDim || nrel < 0) return 0;
+    const int64_t xs = xg_xsplit(d), ks = xg_ksplit(d);
+    return xs * ks > 1 ? (size_t)(ks * B * xs * kXgSplitCols) * sizeof(float) : 0;
 }
 
 int kge_transparse_score_ex(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
@@ -1919,8 +1959,10 @@ int kge_transparse_score_ex(int mode, const float* ent, int64_t nent, int64_t en
     if (workspace && need) {
         if (workspace_bytes < need) return set_error(KGE_EINVAL, "kge_transparse_score_ex: workspace too small");
         if ((uintptr_t)workspace & 15) return set_error(KGE_EINVAL, "kge_transparse_score_ex: workspace not 16-B aligned");
-        p.xsplit = (int)((d + kXgSplitCols - 1) / kXgSplitCols);
-        p.xpart = reinterpret_cast<float2*>(workspace);
+        p.xsplit = (int)xg_xsplit(d);
+        p.ksplit = (int)xg_ksplit(d);
+        p.xk = reinterpret_cast<float*>(workspace);
+        p.xk_ld = (int64_t)p.xsplit * kXgSplitCols;
     }
     if (B == 0 || (!p.grouped && N == 0)) return 0;
     if (!ent || !rel || !W || !pos || !out || (!p.grouped && !neg))

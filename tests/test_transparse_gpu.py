@@ -211,7 +211,8 @@ def test_split_once_forward_is_bitwise_the_register_split_one(monkeypatch, d, N,
 @pytest.mark.parametrize("mode", [1, 3])
 def test_grouped_forward_all_columns_per_block(monkeypatch, d, B, R, premul, mode):
     """Single / tail-batch rows: one relation's row chunk per block over all columns (ts_fwd_x3g_kernel<8, 2>),
-    and split over 128-column ranges through a workspace (ts_fwd_x3g_kernel<4, 1> + the ordered finish):
+    and split over 128-column x 128-k ranges through a workspace (ts_fwd_x3g_kernel<4, 1, 2, MASK> + the ordered
+    finish ts_xk_finish_kernel):
     within 1e-4 of the fp64 oracle, within fp32 rounding of ts_rows_kernel's column order (form 1) and of each
     other, bitwise run to run, with rows of out-of-range relations and heads (NaN), more than 64 rows per
     relation and d past one 512-column pass."""

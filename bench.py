@@ -913,9 +913,10 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
 
 
 def transparse_bench(w, a, device):
-    """c6: TranSparse scoring step = head-batch negatives ([B, N], kge_transparse_score on the fp32
-    MFMA, events around it) + the positives (single, [B, 1]) + the row reductions; plus the
-    autograd train step (deterministic backward + HIP Adam) as a side measurement."""
+    """c6: TranSparse scoring step = both calls of supervisor.py:17-18 in kge_transparse_step_forward (head-batch
+    negatives [B, N] on the bf16x3 MFMA forms with their row reduction, the positives [B, 1] with their
+    logsigmoid; events around the call), after the mask product (kge_transparse_premul); plus the autograd train
+    step (deterministic backward + HIP Adam) as a side measurement."""
     from customknowledgegraphembedding_amd.model import TFKGEModel
     from customknowledgegraphembedding_amd.optim import Adam
     from customknowledgegraphembedding_amd.supervisor import Strategy, Sum, Trainer
@@ -930,15 +931,16 @@ def transparse_bench(w, a, device):
     ent, rel, W, mask = m.entity_embedding.detach(), m.relation_embedding.detach(), m.W.detach(), m.mask
 
     def step(b, ev=None):
+        # supervisor.py:17-18 both calls: kge_transparse_step_forward (the head-batch scores and their row
+        # reduction, the positives' scores and logsigmoid; events around that call)
         pos, neg = b
         M = ops.transparse_premul(W, mask) if ops._want_premul(W, pos, neg, 0) else None
         if ev is not None:
             ev[0].record()
-        ns = ops.transparse_score_raw(0, ent, rel, W, mask, pos, neg, m._gamma_f, M=M)
+        _, on, _, op = ops.transparse_step_forward_raw(0, ent, rel, W, mask, pos, neg, m._gamma_f, M=M)
         if ev is not None:
             ev[1].record()
-        ps = ops.transparse_score_raw(3, ent, rel, W, mask, pos, None, m._gamma_f, M=M)
-        return ops.neg_reduce_raw(ns), ops.log_sigmoid_raw(ps.reshape(-1))
+        return on, op
 
     for i in range(a.warmup):
         step(batches[i % 4])
@@ -950,11 +952,13 @@ def transparse_bench(w, a, device):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     k_s = statistics.mean(e0.elapsed_time(e1) for e0, e1 in evs) / 1e3
-    flops = 2.0 * B * N * d * d
-    # the default forms run the bf16x3 forward (float4 rows: d % 4 == 0, aligned tables)
+    flops = 2.0 * (B * N + B) * d * d
+    # the default forms run the bf16x3 forward (float4 rows: d % 4 == 0, aligned tables). Executed MFMA products
+    # of the call: head-batch 256-column super-tiles x 16-deep chunks; the positives' split form 128-column x
+    # 16-deep blocks
     x3 = d % 4 == 0
-    dp = (d + 127) // 128 * 128  # columns in 128-wide tiles, K in 32-deep chunks: both padded to 128 here
-    mfma_flops = 6 * 2.0 * B * N * dp * ((d + 31) // 32 * 32)
+    dp, dk = (d + 255) // 256 * 256, (d + 15) // 16 * 16
+    mfma_flops = 6 * 2.0 * B * N * dp * dk + 6 * 2.0 * B * ((d + 127) // 128 * 128) * dk
     train = None
     if a.train_steps > 0:
         wts = torch.ones(B, 1, device=device)
@@ -983,7 +987,9 @@ def transparse_bench(w, a, device):
             "config": {"workload": w["name"], "global_batch": B, "n_neg": N, "d": d},
             "roofline": ({"bound": "mfma", "achieved": mfma_flops / k_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                           "frac": mfma_flops / k_s / 1e12 / 2500.0, "traffic": None,
-                          "kernel": ts_kernel_name(),
+                          "kernel": "kge_transparse_step_forward: " + ts_kernel_name() + " with the row reduction in "
+                                    "its epilogue; ts_fwd_x3g_kernel (columns x K split) + ts_xk_finish_kernel with "
+                                    "the logsigmoid",
                           "kernel_avg_us": k_s * 1e6, "fp32_equivalent_tflops": flops / k_s / 1e12,
                           "fp32_equivalent_over_fp32_mfma_peak": flops / k_s / 1e12 / 157.3}
                          if x3 else

@@ -200,6 +200,12 @@ SIGNATURES = {
     "kge_transparse_score_ex": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p,
                                        _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_p, _c_i64, _c_p, _c_p, _c_p,
                                        ctypes.c_size_t, _c_p]),
+    "kge_transparse_step_workspace_size": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
+    # (mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d, gamma, T, adversarial,
+    #  neg_scores, ns_ld, out_neg, pos_scores, out_pos, workspace, workspace_bytes, stream)
+    "kge_transparse_step_forward": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p,
+                                           _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_i, _c_p, _c_i64, _c_p, _c_p,
+                                           _c_p, _c_p, ctypes.c_size_t, _c_p]),
     "kge_transparse_bwd_workspace_size": (ctypes.c_size_t, [_c_i, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
     "kge_transparse_premul": (_c_i, [_c_p, _c_p, _c_i64, _c_p, _c_p]),
     "kge_transparse_score_bwd": (_c_i, [_c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p,

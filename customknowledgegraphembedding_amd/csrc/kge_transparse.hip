@@ -98,6 +98,13 @@ struct TsParams {
     float* xk;
     int64_t xk_ld;
     int form;  // kge_forms.transparse_form: 0 the library's, 1 the forward's operands split per fragment
+    // kge_transparse_step_forward: the negative call's row reduction (model.py:168-171, row_reduce_fast) in the
+    // head-batch kernels' epilogue when one block holds a whole row (out_neg), and the positive call's
+    // logsigmoid (model.py:145) in the split form's finish (out_pos_ls)
+    float* out_neg;
+    float* out_pos_ls;
+    float temperature;
+    int adversarial;
 };
 
 __device__ __forceinline__ int64_t row_entity(const TsParams& p, int64_t b, int64_t n) {
@@ -846,6 +853,13 @@ ts_fwd_x3_kernel(TsParams p) {
         p.out[b * p.out_ld + n] = p.gamma - x.y / sqrtf(x.x);
         if (p.stats) p.stats[b * p.N + n] = x;
     }
+    if (p.out_neg) {  // the block holds the whole row (the launcher sets out_neg only then): its reduction
+        __syncthreads();
+        if (wave == 0) {
+            const float rr = row_reduce_fast(p.out + b * p.out_ld, p.N, p.temperature, p.adversarial, lane);
+            if (lane == 0) p.out_neg[b] = rr;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1101,6 +1115,13 @@ ts_fwd_x3s_kernel(TsParams p) {
         const int64_t n = n0 + t;
         p.out[b * p.out_ld + n] = p.gamma - x.y / sqrtf(x.x);
         if (p.stats) p.stats[b * p.N + n] = x;
+    }
+    if (p.out_neg) {  // the block holds the whole row (the launcher sets out_neg only then): its reduction
+        __syncthreads();
+        if (wave == 0) {
+            const float rr = row_reduce_fast(p.out + b * p.out_ld, p.N, p.temperature, p.adversarial, lane);
+            if (lane == 0) p.out_neg[b] = rr;
+        }
     }
 }
 
@@ -1502,8 +1523,17 @@ __global__ __launch_bounds__(kBlock) void ts_xk_finish_kernel(TsParams p) {
         float2 x = make_float2(0.f, 0.f);
 #pragma unroll
         for (int w = 0; w < kWavesPerBlock; ++w) x = make_float2(x.x + wred[w].x, x.y + wred[w].y);
-        p.out[b * p.out_ld] = p.gamma - x.y / sqrtf(x.x);
+        const float sc = p.gamma - x.y / sqrtf(x.x);
+        p.out[b * p.out_ld] = sc;
         if (p.stats) p.stats[b * p.N] = x;
+        if (p.out_pos_ls) p.out_pos_ls[b] = log_sigmoid(sc);
+    }
+    if (p.out_neg) {  // the tail-batch negative call's [B, 1] row (Q9): its reduction over the one score
+        __syncthreads();
+        if (wave == 0) {
+            const float rr = row_reduce_fast(p.out + b * p.out_ld, 1, p.temperature, p.adversarial, lane);
+            if (lane == 0) p.out_neg[b] = rr;
+        }
     }
 }
 
@@ -1815,8 +1845,9 @@ int fill(TsParams& p, int mode, const float* ent, int64_t nent, int64_t ent_ld, 
 
 int64_t row_blocks(const TsParams& p) { return p.grouped ? (p.nrel + 1) * p.nchunk : p.B * p.nchunk; }
 
+// true: the launch also produced p.out_neg / p.out_pos_ls (the fused epilogues); false: it ignored them
 template <int OP>
-void launch_rows(const TsParams& p, hipStream_t st) {
+bool launch_rows(const TsParams& p, hipStream_t st) {
     const unsigned blocks = (unsigned)row_blocks(p);
     const size_t lds = OP == TS_DH ? 0 : (size_t)p.d * sizeof(float);
     if constexpr (OP == TS_FWD) {
@@ -1842,7 +1873,7 @@ void launch_rows(const TsParams& p, hipStream_t st) {
                     else
                         launch_x3g<kXgSplitWaves, 1, kXgSplitDepth, true>(q, grid, lds, lmax, st);
                     hipLaunchKernelGGL(ts_xk_finish_kernel, dim3((unsigned)p.B), dim3(kBlock), (size_t)p.d * 4, st, q);
-                    return;
+                    return true;
                 }
                 q.xk = nullptr;
                 const size_t lds = 2 * (size_t)kXgStage + (size_t)p.d * 4;
@@ -1851,32 +1882,34 @@ void launch_rows(const TsParams& p, hipStream_t st) {
                     launch_x3g<8, 2, 2, false>(q, (unsigned)chunks, lds, lmax, st);
                 else
                     launch_x3g<8, 2, 2, true>(q, (unsigned)chunks, lds, lmax, st);
-                return;
+                return false;
             }
             if (!p.grouped && p.N > TBM && p.d <= kTsBigMaxDim) {
                 // head-batch rows beyond one 128-row block: 256-row blocks that stage each M_r chunk once for all
                 // the batch row's negatives
                 TsParams q = p;
                 q.nchunk = (int)((p.N + XBR - 1) / XBR);
+                if (q.nchunk != 1) q.out_neg = nullptr;  // the epilogue reduces a row only when one block holds it
                 if (xs_ok) {  // operands split once at staging (ts_fwd_x3s_kernel, bitwise ts_fwd_x3_kernel's scores)
                     const size_t lds = 2 * (size_t)kXsStage + (size_t)p.d * 4;
                     if (q.Mpre)
                         launch_x3s<false>(q, (unsigned)(p.B * q.nchunk), lds, st);
                     else
                         launch_x3s<true>(q, (unsigned)(p.B * q.nchunk), lds, st);
-                    return;
+                    return q.nchunk == 1;
                 }
                 hipLaunchKernelGGL(ts_fwd_x3_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);
-                return;
+                return q.nchunk == 1;
             }
             hipLaunchKernelGGL((ts_rows_kernel<OP, 4, true>), dim3(blocks), dim3(kBlock), lds, st, p);
-            return;
+            return false;
         }
     }
     if (use_v4(p))
         hipLaunchKernelGGL((ts_rows_kernel<OP, 4>), dim3(blocks), dim3(kBlock), lds, st, p);
     else
         hipLaunchKernelGGL((ts_rows_kernel<OP, 1>), dim3(blocks), dim3(kBlock), lds, st, p);
+    return false;
 }
 
 size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1946,11 +1979,13 @@ size_t kge_transparse_score_workspace_size(int mode, int64_t nrel, int64_t B, in
     return xs * ks > 1 ? (size_t)(ks * B * xs * kXgSplitCols) * sizeof(float) : 0;
 }
 
-int kge_transparse_score_ex(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
-                            int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
-                            int64_t neg_ld, int64_t B, int64_t N, int64_t d, float gamma, float* out, int64_t out_ld,
-                            float* stats, const kge_forms* forms, void* workspace, size_t workspace_bytes,
-                            void* stream) {
+static int ts_score_impl(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
+                         int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
+                         int64_t neg_ld, int64_t B, int64_t N, int64_t d, float gamma, float* out, int64_t out_ld,
+                         float* stats, const kge_forms* forms, void* workspace, size_t workspace_bytes,
+                         float* out_neg, float* out_pos_ls, float temperature, int adversarial, bool* fused,
+                         void* stream) {
+    if (fused) *fused = false;
     TsParams p;
     int rc = fill(p, mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d, gamma);
     if (rc) return rc;
@@ -1972,8 +2007,56 @@ int kge_transparse_score_ex(int mode, const float* ent, int64_t nent, int64_t en
     p.out = out;
     p.out_ld = out_ld;
     p.stats = reinterpret_cast<float2*>(stats);
-    launch_rows<TS_FWD>(p, (hipStream_t)stream);
+    p.out_neg = out_neg;
+    p.out_pos_ls = out_pos_ls;
+    p.temperature = temperature;
+    p.adversarial = adversarial;
+    const bool f = launch_rows<TS_FWD>(p, (hipStream_t)stream);
+    if (fused) *fused = f;
     return check("kge_transparse_score");
+}
+
+int kge_transparse_score_ex(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel, int64_t nrel,
+                            int64_t rel_ld, const float* W, const float* mask, const int64_t* pos, const int64_t* neg,
+                            int64_t neg_ld, int64_t B, int64_t N, int64_t d, float gamma, float* out, int64_t out_ld,
+                            float* stats, const kge_forms* forms, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+    return ts_score_impl(mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d, gamma, out,
+                         out_ld, stats, forms, workspace, workspace_bytes, nullptr, nullptr, 1.f, 1, nullptr, stream);
+}
+
+size_t kge_transparse_step_workspace_size(int64_t nrel, int64_t B, int64_t d) {
+    return kge_transparse_score_workspace_size(KGE_SINGLE, nrel, B, d);  // the grouped calls' split; head-batch none
+}
+
+int kge_transparse_step_forward(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel,
+                                int64_t nrel, int64_t rel_ld, const float* W, const float* mask, const int64_t* pos,
+                                const int64_t* neg, int64_t neg_ld, int64_t B, int64_t N, int64_t d, float gamma,
+                                float temperature, int adversarial, float* neg_scores, int64_t ns_ld, float* out_neg,
+                                float* pos_scores, float* out_pos, void* workspace, size_t workspace_bytes,
+                                void* stream) {
+    if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH)
+        return set_error(KGE_EINVAL, "kge_transparse_step_forward: mode must be 0 (head-batch) or 1 (tail-batch)");
+    if (B > 0 && (!out_neg || !out_pos || !neg_scores || !pos_scores))
+        return set_error(KGE_EINVAL, "kge_transparse_step_forward: null output");
+    // the negative call (model.py:121-125): scores, then its row reduction (model.py:168-171)
+    bool fused = false;
+    int rc = ts_score_impl(mode, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, neg, neg_ld, B, N, d, gamma,
+                           neg_scores, ns_ld, nullptr, nullptr, workspace, workspace_bytes, out_neg, nullptr,
+                           temperature, adversarial, &fused, stream);
+    if (rc) return rc;
+    if (!fused && B > 0) {
+        rc = kge_neg_reduce(neg_scores, B, mode == KGE_HEAD_BATCH ? N : 1, ns_ld, temperature, adversarial, out_neg,
+                            stream);
+        if (rc) return rc;
+    }
+    // the positive call (model.py:117-146): the single-mode scores and their logsigmoid (model.py:145)
+    rc = ts_score_impl(KGE_SINGLE, ent, nent, ent_ld, rel, nrel, rel_ld, W, mask, pos, nullptr, 0, B, 1, d, gamma,
+                       pos_scores, 1, nullptr, nullptr, workspace, workspace_bytes, nullptr, out_pos, temperature,
+                       adversarial, &fused, stream);
+    if (rc) return rc;
+    if (!fused && B > 0) return kge_log_sigmoid(pos_scores, B, out_pos, stream);
+    return 0;
 }
 
 size_t kge_transparse_bwd_workspace_size(int mode, int64_t nent, int64_t nrel, int64_t B, int64_t N, int64_t d) {

@@ -189,7 +189,16 @@ class TFKGEModel(_KGEBase):
         if m == SINGLE:
             raise ValueError("step_forward needs the batch's negative mode")
         if self.model_name == "TranSparse":
-            return self(((positive_sample, negative_sample), m)), self(((positive_sample, negative_sample), SINGLE))
+            params = (self.entity_embedding, self.relation_embedding, self.W)
+            if torch.is_grad_enabled() and any(t.requires_grad for t in params):
+                return self(((positive_sample, negative_sample), m)), self(((positive_sample, negative_sample), SINGLE))
+            # no autograd: both calls and their reductions in one entry point (bitwise the two calls above)
+            M = ops.transparse_premul(self.W, self.mask) if ops._want_premul(self.W, positive_sample,
+                                                                              negative_sample, m) else None
+            _, on, _, op = ops.transparse_step_forward_raw(m, self.entity_embedding, self.relation_embedding, self.W,
+                                                           self.mask, positive_sample, negative_sample, self._gamma_f,
+                                                           M=M)
+            return on.unsqueeze(1), op.unsqueeze(1)
         modulus = self.modulus if self.model_name == "pRotatE" else None
         neg, pos = ops.step_forward(FN_IDS[self.model_name], m, self.entity_embedding,
                                     self.relation_embedding, positive_sample, negative_sample,

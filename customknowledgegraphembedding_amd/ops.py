@@ -427,6 +427,46 @@ def transparse_score_raw(mode, ent, rel, W, mask, pos, neg, gamma, stats=None, o
     return out
 
 
+def transparse_step_forward_raw(mode, ent, rel, W, mask, pos, neg, gamma, temperature=1.0, adversarial=True, M=None):
+    """Both calls of supervisor.py:17-18 for TranSparse (kge_transparse_step_forward): returns (neg_scores,
+    out_neg [B], pos_scores [B], out_pos [B]); neg_scores is [B, N] for head-batch, [B, 1] for tail-batch (Q9).
+    Bitwise transparse_score_raw + neg_reduce_raw / log_sigmoid_raw. No autograd (see TFKGEModel.step_forward)."""
+    _need_gpu(ent, rel, W, mask, pos, neg)
+    for t, n in ((ent, "ent"), (rel, "rel"), (W, "W"), (mask, "mask")):
+        _fp32(t, n)
+    _i64(pos, "pos")
+    m = mode_id(mode)
+    if m not in (HEAD_BATCH, TAIL_BATCH):
+        raise ValueError("transparse_step_forward needs the batch's negative mode (0 or 1)")
+    if not (W.is_contiguous() and mask.is_contiguous()):
+        raise ValueError("W and mask must be contiguous [R, d, d]")
+    B, d = pos.shape[0], ent.shape[1]
+    if rel.shape[1] != d or tuple(W.shape) != (rel.shape[0], d, d) or W.shape != mask.shape:
+        raise ValueError("TranSparse needs entity_dim == relation_dim == d and W, mask [R, d, d]")
+    if pos.stride(1) != 1 or pos.stride(0) != 3:
+        pos = pos.contiguous()
+    _i64(neg, "neg")
+    if neg.stride(1) != 1:
+        neg = neg.contiguous()
+    N = neg.shape[1] if m == HEAD_BATCH else 1
+    dev = ent.device
+    ns = torch.empty((B, N), dtype=torch.float32, device=dev)
+    out_neg = torch.empty((B,), dtype=torch.float32, device=dev)
+    ps = torch.empty((B,), dtype=torch.float32, device=dev)
+    out_pos = torch.empty((B,), dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    nbytes = int(lib.kge_transparse_step_workspace_size(rel.shape[0], B, d))
+    ws = _workspace(dev, nbytes)
+    Wp, maskp = (M.data_ptr(), None) if M is not None else (W.data_ptr(), mask.data_ptr())
+    rc = lib.kge_transparse_step_forward(
+        m, ent.data_ptr(), ent.shape[0], ent.stride(0), rel.data_ptr(), rel.shape[0], rel.stride(0), Wp, maskp,
+        pos.data_ptr(), neg.data_ptr(), neg.stride(0), B, neg.shape[1], d, float(gamma), float(temperature),
+        int(bool(adversarial)), ns.data_ptr(), ns.stride(0), out_neg.data_ptr(), ps.data_ptr(), out_pos.data_ptr(),
+        None if ws is None else ws.data_ptr(), nbytes, _stream(dev))
+    check(rc, "kge_transparse_step_forward")
+    return ns, out_neg, ps, out_pos
+
+
 def transparse_score_bwd_raw(mode, ent, rel, W, mask, pos, neg, stats, d_scores, d_ent, d_rel, d_W, M=None):
     """Accumulates the TranSparse gradients into d_ent, d_rel, d_W (deterministic)."""
     m = mode_id(mode)

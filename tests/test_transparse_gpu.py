@@ -244,3 +244,34 @@ def test_grouped_forward_all_columns_per_block(monkeypatch, d, B, R, premul, mod
     ok_pos[3, 1], ok_pos[5, 0] = 0, 0
     ref, _ = _oracle(ent, rel, W, mask, ok_pos, neg, mode, gamma)
     assert rel_close(new[~bad], ref[~bad, 0]) <= 1e-4
+
+
+@pytest.mark.parametrize("mode,N", [(0, 256), (0, 300), (0, 96), (1, 256)])
+@pytest.mark.parametrize("premul", [False, True])
+def test_step_forward_fused_is_bitwise_the_two_calls(mode, N, premul):
+    """kge_transparse_step_forward (both calls of supervisor.py:17-18 and their reductions in one entry point:
+    the head-batch row reduction in ts_fwd_x3s_kernel's epilogue when one block holds the row, N <= 256; the
+    positives' logsigmoid in the split form's finish; the standalone reduction launches otherwise) is bitwise
+    transparse_score + neg_reduce + log_sigmoid, NaN rows included; and TFKGEModel.step_forward under no_grad
+    takes it."""
+    E, R, d, B, gamma = 300, 4, 500, 70, 12.0
+    ent, rel, W, mask = _tables(E, R, d, seed=7)
+    pos, neg = _batch(E, R, B, N, seed=13)
+    pos[4, 1] = R + 1  # out-of-range relation: NaN scores
+    ed, rd, Wd, md, pd, nd = ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV), pos.to(DEV), neg.to(DEV)
+    M = ops.transparse_premul(Wd, md) if premul else None
+    ns, on, ps, op = ops.transparse_step_forward_raw(mode, ed, rd, Wd, md, pd, nd, gamma, M=M)
+    ref_ns = ops.transparse_score_raw(mode, ed, rd, Wd, md, pd, nd, gamma, M=M)
+    ref_on = ops.neg_reduce_raw(ref_ns, 1.0, True)
+    ref_ps = ops.transparse_score_raw(3, ed, rd, Wd, md, pd, None, gamma, M=M).reshape(-1)
+    ref_op = ops.log_sigmoid_raw(ref_ps)
+    torch.cuda.synchronize()
+    for got, ref in ((ns, ref_ns), (on, ref_on), (ps, ref_ps), (op, ref_op)):
+        assert torch.equal(torch.nan_to_num(got, nan=7.0), torch.nan_to_num(ref.reshape(got.shape), nan=7.0))
+    assert torch.isnan(on[4]) and not torch.isnan(on[:4]).any()
+    m = TFKGEModel("TranSparse", E, R, d, gamma, device=DEV, seed=3)
+    with torch.no_grad():
+        n1, p1 = m.step_forward(pd, nd, mode)
+    n2, p2 = m(((pd, nd), mode)), m(((pd, nd), 3))
+    assert torch.equal(torch.nan_to_num(n1, nan=7.0), torch.nan_to_num(n2.detach(), nan=7.0))
+    assert torch.equal(torch.nan_to_num(p1, nan=7.0), torch.nan_to_num(p2.detach(), nan=7.0))

@@ -105,6 +105,10 @@ struct TsParams {
     float* out_pos_ls;
     float temperature;
     int adversarial;
+    // head-batch with a workspace: M_r (= W_r * mask_r) split once per call into three bf16 planes per relation,
+    // [r][plane][K / 16][mp_cols][16] (ts_mplanes_kernel), staged by ts_fwd_x3s_kernel<.., true> with no conversion
+    __bf16* mplanes;
+    int mp_cols, mp_nk;
 };
 
 __device__ __forceinline__ int64_t row_entity(const TsParams& p, int64_t b, int64_t n) {
@@ -899,9 +903,10 @@ __device__ __forceinline__ void split3_x4(f32x4_t v, bf16x4_t& a0, bf16x4_t& a1,
 
 struct XsRegs {
     float4 a[2], b[2], m[2];
+    int4 bp[3];  // B from the pre-split planes (BPL)
 };
 
-template <bool MASK>
+template <bool MASK, bool BPL>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(2))) void
 ts_fwd_x3s_kernel(TsParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char xs_smem[];  // 2 stages, then u - 1 (d floats)
@@ -963,6 +968,11 @@ ts_fwd_x3s_kernel(TsParams p) {
     const rsrc_t rw = make_rsrc(Wr, mbytes);
     constexpr bool fuse_mask = MASK;  // M_r = W_r * mask_r formed at staging (else p.Mpre holds the products)
     const rsrc_t rm = make_rsrc(fuse_mask && rok ? p.mask + r * (int64_t)d * d : p.W, fuse_mask ? mbytes : 0u);
+    // BPL: the relation's three planes; thread t stages column t >> 1, k half t & 1 of each (16 B, x3p's pattern)
+    const int64_t mp_plane = (int64_t)p.mp_nk * p.mp_cols * 16;  // elements of one plane of one relation
+    const rsrc_t rp = make_rsrc(BPL && rok ? p.mplanes + r * 3 * mp_plane : nullptr,
+                                BPL && rok ? (uint32_t)(3 * mp_plane * 2) : 0u);
+    const int spc = t >> 1, sph = t & 1;
     // this thread's staging slots: A rows (t >> 2) + 128 u, k quad t & 3; B k pair t & 7 (+u), columns 4 (t >> 3)
     int aid[2];
 #pragma unroll
@@ -982,6 +992,7 @@ ts_fwd_x3s_kernel(TsParams p) {
             const auto va = __builtin_amdgcn_raw_buffer_load_b128(ra, oa, 0, 0);
             R.a[u] = make_float4(__uint_as_float(va[0]), __uint_as_float(va[1]), __uint_as_float(va[2]),
                                  __uint_as_float(va[3]));
+            if constexpr (BPL) continue;
             const int kb = in ? k0 + 2 * bkp + u : d, j = ct * XBC + 4 * bjq;
             const uint32_t ob = (kb < d && j < d) ? (uint32_t)(((int64_t)kb * d + j) * 4) : kXsOOB;
             const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rw, ob, 0, 0);
@@ -991,6 +1002,16 @@ ts_fwd_x3s_kernel(TsParams p) {
                 const auto vm = __builtin_amdgcn_raw_buffer_load_b128(rm, ob, 0, 0);
                 R.m[u] = make_float4(__uint_as_float(vm[0]), __uint_as_float(vm[1]), __uint_as_float(vm[2]),
                                      __uint_as_float(vm[3]));
+            }
+        }
+        if constexpr (BPL) {
+            // a chunk past the end (g >= T) reloads chunk 0: never multiplied, and no branch around the loads
+            const int kc = in ? (k0 >> 4) : 0, cc = in ? ct * XBC : 0;
+            const uint32_t ob = (uint32_t)((((int64_t)kc * p.mp_cols + cc + spc) * 16 + 8 * sph) * 2);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, ob + (uint32_t)(pl * mp_plane * 2), 0, 0);
+                R.bp[pl] = make_int4(v[0], v[1], v[2], v[3]);
             }
         }
     };
@@ -1006,6 +1027,11 @@ ts_fwd_x3s_kernel(TsParams p) {
             *reinterpret_cast<bf16x4_t*>(A + o) = s0;
             *reinterpret_cast<bf16x4_t*>(A + kXsPlane + o) = s1;
             *reinterpret_cast<bf16x4_t*>(A + 2 * kXsPlane + o) = s2;
+        }
+        if constexpr (BPL) {  // B: the planes' [column][16 k] rows as they are
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<int4*>(Bp + pl * kXsPlane + xs_off(spc, sph)) = R.bp[pl];
+            return;
         }
         // B: the two k rows of this thread's 4 columns, transposed into [column][k]
         float4 b0 = R.b[0], b1 = R.b[1];
@@ -1453,13 +1479,57 @@ ts_fwd_x3g_kernel(TsParams p) {
     }
 }
 
-template <bool MASK>
+// M_r split once per call into the planes ts_fwd_x3s_kernel<.., true> stages (split3_x4's arithmetic on the same
+// products W * mask or Mpre, so the bf16 terms and the scores are bitwise the in-kernel split's): one thread per
+// (relation, 16-k chunk, column), 16 k values -> 32 B per plane; columns past d and k past d are zero.
+__global__ __launch_bounds__(kBlock) void ts_mplanes_kernel(const float* __restrict__ src, const float* __restrict__ mask,
+                                                            int64_t nrel, int d, int cols, int nk,
+                                                            __bf16* __restrict__ P) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nrel * nk * cols) return;
+    const int j = (int)(i % cols);
+    const int64_t q = i / cols;
+    const int kc = (int)(q % nk);
+    const int64_t r = q / nk;
+    const int64_t plane = (int64_t)nk * cols * 16;
+    __bf16* o = P + r * 3 * plane + ((int64_t)kc * cols + j) * 16;
+    // clamped addresses and a select (no branch around a load): the 16 loads (32 with the mask) issue together
+    const int jc = min(j, d - 1);
+    float x[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int k = min(kc * 16 + e, d - 1);
+        const int64_t at = (r * d + k) * (int64_t)d + jc;
+        x[e] = mask ? src[at] * mask[at] : src[at];
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        f32x4_t v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = kc * 16 + 4 * g + e;
+            v[e] = (k < d && j < d) ? x[4 * g + e] : 0.f;
+        }
+        bf16x4_t s0, s1, s2;
+        split3_x4(v, s0, s1, s2);
+        *reinterpret_cast<bf16x4_t*>(o + 4 * g) = s0;
+        *reinterpret_cast<bf16x4_t*>(o + plane + 4 * g) = s1;
+        *reinterpret_cast<bf16x4_t*>(o + 2 * plane + 4 * g) = s2;
+    }
+}
+
+int64_t mplanes_bytes(int64_t nrel, int64_t d) {
+    const int64_t cols = (d + XBC - 1) / XBC * XBC, nk = (d + 15) / 16;
+    return nrel * 3 * nk * cols * 16 * 2;
+}
+
+template <bool MASK, bool BPL>
 void launch_x3s(const TsParams& q, unsigned grid, size_t lds, hipStream_t st) {
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel<MASK>),
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel<MASK, BPL>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  2 * kXsStage + kXsMaxDim * 4) == hipSuccess;
     (void)attr;
-    hipLaunchKernelGGL(ts_fwd_x3s_kernel<MASK>, dim3(grid), dim3(kXThreads), lds, st, q);
+    hipLaunchKernelGGL((ts_fwd_x3s_kernel<MASK, BPL>), dim3(grid), dim3(kXThreads), lds, st, q);
 }
 
 template <int NWV, int JPW, int DEP, bool MASK>
@@ -1892,10 +1962,17 @@ bool launch_rows(const TsParams& p, hipStream_t st) {
                 if (q.nchunk != 1) q.out_neg = nullptr;  // the epilogue reduces a row only when one block holds it
                 if (xs_ok) {  // operands split once at staging (ts_fwd_x3s_kernel, bitwise ts_fwd_x3_kernel's scores)
                     const size_t lds = 2 * (size_t)kXsStage + (size_t)p.d * 4;
-                    if (q.Mpre)
-                        launch_x3s<false>(q, (unsigned)(p.B * q.nchunk), lds, st);
-                    else
-                        launch_x3s<true>(q, (unsigned)(p.B * q.nchunk), lds, st);
+                    if (q.mplanes) {  // M_r split once for every block of the relation (workspace)
+                        const int64_t n = (p.nrel) * q.mp_nk * (int64_t)q.mp_cols;
+                        hipLaunchKernelGGL(ts_mplanes_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock),
+                                           0, st, q.Mpre ? q.Mpre : q.W, q.Mpre ? nullptr : q.mask, p.nrel, p.d,
+                                           q.mp_cols, q.mp_nk, q.mplanes);
+                        launch_x3s<false, true>(q, (unsigned)(p.B * q.nchunk), lds, st);
+                    } else if (q.Mpre) {
+                        launch_x3s<false, false>(q, (unsigned)(p.B * q.nchunk), lds, st);
+                    } else {
+                        launch_x3s<true, false>(q, (unsigned)(p.B * q.nchunk), lds, st);
+                    }
                     return q.nchunk == 1;
                 }
                 hipLaunchKernelGGL(ts_fwd_x3_kernel, dim3((unsigned)(p.B * q.nchunk)), dim3(kXThreads), lds, st, q);
@@ -1973,8 +2050,10 @@ int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_l
 }
 
 size_t kge_transparse_score_workspace_size(int mode, int64_t nrel, int64_t B, int64_t d) {
-    // only the grouped rows (single / tail-batch) split; the partial projections [ksplit][B][xsplit 128] floats
-    if (mode == KGE_HEAD_BATCH || B <= 0 || d <= 0 || d > kXsMaxDim || nrel < 0) return 0;
+    if (B <= 0 || d <= 0 || d > kXsMaxDim || nrel < 0) return 0;
+    // head-batch: M_r as bf16 planes for the 256-row kernel
+    if (mode == KGE_HEAD_BATCH) return (size_t)mplanes_bytes(nrel, d);
+    // the grouped rows (single / tail-batch): the partial projections [ksplit][B][xsplit 128] floats
     const int64_t xs = xg_xsplit(d), ks = xg_ksplit(d);
     return xs * ks > 1 ? (size_t)(ks * B * xs * kXgSplitCols) * sizeof(float) : 0;
 }
@@ -1994,10 +2073,16 @@ static int ts_score_impl(int mode, const float* ent, int64_t nent, int64_t ent_l
     if (workspace && need) {
         if (workspace_bytes < need) return set_error(KGE_EINVAL, "kge_transparse_score_ex: workspace too small");
         if ((uintptr_t)workspace & 15) return set_error(KGE_EINVAL, "kge_transparse_score_ex: workspace not 16-B aligned");
-        p.xsplit = (int)xg_xsplit(d);
-        p.ksplit = (int)xg_ksplit(d);
-        p.xk = reinterpret_cast<float*>(workspace);
-        p.xk_ld = (int64_t)p.xsplit * kXgSplitCols;
+        if (p.grouped) {
+            p.xsplit = (int)xg_xsplit(d);
+            p.ksplit = (int)xg_ksplit(d);
+            p.xk = reinterpret_cast<float*>(workspace);
+            p.xk_ld = (int64_t)p.xsplit * kXgSplitCols;
+        } else {
+            p.mplanes = reinterpret_cast<__bf16*>(workspace);
+            p.mp_cols = (int)((d + XBC - 1) / XBC * XBC);
+            p.mp_nk = (int)((d + 15) / 16);
+        }
     }
     if (B == 0 || (!p.grouped && N == 0)) return 0;
     if (!ent || !rel || !W || !pos || !out || (!p.grouped && !neg))
@@ -2026,7 +2111,9 @@ int kge_transparse_score_ex(int mode, const float* ent, int64_t nent, int64_t en
 }
 
 size_t kge_transparse_step_workspace_size(int64_t nrel, int64_t B, int64_t d) {
-    return kge_transparse_score_workspace_size(KGE_SINGLE, nrel, B, d);  // the grouped calls' split; head-batch none
+    // the calls run in order on one stream: the head-batch planes, then the grouped rows' partial projections
+    return std::max(kge_transparse_score_workspace_size(KGE_HEAD_BATCH, nrel, B, d),
+                    kge_transparse_score_workspace_size(KGE_SINGLE, nrel, B, d));
 }
 
 int kge_transparse_step_forward(int mode, const float* ent, int64_t nent, int64_t ent_ld, const float* rel,

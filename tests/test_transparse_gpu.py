@@ -180,8 +180,9 @@ def test_trainer_step_matches_oracle_loss():
 @pytest.mark.parametrize("d,N,premul", [(500, 256, True), (500, 300, False), (128, 200, True), (260, 129, False),
                                         (1024, 160, True)])
 def test_split_once_forward_is_bitwise_the_register_split_one(monkeypatch, d, N, premul):
-    """ts_fwd_x3s_kernel (operands split once at staging, buffer loads) against ts_fwd_x3_kernel (the same
-    products split per fragment in the MFMA loop): head-batch scores and stats are bitwise equal, with
+    """ts_fwd_x3s_kernel (operands split once at staging, buffer loads; or M_r from bf16 planes split once per
+    call) against ts_fwd_x3_kernel (the same products split per fragment in the MFMA loop): head-batch scores and
+    stats are bitwise equal, with
     out-of-range ids, partial K chunks and partial column super-tiles; and within 1e-4 of the fp64 oracle."""
     E, R, B, gamma = 300, 3, 5, 12.0
     ent, rel, W, mask = _tables(E, R, d, seed=4)
@@ -191,14 +192,17 @@ def test_split_once_forward_is_bitwise_the_register_split_one(monkeypatch, d, N,
     ed, rd, Wd, md = ent.to(DEV), rel.to(DEV), W.to(DEV), mask.to(DEV)
     M = ops.transparse_premul(Wd, md) if premul else None
     outs = []
-    for form in (1, 0):  # 1: split per fragment in registers (ts_fwd_x3_kernel), 0: split once (ts_fwd_x3s_kernel)
+    # 1: split per fragment in registers (ts_fwd_x3_kernel); 0 + workspace: M_r split once into bf16 planes per
+    # call (ts_mplanes_kernel + ts_fwd_x3s_kernel<.., true>); 0 without: split once at staging (ts_fwd_x3s_kernel)
+    for form, split in ((1, True), (0, True), (0, False)):
         st = torch.empty((B * N, 2), dtype=torch.float32, device=DEV)
         s = ops.transparse_score_raw(0, ed, rd, Wd, md, pos.to(DEV), neg.to(DEV), gamma, stats=st, M=M,
-                                     forms=dict(transparse_form=form))
+                                     forms=dict(transparse_form=form), split=split)
         torch.cuda.synchronize()
         outs.append((s.cpu(), st.cpu()))
-    assert np.array_equal(outs[0][0].numpy(), outs[1][0].numpy(), equal_nan=True)
-    assert np.array_equal(outs[0][1].numpy(), outs[1][1].numpy(), equal_nan=True)
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0].numpy(), o[0].numpy(), equal_nan=True)
+        assert np.array_equal(outs[0][1].numpy(), o[1].numpy(), equal_nan=True)
     ok = (neg >= 0) & (neg < E)
     ref, _ = _oracle(ent, rel, W, mask, pos, neg.clamp(0, E - 1), 0, gamma)
     got = outs[1][0].numpy()

@@ -839,18 +839,22 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                                  torch.cuda.current_stream().cuda_stream)
 
     def step(b, ev=None):
-        """One query batch: Q = h*r or r*t (kge_eval_query), S = Q . E^T (the query's bf16 planes and
-        kge_gemm_nt_bf16x3_planes on the pass's entity planes, events around both; or kge_gemm_nt_bf16x3), exact
-        filtered ranks."""
+        """One query batch: Q = h*r or r*t written as bf16 planes (kge_eval_query_planes), S = Q . E^T
+        (kge_gemm_nt_bf16x3_planes on the pass's entity planes, events around it; or kge_eval_query +
+        kge_gemm_nt_bf16x3, the staging form), exact filtered ranks."""
         pos, mode, truth, fptr, fids = b
         st = torch.cuda.current_stream().cuda_stream
-        lib.kge_eval_query(FN_IDS[w["fn"]], 0 if mode == "head-batch" else 1, ent.data_ptr(), E, ent.stride(0),
-                           m.relation_embedding.data_ptr(), R, m.relation_embedding.stride(0), pos.data_ptr(), Bq,
-                           m._D, Q.data_ptr(), K, st)
+        md = 0 if mode == "head-batch" else 1
+        rel_ = m.relation_embedding
+        if split == "planes":
+            lib.kge_eval_query_planes(FN_IDS[w["fn"]], md, ent.data_ptr(), E, ent.stride(0), rel_.data_ptr(), R,
+                                      rel_.stride(0), pos.data_ptr(), Bq, m._D, qp.data_ptr(), Bq, st)
+        else:
+            lib.kge_eval_query(FN_IDS[w["fn"]], md, ent.data_ptr(), E, ent.stride(0), rel_.data_ptr(), R,
+                               rel_.stride(0), pos.data_ptr(), Bq, m._D, Q.data_ptr(), K, st)
         if ev is not None:
             ev[0].record()
         if split == "planes":
-            lib.kge_split_bf16x3(Q.data_ptr(), Bq, K, K, qp.data_ptr(), Bq, st)
             lib.kge_gemm_nt_bf16x3_planes(qp.data_ptr(), Bq, ep.data_ptr(), E, K, S.data_ptr(), E, Bq, E, st)
         else:
             lib.kge_gemm_nt_bf16x3(Q.data_ptr(), K, ent.data_ptr(), ent.stride(0), S.data_ptr(), E, Bq, E, K, st)
@@ -900,8 +904,9 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                        "parallelism": f"replicas{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": mfma_flops / gemm_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                          "frac": mfma_flops / gemm_s / 1e12 / 2500.0, "traffic": None,
-                         "kernel": ("split3_planes_kernel (the query block's bf16 planes) + gemm_nt_x3p_kernel (256 x "
-                                    "256 tiles from the query and entity bf16 planes, no conversion in the loop, six "
+                         "kernel": ("gemm_nt_x3p_kernel (256 x 256 tiles from the query planes, which "
+                                    "kge_eval_query_planes writes directly, and the entity bf16 planes, no "
+                                    "conversion in the loop, six "
                                     "products per 16 k on v_mfma_f32_32x32x16_bf16; the entity planes made once per "
                                     "evaluation pass, inside the timed region)" if split == "planes" else
                                     "gemm_nt_x3s_kernel (256 x 256 tiles, operands split once at staging into bf16 "

@@ -1112,6 +1112,35 @@ int kge_eval_query(int fn, int mode, const float* ent, int64_t nentity, int64_t 
     return check_launch("kge_eval_query");
 }
 
+int kge_eval_query_planes(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                          int64_t nrelation, int64_t rel_ld, const int64_t* pos, int64_t B, int64_t D, void* planes,
+                          int64_t plane_rows, void* stream) {
+    int rc = check_fn_mode(fn, mode);
+    if (rc) return rc;
+    if (fn != KGE_DISTMULT && fn != KGE_COMPLEX)
+        return fail(KGE_ENOTSUP, "kge_eval_query_planes: only DistMult and ComplEx score as a dense contraction");
+    if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_eval_query_planes needs mode 0 or 1");
+    if (B < 0 || D <= 0 || plane_rows < B) return fail(KGE_EINVAL, "bad shape");
+    if (B == 0) return ok();
+    if (!ent || !rel || !pos || !planes) return fail(KGE_EINVAL, "null pointer");
+    if (!aligned(planes, 16)) return fail(KGE_EINVAL, "kge_eval_query_planes: planes not 16-B aligned");
+    ScoreParams p;
+    fill_indexed(p, fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, 0, pos, nullptr, 0, B, 1, D, 0.f, 1.f,
+                 0.f);
+    int V = 1, G = 1;
+    rc = pick_vg(p, V, G);
+    if (rc) return rc;
+    if (V != 4) return fail(KGE_ENOTSUP, "kge_eval_query_planes needs D % 4 == 0 and 16-B aligned tables");
+    G = 1;
+    while (G * kWave * V < D) G <<= 1;
+    if (G > kMaxG) return fail(KGE_ENOTSUP, "dimension too large");
+    const int64_t blocks = (B + kWavesPerBlock - 1) / kWavesPerBlock;
+    rc = launch_eval_query_any(fn, mode == KGE_HEAD_BATCH, p, (hipStream_t)stream, (int)blocks, V, G, nullptr, 0,
+                               planes, plane_rows);
+    if (rc) return fail(rc, "no eval-query kernel for this width");
+    return check_launch("kge_eval_query_planes");
+}
+
 int kge_gemm_nt(const float* A, int64_t lda, const float* Bm, int64_t ldb, float* C, int64_t ldc, int64_t M,
                 int64_t N, int64_t K, void* stream) {
     if (M < 0 || N < 0 || K < 0) return fail(KGE_EINVAL, "bad shape");

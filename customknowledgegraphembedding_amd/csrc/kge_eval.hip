@@ -25,8 +25,19 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // Query operand rows for the MFMA contraction: Q[b] = q0 (DistMult) or [q0 | q1] (ComplEx), built by
 // the same Query<> code the scoring kernels use (tail mode: (h, r); head mode: (r, t)).
 // ---------------------------------------------------------------------------------------------
+typedef float xs_f32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 xs_bf16x4_t __attribute__((ext_vector_type(4)));
+// xs_split3's arithmetic (the planes' three bf16 terms)
+__device__ __forceinline__ void xs_split3_t(xs_f32x4_t v, xs_bf16x4_t& a0, xs_bf16x4_t& a1, xs_bf16x4_t& a2) {
+    a0 = __builtin_convertvector(v, xs_bf16x4_t);
+    const xs_f32x4_t r1 = v - __builtin_convertvector(a0, xs_f32x4_t);
+    a1 = __builtin_convertvector(r1, xs_bf16x4_t);
+    a2 = __builtin_convertvector(r1 - __builtin_convertvector(a1, xs_f32x4_t), xs_bf16x4_t);
+}
+
 template <int FN, bool CH, int V, int G>
-__global__ __launch_bounds__(kBlock) void eval_query_kernel(ScoreParams p, float* __restrict__ Q, int64_t ldq) {
+__global__ __launch_bounds__(kBlock) void eval_query_kernel(ScoreParams p, float* __restrict__ Q, int64_t ldq,
+                                                            __bf16* __restrict__ P, int64_t prows) {
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (b >= p.B) return;
     const int lane = threadIdx.x & 63;
@@ -35,6 +46,31 @@ __global__ __launch_bounds__(kBlock) void eval_query_kernel(ScoreParams p, float
     bool qok, rok;
     build_query_for<FN, CH, V, G>(p, b, lane, q, qi, ri, qok, rok);
     const int DV = p.D / V;
+    if constexpr (V == 4) {
+        if (P) {  // kge_eval_query_planes: the row straight into the GEMM's bf16 planes (split3_planes_kernel's
+                  // arithmetic and layout, [kp / 16][prows][16] per plane, k past K zero)
+            const int K = FN == KGE_COMPLEX ? 2 * p.D : p.D, kp = (K + 15) / 16 * 16;
+            const int64_t plane = prows * kp;
+            auto put = [&](int k, const vecf<4>& v) {
+                xs_bf16x4_t s0, s1, s2;
+                xs_split3_t(xs_f32x4_t{v.a[0], v.a[1], v.a[2], v.a[3]}, s0, s1, s2);
+                __bf16* d = P + ((int64_t)(k >> 4) * prows + b) * 16 + (k & 15);
+                *reinterpret_cast<xs_bf16x4_t*>(d) = s0;
+                *reinterpret_cast<xs_bf16x4_t*>(d + plane) = s1;
+                *reinterpret_cast<xs_bf16x4_t*>(d + 2 * plane) = s2;
+            };
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                const int g = lane + k * kWave;
+                if (g < DV) {
+                    put(4 * g, q.q0[k]);
+                    if constexpr (FN == KGE_COMPLEX) put(p.D + 4 * g, q.q1[k]);
+                }
+            }
+            for (int k = K + 4 * lane; k < kp; k += 4 * kWave) put(k, vzero<4>());  // the zero pad of the last chunk
+            return;
+        }
+    }
     float* row = Q + b * ldq;
 #pragma unroll
     for (int k = 0; k < G; ++k) {
@@ -341,10 +377,12 @@ __global__ __launch_bounds__(kBlock) void rank_kernel(const float* __restrict__ 
 }
 
 template <int FN, bool CH>
-int launch_eval_query(const ScoreParams& p, hipStream_t st, int blocks, int V, int G, float* Q, int64_t ldq) {
+int launch_eval_query(const ScoreParams& p, hipStream_t st, int blocks, int V, int G, float* Q, int64_t ldq,
+                      __bf16* P, int64_t prows) {
 #define KGE_EQ(VV, GG)                                                                                   \
     if (V == VV && G == GG) {                                                                            \
-        hipLaunchKernelGGL((eval_query_kernel<FN, CH, VV, GG>), dim3(blocks), dim3(kBlock), 0, st, p, Q, ldq); \
+        hipLaunchKernelGGL((eval_query_kernel<FN, CH, VV, GG>), dim3(blocks), dim3(kBlock), 0, st, p, Q, ldq, P, \
+                           prows);                                                                       \
         return 0;                                                                                        \
     }
     KGE_EQ(4, 1) KGE_EQ(4, 2) KGE_EQ(4, 4) KGE_EQ(4, 8)
@@ -357,13 +395,14 @@ int launch_eval_query(const ScoreParams& p, hipStream_t st, int blocks, int V, i
 }  // namespace
 
 int launch_eval_query_any(int fn, bool ch, const ScoreParams& p, hipStream_t st, int blocks, int V, int G, float* Q,
-                          int64_t ldq) {
+                          int64_t ldq, void* P, int64_t prows) {
+    __bf16* pp = static_cast<__bf16*>(P);
     if (fn == KGE_DISTMULT)
-        return ch ? launch_eval_query<KGE_DISTMULT, true>(p, st, blocks, V, G, Q, ldq)
-                  : launch_eval_query<KGE_DISTMULT, false>(p, st, blocks, V, G, Q, ldq);
+        return ch ? launch_eval_query<KGE_DISTMULT, true>(p, st, blocks, V, G, Q, ldq, pp, prows)
+                  : launch_eval_query<KGE_DISTMULT, false>(p, st, blocks, V, G, Q, ldq, pp, prows);
     if (fn == KGE_COMPLEX)
-        return ch ? launch_eval_query<KGE_COMPLEX, true>(p, st, blocks, V, G, Q, ldq)
-                  : launch_eval_query<KGE_COMPLEX, false>(p, st, blocks, V, G, Q, ldq);
+        return ch ? launch_eval_query<KGE_COMPLEX, true>(p, st, blocks, V, G, Q, ldq, pp, prows)
+                  : launch_eval_query<KGE_COMPLEX, false>(p, st, blocks, V, G, Q, ldq, pp, prows);
     return KGE_ENOTSUP;
 }
 

@@ -214,7 +214,7 @@ int launch_protate(const ScoreParams& p, int kind, hipStream_t st, int blocks, b
 
 // link-prediction evaluation (kge_eval.hip)
 int launch_eval_query_any(int fn, bool ch, const ScoreParams& p, hipStream_t st, int blocks, int V, int G, float* Q,
-                          int64_t ldq);
+                          int64_t ldq, void* P = nullptr, int64_t prows = 0);
 int launch_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
                    int64_t ldc, hipStream_t st);
 int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,

@@ -97,13 +97,27 @@ def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor
         return out
     if model.model_name in MFMA_FNS:
         K = ent.shape[1]
-        Q = torch.empty((B, K), dtype=torch.float32, device=dev)
         lib = _lib.load()
-        check(lib.kge_eval_query(FN_IDS[model.model_name], m, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(),
+        fq = FN_IDS[model.model_name]
+        # S = Q . E^T at fp32 accuracy on the bf16 matrix cores (bf16x3 terms, six products): from the pass's
+        # entity planes and the batch's query planes (kge_eval_query_planes: the query rows written as planes, one
+        # launch), or with the operands split at staging
+        if planes is not None and model._D % 4 == 0 and ent.data_ptr() % 16 == 0 and rel.data_ptr() % 16 == 0:
+            key = (str(dev), st)
+            nbytes = int(lib.kge_split_bf16x3_bytes(B, K))
+            qp = _Q_PLANES.get(key)
+            if qp is None or qp.numel() < nbytes:
+                qp = _Q_PLANES[key] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            check(lib.kge_eval_query_planes(fq, m, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(), rel.shape[0],
+                                            rel.stride(0), positive_sample.data_ptr(), B, model._D, qp.data_ptr(), B,
+                                            st), "kge_eval_query_planes")
+            check(lib.kge_gemm_nt_bf16x3_planes(qp.data_ptr(), B, planes.data_ptr(), E, K, out.data_ptr(),
+                                                out.stride(0), B, E, st), "kge_gemm_nt_bf16x3_planes")
+            return out
+        Q = torch.empty((B, K), dtype=torch.float32, device=dev)
+        check(lib.kge_eval_query(fq, m, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(),
                                  rel.shape[0], rel.stride(0), positive_sample.data_ptr(), B, model._D, Q.data_ptr(),
                                  Q.stride(0), st), "kge_eval_query")
-        # S = Q . E^T at fp32 accuracy on the bf16 matrix cores (bf16x3 terms, six products): from the pass's
-        # entity planes and the batch's query planes, or with the operands split at staging
         if planes is not None:
             key = (str(dev), st)
             qp = _Q_PLANES[key] = split_planes(Q, _Q_PLANES.get(key))

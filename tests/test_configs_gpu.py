@@ -66,10 +66,12 @@ def test_c2_wn18rr_interht_full_size_real_positives():
     _step_forward_vs_oracle("InterHT", 40943, 11, 1000, 24.0, True, False, True, "wn18rr", 512, 256)
 
 
-def _all_rows_vs_oracle(name, E, R, d, gamma, de, dr, tr, key, B, N, modes, outputs, chunk=64):
+def _all_rows_vs_oracle(name, E, R, d, gamma, de, dr, tr, key, B, N, modes, outputs, chunk=64, useful=False):
     """Every batch row of a full-size step (not the sampled ROWS) against the fp64 oracle, in chunks of rows
     so the oracle's [chunk, N, d] gathers stay small: the raw scores, and with `outputs` the two calls' row
-    outputs (self-adversarial negative term, positive log-sigmoid)."""
+    outputs (self-adversarial negative term, positive log-sigmoid). `useful`: the row outputs from the selected
+    branch only (O.adv_reduce of the reference scores, O.score in mode 3: tf_call's values whenever no branch
+    is NaN, at a third of the oracle's work)."""
     m = kge.TFKGEModel(name, E, R, d, gamma, double_entity_embedding=de, double_relation_embedding=dr,
                        triple_relation_embedding=tr, device=DEV, seed=0)
     ent = m.entity_embedding.detach().cpu().double()
@@ -87,7 +89,12 @@ def _all_rows_vs_oracle(name, E, R, d, gamma, de, dr, tr, key, B, N, modes, outp
             rows = slice(r0, min(B, r0 + chunk))
             ref_s = O.score(name, ent, rel, pos[rows], neg[rows], mode, gamma, m._range_f).numpy()
             worst = max(worst, rel_close(ns[rows], ref_s))
-            if outputs:
+            if outputs and useful:
+                ref_n = O.adv_reduce(torch.from_numpy(ref_s)).numpy()[:, 0]
+                ref_p = torch.nn.functional.logsigmoid(
+                    O.score(name, ent, rel, pos[rows], neg[rows], 3, gamma, m._range_f)).numpy()[:, 0]
+                worst = max(worst, rel_close(out_neg[rows], ref_n), rel_close(out_pos[rows], ref_p))
+            elif outputs:
                 ref_n = O.tf_call(name, ent, rel, pos[rows], neg[rows], mode, gamma, m._range_f).numpy()[:, 0]
                 ref_p = O.tf_call(name, ent, rel, pos[rows], neg[rows], 3, gamma, m._range_f).numpy()[:, 0]
                 worst = max(worst, rel_close(out_neg[rows], ref_n), rel_close(out_pos[rows], ref_p))
@@ -100,12 +107,18 @@ def test_c2_every_row_full_size():
     _all_rows_vs_oracle("InterHT", 40943, 11, 1000, 24.0, True, False, True, "wn18rr", 512, 256, (0, 1), True)
 
 
-def test_c3_c4_every_row_scores_full_size():
-    """C3 head-batch and C4 tail-batch: every row's raw scores of a full-size step against the fp64 oracle
-    (the other modes and the row outputs are covered on sampled rows above)."""
-    _all_rows_vs_oracle("RotatE", 14541, 237, 1000, 9.0, True, False, False, "fb15k237", 512, 256, (0,), False)
-    _all_rows_vs_oracle("DistMult", 123182, 37, 500, 24.0, False, False, False, "yago3_10", 512, 1024, (1,), False,
-                        chunk=32)
+def test_c3_every_row_full_size():
+    """C3: every row of a full-size FB15k-237 RotatE step, both modes, raw scores and both calls' row outputs
+    against the fp64 oracle."""
+    _all_rows_vs_oracle("RotatE", 14541, 237, 1000, 9.0, True, False, False, "fb15k237", 512, 256, (0, 1), True,
+                        useful=True)
+
+
+def test_c4_every_row_full_size():
+    """C4 (unsharded): every row of a full-size YAGO3-10 DistMult N = 1 024 step, both modes, raw scores and both
+    calls' row outputs against the fp64 oracle."""
+    _all_rows_vs_oracle("DistMult", 123182, 37, 500, 24.0, False, False, False, "yago3_10", 512, 1024, (0, 1), True,
+                        chunk=32, useful=True)
 
 
 def test_c2_xcd_phases_bitwise():

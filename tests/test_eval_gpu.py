@@ -214,3 +214,44 @@ def test_score_all_with_entity_planes_is_bitwise_the_per_call_split():
             b = evaluate.score_all(m, pos, mode, planes=planes)
             torch.cuda.synchronize()
             assert torch.equal(a, b), (name, mode)
+
+
+@pytest.mark.parametrize("fn,D,B,mode", [("DistMult", 1000, 300, 0), ("DistMult", 36, 70, 1), ("ComplEx", 500, 130, 1),
+                                         ("ComplEx", 24, 9, 0)])
+def test_eval_query_planes_is_bitwise_query_then_split(fn, D, B, mode):
+    """kge_eval_query_planes (the query rows written straight into the GEMM's bf16 planes, the zero pad of the
+    last 16-k chunk included) is bitwise kge_eval_query followed by kge_split_bf16x3, and the plane GEMM on it
+    gives the same scores; plane rows beyond B are never read."""
+    from customknowledgegraphembedding_amd import _lib as L
+    lib = L.load()
+    E, R = 400, 7
+    torch.manual_seed(3)
+    d_ent = 2 * D if fn == "ComplEx" else D
+    ent = (torch.rand(E, d_ent, device=DEV) - 0.5)
+    rel = (torch.rand(R, d_ent, device=DEV) - 0.5)
+    g = np.random.RandomState(5)
+    pos = torch.from_numpy(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1)).to(DEV)
+    K = d_ent
+    st = torch.cuda.current_stream().cuda_stream
+    fq = L.FN_IDS[fn]
+    Q = torch.empty((B, K), dtype=torch.float32, device=DEV)
+    assert lib.kge_eval_query(fq, mode, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(), R, rel.stride(0),
+                              pos.data_ptr(), B, D, Q.data_ptr(), K, st) == 0
+    nb = int(lib.kge_split_bf16x3_bytes(B + 5, K))
+    ref = torch.zeros(nb, dtype=torch.uint8, device=DEV)
+    got = torch.full((nb,), 0x7F, dtype=torch.uint8, device=DEV)  # garbage everywhere the kernel does not write
+    assert lib.kge_split_bf16x3(Q.data_ptr(), B, K, K, ref.data_ptr(), B + 5, st) == 0
+    assert lib.kge_eval_query_planes(fq, mode, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(), R, rel.stride(0),
+                                     pos.data_ptr(), B, D, got.data_ptr(), B + 5, st) == 0
+    torch.cuda.synchronize()
+    kp = (K + 15) // 16 * 16
+    r = ref.view(torch.bfloat16).view(3, kp // 16, B + 5, 16)[:, :, :B]
+    q = got.view(torch.bfloat16).view(3, kp // 16, B + 5, 16)[:, :, :B]
+    assert torch.equal(r.view(torch.int16), q.view(torch.int16))
+    ep = evaluate.split_planes(ent)
+    S1 = torch.empty((B, E), dtype=torch.float32, device=DEV)
+    S2 = torch.empty((B, E), dtype=torch.float32, device=DEV)
+    assert lib.kge_gemm_nt_bf16x3_planes(ref.data_ptr(), B + 5, ep.data_ptr(), E, K, S1.data_ptr(), E, B, E, st) == 0
+    assert lib.kge_gemm_nt_bf16x3_planes(got.data_ptr(), B + 5, ep.data_ptr(), E, K, S2.data_ptr(), E, B, E, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(S1, S2)

@@ -152,3 +152,22 @@ def test_step_forward_order_choice_reads_no_environment(monkeypatch):
     assert lib.kge_step_forward_order(123182, 1024) == 2  # C4
     assert lib.kge_step_forward_order(40943, 127) == 0
     assert lib.kge_step_forward_order(8 << 25, 256) == 0
+
+
+def test_workspace_queries_are_host_arithmetic():
+    """The round-5 workspace and plane-size queries (no GPU needed): TranSparse head-batch M_r planes
+    [R][3][K / 16][columns rounded to 256][16] bf16, the single / tail-batch partial projections
+    [ksplit][B][xsplit 128] fp32, the step's maximum of the two, and the bf16x3 planes of a [rows, K] matrix."""
+    lib = _lib.load()
+    R, B, d = 11, 512, 500
+    planes = R * 3 * ((d + 15) // 16) * ((d + 255) // 256 * 256) * 16 * 2
+    ksplit, xsplit = ((d + 15) // 16 + 7) // 8, (d + 127) // 128
+    xk = ksplit * B * xsplit * 128 * 4
+    assert lib.kge_transparse_score_workspace_size(0, R, B, d) == planes
+    assert lib.kge_transparse_score_workspace_size(3, R, B, d) == xk
+    assert lib.kge_transparse_score_workspace_size(1, R, B, d) == xk
+    assert lib.kge_transparse_step_workspace_size(R, B, d) == max(planes, xk)
+    assert lib.kge_transparse_score_workspace_size(0, R, B, 2048) == 0    # past the planes form's d <= 1024
+    assert lib.kge_transparse_score_workspace_size(3, R, B, 100) == 0     # one 128-column, one 128-k range
+    assert lib.kge_split_bf16x3_bytes(4096, 1000) == 3 * 4096 * 1008 * 2
+    assert lib.kge_split_bf16x3_bytes(7, 36) == 3 * 7 * 48 * 2

@@ -703,14 +703,12 @@ def native_host_cost(tables, world, device, batches, steps):
 def shard_sim_bench(device, world=8, reps=10, v1=None):
     """Single-GPU evidence for the row-sharded scaling at the full C4 size (YAGO3-10
     DistMult d=500, E=123182, N=1024, global batch of world x 512 rows):
-      * the WHOLE `world`-rank forward step on this GPU: every rank a thread (ThreadComm: the
-        all-gather / all-to-all are device copies here), every rank's kernels serialised on one device;
       * rank 0's own kernels of one step (plan, per-chunk query gather and compact scoring, finish),
         timed alone with events on the launch stream: the per-GPU compute of an N-GPU step;
       * the payload rank 0's collectives carry per step, and the RCCL bandwidth a step needs to reach
         6x the 1-GPU row-sharded throughput `v1` (triples/s) when the collectives do not overlap;
       * the sharded train step's kernels of rank 0 (forward, combine, backward)."""
-    from customknowledgegraphembedding_amd.distributed import HipShardKernels, ShardedKGE, ThreadComm, run_threads
+    from customknowledgegraphembedding_amd.distributed import HipShardKernels, ShardedKGE, ThreadComm
     from customknowledgegraphembedding_amd.model import TFKGEModel
     w = WORKLOADS["c4s"]
     E, d, N = w["nentity"], w["hidden_dim"], w["N"]
@@ -742,9 +740,6 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
     comm = ThreadComm(world)
     ranks = [ShardedKGE("DistMult", E, w["nrelation"], d, w["gamma"], device=device, world=world, rank=r, comm=comm,
                         full_tables=tables) for r in range(world)]
-    t0 = time.perf_counter()
-    sim_dev_us = timed(lambda: run_threads([lambda sk=sk: sk.step_forward(pos, neg, 0) for sk in ranks]), 3, False)
-    sim_wall_us = (time.perf_counter() - t0) / 4 * 1e6
     # rank 0 alone: the kernels of one step, with the other ranks' contributions prepared untimed
     HK = HipShardKernels
     r0 = ranks[0]
@@ -761,8 +756,6 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
     B_ = Bg // world
     out = {"workload": f"C4 YAGO3-10 DistMult d=500 N=1024, global batch {world} x 512 (YAGO3-10 positives), "
                        f"entity table split over {world} simulated ranks",
-           "step_us_all_ranks_one_gpu": sim_dev_us,
-           "step_wall_us_all_ranks_one_gpu": sim_wall_us,
            "rank_step_kernels_us": {"plan_side_stream": t_plan, "query_gather": t_gather, "compact_scoring": t_score,
                                     "finish": t_finish, "critical_path": rank_us},
            "host_us_per_rank_step": rank_host_cost(tables, world, device),
@@ -775,9 +768,8 @@ def shard_sim_bench(device, world=8, reps=10, v1=None):
            "chunks": K,
            "what": "rank_step_kernels_us: rank 0's kernels of one 8-rank step, device time (queued behind a sleep "
                    "kernel): its per-GPU compute in an 8-GPU step (critical_path: without the plan, which the "
-                   "step makes a step ahead on a side stream); step_us_all_ranks_one_gpu: the whole 8-rank "
-                   "ShardedKGE.step_forward by 8 threads on this GPU (every rank's kernels serialised, ThreadComm "
-                   "device copies standing in for RCCL, host-bound)"}
+                   "step makes a step ahead on a side stream); collective_bytes_per_rank_step: what its two "
+                   "all-to-alls carry; six_x_target: the RCCL rate those bytes need for 6x the 1-GPU line"}
     if v1:
         t6 = world * B_ * (N + 1) / (6.0 * v1) * 1e6  # us per step at 6x the 1-GPU throughput
         out["six_x_target"] = {"one_gpu_triples_per_s": v1, "step_budget_us": t6,

@@ -90,6 +90,7 @@ SIGNATURES = {
         _c_i, [_c_p, _c_i, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_f,
                _c_f, _c_i, _c_p, _c_p, _c_i64, _c_p]),
     "kge_step_planner_set_modulus": (_c_i, [_c_p, _c_f]),
+    "kge_step_planner_set_sweep": (_c_i, [_c_p, _c_i]),
     "kge_step_planner_plan": (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i]),
     "kge_step_planner_step": (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_i, _c_p, _c_p, _c_p, _c_p]),
     "kge_step_planner_destroy": (_c_i, [_c_p]),
@@ -153,6 +154,8 @@ SIGNATURES = {
     "kge_split_bf16x3_bytes": (_c_i64, [_c_i64, _c_i64]),
     "kge_split_bf16x3": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
     "kge_gemm_nt_bf16x3_planes": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p]),
+    "kge_gemm_nt_bf16x3_planes_ex": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p,
+                                            _c_p]),
     "kge_rank_filtered": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "kge_score_dense": (
         _c_i,

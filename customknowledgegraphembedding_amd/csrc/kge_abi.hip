@@ -853,12 +853,30 @@ int kge_step_plan(int fn, int mode, int64_t nentity, int64_t ent_ld, int64_t nre
     return check_launch("kge_step_plan");
 }
 
+static int step_forward_planned(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                                int64_t nrelation, int64_t rel_ld, int64_t rel_off, int64_t B, int64_t N, int64_t D,
+                                float gamma, float emb_range, float modulus, float temperature, int adversarial,
+                                const void* plan, const int64_t* next_pos, const int64_t* next_neg,
+                                int64_t next_neg_ld, int next_mode, void* next_plan, float* neg_scores, int64_t ns_ld,
+                                float* out_neg, float* pos_scores, float* out_pos, int reverse, void* stream);
+
 int kge_step_forward_planned(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
                              int64_t nrelation, int64_t rel_ld, int64_t rel_off, int64_t B, int64_t N, int64_t D,
                              float gamma, float emb_range, float modulus, float temperature, int adversarial,
                              const void* plan, const int64_t* next_pos, const int64_t* next_neg, int64_t next_neg_ld,
                              int next_mode, void* next_plan, float* neg_scores, int64_t ns_ld, float* out_neg,
                              float* pos_scores, float* out_pos, void* stream) {
+    return step_forward_planned(fn, mode, ent, nentity, ent_ld, rel, nrelation, rel_ld, rel_off, B, N, D, gamma,
+                                emb_range, modulus, temperature, adversarial, plan, next_pos, next_neg, next_neg_ld,
+                                next_mode, next_plan, neg_scores, ns_ld, out_neg, pos_scores, out_pos, 0, stream);
+}
+
+static int step_forward_planned(int fn, int mode, const float* ent, int64_t nentity, int64_t ent_ld, const float* rel,
+                                int64_t nrelation, int64_t rel_ld, int64_t rel_off, int64_t B, int64_t N, int64_t D,
+                                float gamma, float emb_range, float modulus, float temperature, int adversarial,
+                                const void* plan, const int64_t* next_pos, const int64_t* next_neg,
+                                int64_t next_neg_ld, int next_mode, void* next_plan, float* neg_scores, int64_t ns_ld,
+                                float* out_neg, float* pos_scores, float* out_pos, int reverse, void* stream) {
     int rc = check_fn_mode(fn, mode);
     if (rc) return rc;
     if (mode == KGE_SINGLE) return fail(KGE_EINVAL, "kge_step_forward_planned needs a negative mode (0 or 1)");
@@ -889,6 +907,7 @@ int kge_step_forward_planned(int fn, int mode, const float* ent, int64_t nentity
     p.out_pos_raw = pos_scores;
     p.out_pos_ls = out_pos;
     p.tile_pos = 1;
+    p.tile_rev = reverse;
     p.tile_plan = reinterpret_cast<const int*>(plan);
     // the next batch's plan: the scoring launch's tail blocks, on the CUs its scoring blocks free up at its end
     // (C2 device time per step, alternating modes: 93.6 us; made beside the row reductions 99.5 us, as a launch
@@ -916,6 +935,8 @@ struct kge_step_planner {
     void* plans[2] = {nullptr, nullptr};
     int cur = -1;  // the buffer holding the next step's plan (-1: none)
     int mode = 0;  // that plan's batch mode
+    int sweep = 0;      // kge_step_planner_set_sweep: 1 = the tile sweep's direction alternates step by step
+    int64_t steps = 0;  // steps issued
     void* stream = nullptr;
 };
 
@@ -960,6 +981,13 @@ int kge_step_planner_set_modulus(kge_step_planner* sp, float modulus) {
     return ok();
 }
 
+int kge_step_planner_set_sweep(kge_step_planner* sp, int alternate) {
+    if (!sp) return fail(KGE_EINVAL, "kge_step_planner_set_sweep: null pointer");
+    if (alternate != 0 && alternate != 1) return fail(KGE_EINVAL, "kge_step_planner_set_sweep: 0 or 1");
+    sp->sweep = alternate;
+    return ok();
+}
+
 int kge_step_planner_plan(kge_step_planner* sp, const int64_t* pos, const int64_t* neg, int64_t neg_ld, int mode) {
     if (!sp) return fail(KGE_EINVAL, "kge_step_planner_plan: null pointer");
     const int buf = sp->cur < 0 ? 0 : sp->cur;
@@ -976,12 +1004,13 @@ int kge_step_planner_step(kge_step_planner* sp, const int64_t* next_pos, const i
     if (!sp) return fail(KGE_EINVAL, "kge_step_planner_step: null pointer");
     if (sp->cur < 0) return fail(KGE_EINVAL, "kge_step_planner_step: no batch planned (kge_step_planner_plan first)");
     const bool nxt = next_pos && next_neg;
-    const int rc = kge_step_forward_planned(
+    const int rc = step_forward_planned(
         sp->fn, sp->mode, sp->ent, sp->nentity, sp->ent_ld, sp->rel, sp->nrelation, sp->rel_ld, sp->rel_off, sp->B,
         sp->N, sp->D, sp->gamma, sp->emb_range, sp->modulus, sp->temperature, sp->adversarial, sp->plans[sp->cur],
         next_pos, next_neg, next_neg_ld, next_mode, nxt ? sp->plans[1 - sp->cur] : nullptr, neg_scores, sp->N, out_neg,
-        pos_scores, out_pos, sp->stream);
+        pos_scores, out_pos, sp->sweep ? (int)(sp->steps & 1) : 0, sp->stream);
     if (rc) return rc;
+    ++sp->steps;
     if (nxt) {
         sp->cur = 1 - sp->cur;
         sp->mode = next_mode;
@@ -1172,6 +1201,15 @@ int kge_split_bf16x3(const float* X, int64_t rows, int64_t cols, int64_t ld, voi
 
 int kge_gemm_nt_bf16x3_planes(const void* A_planes, int64_t a_rows, const void* B_planes, int64_t b_rows, int64_t K,
                               float* C, int64_t ldc, int64_t M, int64_t N, void* stream) {
+    return kge_gemm_nt_bf16x3_planes_ex(A_planes, a_rows, B_planes, b_rows, K, C, ldc, M, N, nullptr, stream);
+}
+
+// the plane GEMM the library runs (forms->gemm_form 0): 1 = gemm_nt_x3p_kernel, 2 = gemm_nt_x3d_kernel
+constexpr int kPlanesGemmForm = 1;
+
+int kge_gemm_nt_bf16x3_planes_ex(const void* A_planes, int64_t a_rows, const void* B_planes, int64_t b_rows, int64_t K,
+                                 float* C, int64_t ldc, int64_t M, int64_t N, const kge_forms* forms, void* stream) {
+    const int form = forms && (forms->gemm_form == 1 || forms->gemm_form == 2) ? forms->gemm_form : kPlanesGemmForm;
     if (M < 0 || N < 0 || K <= 0 || M > a_rows || N > b_rows) return fail(KGE_EINVAL, "bad shape");
     if (M == 0 || N == 0) return ok();
     if (!A_planes || !B_planes || !C) return fail(KGE_EINVAL, "null pointer");
@@ -1180,7 +1218,7 @@ int kge_gemm_nt_bf16x3_planes(const void* A_planes, int64_t a_rows, const void* 
     if (kge_split_bf16x3_bytes(a_rows, K) >= ((int64_t)1 << 32) - 16 ||
         kge_split_bf16x3_bytes(b_rows, K) >= ((int64_t)1 << 32) - 16)
         return fail(KGE_ENOTSUP, "kge_gemm_nt_bf16x3_planes: planes past 4 GB");
-    launch_gemm_nt_x3p(A_planes, a_rows, B_planes, b_rows, K, C, ldc, (int)M, (int)N, (hipStream_t)stream);
+    launch_gemm_nt_x3p(A_planes, a_rows, B_planes, b_rows, K, C, ldc, (int)M, (int)N, (hipStream_t)stream, form);
     return check_launch("kge_gemm_nt_bf16x3_planes");
 }
 

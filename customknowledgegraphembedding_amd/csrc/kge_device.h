@@ -1121,8 +1121,10 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
     if (pl) {
         const int mode = CH ? KGE_HEAD_BATCH : KGE_TAIL_BATCH;
         if (pl[0] != kPlanMagic || pl[1] != (int)p.B || pl[2] != (int)p.N || pl[3] != mode || pl[4] != R ||
-            pl[5] != (int)p.c_rows) {
-            // not this batch shape's plan: every output of the block's rows (by index) becomes NaN, loudly
+            pl[5] != (int)p.c_rows || (pl[6] != 0) != (p.tile_sort != 0)) {
+            // not this batch shape's plan (or a plan made for a score function with the other row order): every
+            // output of the block's rows (by index) becomes NaN, loudly. A plan of the same shape made from other
+            // ids is not detectable here: kge_step_planner_* (ops.StepPlanner) pairs plans with batches
             if (x == 0)
                 for (int r = w; r < nr; r += NWV) {
                     for (int64_t n = lane; n < p.N; n += kWave) p.out[(g0 + r) * p.out_ld + n] = __builtin_nanf("");
@@ -1399,12 +1401,14 @@ __global__ __launch_bounds__(NWV * kWave) void step_fwd_tile_kernel(ScoreParams 
         int code = 0;
         int64_t my_id = 0;
         if (lane < nc) {
+            // p.tile_rev: the list walked from its end (descending entity order), the same items
+            const int ci = p.tile_rev ? cnt - 1 - (c0 + NWV * lane) : c0 + NWV * lane;
             if (pl) {  // (checked entity id, code): no dependent id load
-                const int2 e = plist[plo + c0 + NWV * lane];
+                const int2 e = plist[plo + ci];
                 code = e.y;
                 my_id = e.x;
             } else {
-                code = list[c0 + NWV * lane];
+                code = list[ci];
                 const int r = code >> 16, n = code & 0xFFFF;
                 const int64_t b = brow[r];
                 my_id = n < p.N ? p.c_idx[b * p.c_stride + n] : p.pos_base[b * 3 + 2];
@@ -1870,10 +1874,12 @@ __device__ __forceinline__ void group_jac_ih(const vecf<V>& ca, const vecf<V>& c
 }
 
 // Softmax / sigmoid weights of the fused query pass on the hardware exp / log / rcp (v_exp_f32, v_log_f32,
-// v_rcp_f32). They weight gradient terms only (the forward's outputs are row_reduce's, in full precision).
+// v_rcp_f32). They weight gradient terms only (the forward's outputs are row_reduce's, in full precision). The
+// log-sigmoid is the row reductions' (rr_log1p's series below 1/128): with log(1 + e) a well-separated row's
+// f = logsigmoid(-s) ~ -e^s flushed to 0 under e^s < 2^-24, dropping the T f half of its weight wa.
 __device__ __forceinline__ float fexp(float x) { return __expf(x); }
 __device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-__device__ __forceinline__ float flog_sigmoid(float x) { return fminf(x, 0.f) - __logf(1.f + __expf(-fabsf(x))); }
+__device__ __forceinline__ float flog_sigmoid(float x) { return rr_log_sigmoid(x); }
 
 // (xr, xi) / |(xr, xi)| and 0 at (and, fast form, within FLT_MIN of) the origin: the derivative of RotatE's
 // modulus, in every gradient path. One hardware reciprocal square root for both components

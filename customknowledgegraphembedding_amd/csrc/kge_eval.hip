@@ -749,6 +749,138 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The plane GEMM with B's fragments loaded straight into registers (round 6). gemm_nt_x3p_kernel stages both
+// operands through LDS in 16-k chunks with one barrier per chunk, and each B fragment is read from LDS by the four
+// waves of its column half (MFMA busy 0.72). Here each of the 8 waves of a 256 x 256 tile owns 32
+// columns and all 256 rows: its B fragments (one 32-column tile) are read by no other wave, so they are loaded
+// once per block straight from the chunk-major planes (1 KB contiguous per wave-instruction, one stage ahead) and
+// never touch LDS; A (8 row tiles, shared by every wave) is staged, 32 k per stage (48 KB, two stages), so there
+// is one barrier per 32 k. Per accumulator the products, their order (chunk by chunk; kX3A / kX3B within a chunk)
+// and C are bitwise gemm_nt_x3p_kernel's.
+// ---------------------------------------------------------------------------------------------
+constexpr int XD_CH = 2;                        // 16-k chunks per stage
+constexpr int XD_STAGE = XD_CH * 3 * XS_PLANE;  // A only: 2 chunks x 3 planes x 256 rows x 32 B = 48 KB
+
+struct XdARegs {
+    int4 a[XD_CH * 3];
+};
+struct XdBRegs {
+    bf16x8 b[XD_CH][3];
+};
+
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2))) void gemm_nt_x3d_kernel(
+    const __bf16* __restrict__ Ap, int64_t a_plane, const __bf16* __restrict__ Bp, int64_t b_plane, int kp,
+    float* __restrict__ C, int M, int N, int64_t ldc) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char gd_smem[];  // 2 stages of A
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int half = lane >> 5, col = lane & 31;
+    const int ntn = (N + XS_T - 1) / XS_T, ntm = (M + XS_T - 1) / XS_T;
+    const int nblk = ntn * ntm;
+    int bid = blockIdx.x;
+    {  // XCD-aware bijective remap (gemm_nt_x3s_kernel's): each XCD walks a contiguous run of B tiles
+        const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    }
+    const int tn = bid / ntm, tm = bid % ntm;
+    const int m0 = tm * XS_T, n0 = tn * XS_T;
+    const rsrc_t ra = make_rsrc(Ap, (uint32_t)(3 * a_plane * 2));
+    const rsrc_t rb = make_rsrc(Bp, (uint32_t)(3 * b_plane * 2));
+    const int T = kp / 16;            // 16-k chunks
+    const int S = (T + XD_CH - 1) / XD_CH;  // stages
+    const uint32_t pa = (uint32_t)(a_plane * 2), pb = (uint32_t)(b_plane * 2);
+    const uint32_t sa = (uint32_t)(a_plane / kp * 32), sb = (uint32_t)(b_plane / kp * 32);  // one chunk slab
+    // A staging: thread t takes row t >> 1, k half t & 1 of every (chunk, plane) piece of the stage
+    const int srow = t >> 1, sh = t & 1;
+    const uint32_t oa0 = m0 + srow < M ? (uint32_t)(((int64_t)(m0 + srow) * 16 + 8 * sh) * 2) : XS_OOB;
+    const int so = xs_off(srow, sh);
+    // B fragment of this lane: column n0 + 32 wave + col, k half `half` of each chunk
+    const int bn = n0 + wave * 32 + col;
+    const uint32_t ob0 = bn < N ? (uint32_t)(((int64_t)bn * 16 + 8 * half) * 2) : XS_OOB;
+    auto gload_a = [&](XdARegs& R, int s) {  // a chunk past K reads zeros (and is never multiplied)
+#pragma unroll
+        for (int c = 0; c < XD_CH; ++c) {
+            const int g = s * XD_CH + c;
+            const bool in = oa0 != XS_OOB && g < T;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(ra, in ? oa0 + p * pa + g * sa : XS_OOB, 0, 0);
+                R.a[c * 3 + p] = make_int4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    };
+    auto sstore_a = [&](const XdARegs& R, int stage) {
+        unsigned char* As = gd_smem + stage * XD_STAGE;
+#pragma unroll
+        for (int i = 0; i < XD_CH * 3; ++i) *reinterpret_cast<int4*>(As + i * XS_PLANE + so) = R.a[i];
+    };
+    auto gload_b = [&](XdBRegs& R, int s) {
+#pragma unroll
+        for (int c = 0; c < XD_CH; ++c) {
+            const int g = s * XD_CH + c;
+            const bool in = ob0 != XS_OOB && g < T;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, in ? ob0 + p * pb + g * sb : XS_OOB, 0, 0);
+                R.b[c][p] = __builtin_bit_cast(bf16x8, v);
+            }
+        }
+    };
+    f32x16 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r2 = 0; r2 < 16; ++r2) acc[i][r2] = 0.f;
+    auto compute = [&](int stage, const XdBRegs& Bf, int s) {
+        const unsigned char* As = gd_smem + stage * XD_STAGE;
+#pragma unroll
+        for (int c = 0; c < XD_CH; ++c) {
+            if (s * XD_CH + c >= T) break;  // block-uniform: the last stage of an odd chunk count
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int o = xs_off(i * 32 + col, half);
+                bf16x8 a[3];
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const bf16x8*>(As + (c * 3 + pl) * XS_PLANE + o);
+#pragma unroll
+                for (int q = 0; q < 6; ++q)
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kX3A[q]], Bf.b[c][kX3B[q]], acc[i], 0, 0, 0);
+            }
+        }
+    };
+    // one stage: B of the next stage requested first (its latency under this stage's MFMAs), A of this stage
+    // multiplied from LDS, A of the next stage (in registers since the stage before) stored into the other LDS
+    // stage, A of the stage after it requested
+    XdARegs RA;
+    XdBRegs B0, B1;
+    gload_a(RA, 0);
+    gload_b(B0, 0);
+    sstore_a(RA, 0);
+    gload_a(RA, 1);
+    __syncthreads();
+    auto step = [&](int s, const XdBRegs& Bc, XdBRegs& Bn) {
+        gload_b(Bn, s + 1);
+        compute(s & 1, Bc, s);
+        sstore_a(RA, (s + 1) & 1);
+        gload_a(RA, s + 2);
+        __syncthreads();
+    };
+    int s = 0;
+    for (; s + 1 < S; s += 2) {
+        step(s, B0, B1);
+        step(s + 1, B1, B0);
+    }
+    if (s < S) step(s, B0, B1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int gm = m0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            if (gm < M && bn < N) C[(int64_t)gm * ldc + bn] = acc[i][r];
+        }
+    }
+}
+
 }  // namespace
 
 int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
@@ -782,12 +914,21 @@ int launch_split3_planes(const float* X, int64_t rows, int64_t cols, int64_t ld,
 }
 
 int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, float* C, int64_t ldc,
-                       int M, int N, hipStream_t st) {
+                       int M, int N, hipStream_t st, int form) {
+    const int kp = (int)((K + 15) / 16 * 16);
+    const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
+    if (form == 2) {  // B straight into registers, A staged 32 k per barrier (gemm_nt_x3d_kernel)
+        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3d_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XD_STAGE) == hipSuccess;
+        (void)attr;
+        hipLaunchKernelGGL(gemm_nt_x3d_kernel, dim3((unsigned)tiles), dim3(512), 2 * XD_STAGE, st,
+                           static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp,
+                           C, M, N, ldc);
+        return 0;
+    }
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
     (void)attr;
-    const int kp = (int)((K + 15) / 16 * 16);
-    const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
     hipLaunchKernelGGL(gemm_nt_x3p_kernel, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st,
                        static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp, C, M,
                        N, ldc);

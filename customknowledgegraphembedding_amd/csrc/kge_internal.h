@@ -121,6 +121,7 @@ struct ScoreParams {
     int tile_sort;        // step_fwd_tile_kernel: 0, or the power of two >= B of the (relation, row) sort
     int tile_waves;       // step_fwd_tile_kernel: waves per block (8 or 16)
     int tile_dry;         // step_fwd_tile_kernel: setup only, no scoring (A/B knob KGE_TILE_DRY)
+    int tile_rev;         // step_fwd_tile_kernel: sweep each block's sorted list in descending entity order
     const int* tile_plan; // step_fwd_tile_kernel: this batch's plan (kge_step_forward_planned), or null
     int tile_blocks;      // step_fwd_tile_kernel: scoring blocks; blocks past them make the next batch's plan
     PlanArgs tile_next;   // ... that plan (tile_next.plan null: none)
@@ -221,8 +222,10 @@ int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N,
                          int64_t ldc, hipStream_t st, int form = 0);
 int launch_split3_planes(const float* X, int64_t rows, int64_t cols, int64_t ld, void* planes, int64_t plane_rows,
                          hipStream_t st);
+// form 1: both operands staged through LDS per 16-k chunk (gemm_nt_x3p_kernel); 2: B straight into registers, A
+// staged per 32 k (gemm_nt_x3d_kernel). Bitwise the same C.
 int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, float* C, int64_t ldc,
-                       int M, int N, hipStream_t st);
+                       int M, int N, hipStream_t st, int form);
 int launch_rank(const float* S, int64_t M, int64_t N, int64_t ld, const int64_t* truth, const int64_t* fptr,
                 const int64_t* fids, int64_t* ranks, hipStream_t st);
 

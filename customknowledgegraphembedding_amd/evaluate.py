@@ -60,13 +60,23 @@ def split_planes(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tens
     return out
 
 
+PLANES_MAX_BYTES = (1 << 32) - 16  # the plane GEMM's 32-bit buffer offsets (kge_split_bf16x3 refuses past it)
+
+
 def entity_planes(model) -> torch.Tensor | None:
     """The entity table's bf16 planes for one evaluation pass (DistMult / ComplEx), made once and passed to
     every score_all call of the pass: the table does not change while it is evaluated. None for the other
-    score functions."""
+    score functions, and None where the planes do not fit (PLANES_MAX_BYTES, or no device memory for their
+    1.5x the table): score_all then splits the operands at staging (kge_gemm_nt_bf16x3), at the same accuracy."""
     if model.model_name not in MFMA_FNS:
         return None
-    return split_planes(model.entity_embedding.detach())
+    ent = model.entity_embedding.detach()
+    if int(_lib.load().kge_split_bf16x3_bytes(ent.shape[0], ent.shape[1])) >= PLANES_MAX_BYTES:
+        return None
+    try:
+        return split_planes(ent)
+    except torch.OutOfMemoryError:
+        return None
 
 
 _Q_PLANES = {}

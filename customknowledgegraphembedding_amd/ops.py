@@ -206,6 +206,7 @@ class StepPlanner:
         self._planned = False
         self._held = None      # the tensors the waiting plan was made from (kept alive until its step)
         self._pshape, self._nshape = (B, 3), (B, N)
+        self._out_ok = None
 
     @staticmethod
     def plan_size(fn, ent, rel, rel_off, D, B, N):
@@ -227,6 +228,10 @@ class StepPlanner:
         if pos.stride() != (3, 1) or neg.stride(1) != 1:
             raise ValueError("pos must be contiguous and neg row-contiguous")
 
+    def set_sweep(self, alternate):
+        """1: the tile sweep's direction alternates step by step (kge_step_planner_set_sweep); 0: ascending."""
+        check(self._lib.kge_step_planner_set_sweep(self._h, int(alternate)), "kge_step_planner_set_sweep")
+
     def set_modulus(self, modulus):
         check(self._lib.kge_step_planner_set_modulus(self._h, float(modulus)), "kge_step_planner_set_modulus")
 
@@ -245,12 +250,28 @@ class StepPlanner:
                 torch.empty((self.B, self.N), dtype=torch.float32, device=dev),
                 torch.empty((self.B,), dtype=torch.float32, device=dev))
 
+    def _check_outputs(self, out):
+        """the planner writes neg_scores with row stride N and the three row outputs densely, fp32, on
+        the tables' device; anything else would be written silently wrong."""
+        if not isinstance(out, (tuple, list)) or len(out) != 4:
+            raise ValueError("StepPlanner.step: out must be (out_neg, out_pos, neg_scores, pos_scores)")
+        shapes = ((self.B,), (self.B,), (self.B, self.N), (self.B,))
+        strides = ((1,), (1,), (self.N, 1), (1,))
+        for t, shp, std, nm in zip(out, shapes, strides, ("out_neg", "out_pos", "neg_scores", "pos_scores")):
+            if not isinstance(t, torch.Tensor) or t.dtype != torch.float32 or t.device != self.ent.device:
+                raise TypeError(f"StepPlanner.step: {nm} must be a float32 tensor on {self.ent.device}")
+            if tuple(t.shape) != shp or (t.numel() > 1 and tuple(t.stride()) != std):
+                raise ValueError(f"StepPlanner.step: {nm} must have shape {shp} and strides {std}")
+
     def step(self, nxt=None, out=None):
         """Both model calls on the planned batch -> (out_neg [B], out_pos [B], neg_scores [B, N],
         pos_scores [B]); with nxt = (pos, neg, mode) the same launch plans that batch for the next step.
         `out`: outputs to write (from outputs(); neg_scores contiguous), else fresh tensors."""
         if not self._planned:
             raise RuntimeError("StepPlanner.step: no batch planned (call plan() first, or pass nxt to step)")
+        if out is not None and out is not self._out_ok:
+            self._check_outputs(out)
+            self._out_ok = out  # a caller reusing one set of outputs pays the check once
         out_neg, out_pos, neg_scores, pos_scores = out if out is not None else self.outputs()
         if nxt is None:
             rc = self._step_fn(self._h, None, None, 0, 0, neg_scores.data_ptr(), out_neg.data_ptr(),

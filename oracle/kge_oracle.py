@@ -344,6 +344,55 @@ def eval_ranks(name, ent, rel, pos, mode, all_true, gamma, embedding_range=None,
     return torch.tensor(ranks, dtype=torch.int64)
 
 
+def eval_query_dense(name, ent, rel, pos, mode):
+    """The query side Q [B, K] of DistMult / ComplEx all-entity scoring, so that score(e) = Q . ent[e] (the
+    candidate enters both formulas linearly: distmult / complex_ above with the candidate's factors pulled out;
+    upstream DistMult / ComplEx head-batch and tail-batch)."""
+    h, r, t = ent[pos[:, 0]], rel[pos[:, 1]], ent[pos[:, 2]]
+    if name == "DistMult":
+        return r * t if mode == "head-batch" else h * r
+    if name != "ComplEx":
+        raise ValueError(name)
+    re_h, im_h = torch.chunk(h, 2, dim=1)
+    re_r, im_r = torch.chunk(r, 2, dim=1)
+    re_t, im_t = torch.chunk(t, 2, dim=1)
+    if mode == "head-batch":
+        return torch.cat([re_r * re_t + im_r * im_t, re_r * im_t - im_r * re_t], dim=1)
+    return torch.cat([re_h * re_r - im_h * im_r, re_h * im_r + im_h * re_r], dim=1)
+
+
+def eval_ranks_dense(name, ent, rel, pos, mode, all_true, rtol=1e-6):
+    """eval_ranks (upstream test_step's filtered rank) for DistMult / ComplEx over every entity at once:
+    S = Q . ent^T, rank = 1 + #(unfiltered e != truth with S[e] > S[truth]) (a filtered candidate carries the
+    positive's score - 1, below it). Also returns the bounds [lo, hi] of the rank under a score perturbation of
+    rtol * sum_k |Q_k ent[e]_k| per candidate (the accuracy of an fp32 evaluation): lo counts the candidates
+    above the truth by more than both bounds, hi those not below it by more. Returns (ranks, lo, hi), int64 [B]."""
+    E = ent.shape[0]
+    col = 0 if mode == "head-batch" else 2
+    Q = eval_query_dense(name, ent, rel, pos, mode)
+    S = Q @ ent.T
+    T = rtol * (Q.abs() @ ent.abs().T)
+    others = {}  # (r, t) -> true heads, or (h, r) -> true tails
+    for h, r, t in map(tuple, all_true):
+        key, e = ((r, t), h) if mode == "head-batch" else ((h, r), t)
+        others.setdefault(key, set()).add(e)
+    ranks, lo, hi = [], [], []
+    for i, (h, r, t) in enumerate(pos.tolist()):
+        truth = (h, r, t)[col]
+        keep = torch.ones(E, dtype=torch.bool)
+        keep[truth] = False
+        filt = others.get((r, t) if mode == "head-batch" else (h, r), set())
+        if filt:
+            keep[torch.tensor(sorted(filt), dtype=torch.int64)] = False
+        d = S[i] - S[i, truth]
+        tol = T[i] + T[i, truth]
+        ranks.append(1 + int(((d > 0) & keep).sum()))
+        lo.append(1 + int(((d > tol) & keep).sum()))
+        hi.append(1 + int(((d > -tol) & keep).sum()))
+    return (torch.tensor(ranks, dtype=torch.int64), torch.tensor(lo, dtype=torch.int64),
+            torch.tensor(hi, dtype=torch.int64))
+
+
 # ------------------------------------------------------------------------------------------------
 # negative sampler: upstream TrainDataset.__getitem__ with numpy itself (the reference's own RNG and
 # set-membership code, so this part of the oracle is pinned by numpy, not restated)

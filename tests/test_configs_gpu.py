@@ -198,6 +198,38 @@ def test_c5_fb15k_filtered_ranks_full_entity_set():
         assert torch.equal(got, want), (mode, got, want)
 
 
+@pytest.mark.parametrize("name", ["DistMult", "ComplEx"])
+def test_c5_fb15k_filtered_ranks_512_queries(name):
+    """C5 at the bench's query scale: 512 valid.txt queries per mode through test_step's own path (entity planes
+    made once, query planes, the bf16x3 plane GEMM, kge_rank_filtered) against O.eval_ranks_dense (S = Q . E^T
+    in fp64; pinned to the per-query eval_ranks in test_oracle.py). A rank must equal the oracle's exactly
+    wherever no candidate lies within the fp32 accuracy bound (1e-6 sum|q e|) of the truth's score, and lie in
+    the oracle's [lo, hi] otherwise; at least 97 % of the queries must be decided exactly."""
+    E, R, d = 14951, 1345, 1000
+    de = name == "ComplEx"
+    m = kge.KGEModel(name, E, R, d, 24.0, double_entity_embedding=de, double_relation_embedding=de, device=DEV,
+                     seed=0)
+    true = _triples("fb15k")
+    q = true[np.random.RandomState(7).choice(len(true), 512, replace=False)]
+    ent = m.entity_embedding.detach().cpu().double()
+    rel = m.relation_embedding.detach().cpu().double()
+    planes = evaluate.entity_planes(m)
+    assert planes is not None
+    for mode in ("head-batch", "tail-batch"):
+        ptr, ids = evaluate.build_filter(q, mode, true)
+        pos = torch.from_numpy(q).to(DEV)
+        S = evaluate.score_all(m, pos, mode, planes=planes)
+        col = 0 if mode == "head-batch" else 2
+        got = evaluate.rank_filtered(S, pos[:, col].contiguous(), torch.from_numpy(ptr).to(DEV),
+                                     torch.from_numpy(ids).to(DEV)).cpu()
+        want, lo, hi = O.eval_ranks_dense(name, ent, rel, torch.from_numpy(q), mode, true)
+        decided = lo == hi
+        assert bool(((lo <= got) & (got <= hi)).all()), (name, mode)
+        assert torch.equal(got[decided], want[decided]), (name, mode)
+        assert float(decided.double().mean()) >= 0.97, (name, mode, int(decided.sum()))
+        assert int(want.max()) > 100  # the ranks span the table, not only the top
+
+
 # ------------------------------------------------------------------------------------------------
 # upstream loss flags (model.py:4-44; upstream KGEModel.train_step) vs the oracle's fp64 autograd
 # ------------------------------------------------------------------------------------------------

@@ -127,6 +127,29 @@ def test_test_step_metrics():
         assert met[k] == pytest.approx(want[k], rel=1e-12)
 
 
+def test_test_step_without_entity_planes(monkeypatch):
+    """a table whose bf16 planes would pass the plane GEMM's 4 GB limit (forced here by lowering
+    evaluate.PLANES_MAX_BYTES) gets no planes, and test_step runs on the staging-split GEMM with the same metrics;
+    a device allocation failure takes the same path."""
+    E, R, d = 150, 4, 8
+    m = kge.KGEModel("DistMult", E, R, d, 9.0, device=DEV, seed=1)
+    g = np.random.RandomState(0)
+    true = np.stack([g.randint(E, size=300), g.randint(R, size=300), g.randint(E, size=300)], 1)
+    assert evaluate.entity_planes(m) is not None
+    want = evaluate.test_step(m, true[:40], true, batch_size=16)
+    monkeypatch.setattr(evaluate, "PLANES_MAX_BYTES", 16)
+    assert evaluate.entity_planes(m) is None
+    assert evaluate.test_step(m, true[:40], true, batch_size=16) == want
+    monkeypatch.setattr(evaluate, "PLANES_MAX_BYTES", (1 << 32) - 16)
+
+    def oom(*a, **k):
+        raise torch.OutOfMemoryError("forced")
+
+    monkeypatch.setattr(evaluate, "split_planes", oom)
+    assert evaluate.entity_planes(m) is None
+    assert evaluate.test_step(m, true[:40], true, batch_size=16) == want
+
+
 def test_countries_auc_pr_matches_oracle():
     """Upstream test_step with args.countries on the reference's countries_S1 test triples and regions:
     single-mode scores on the GPU, auc_pr vs sklearn on the fp64 oracle's scores."""
@@ -255,3 +278,28 @@ def test_eval_query_planes_is_bitwise_query_then_split(fn, D, B, mode):
     assert lib.kge_gemm_nt_bf16x3_planes(got.data_ptr(), B + 5, ep.data_ptr(), E, K, S2.data_ptr(), E, B, E, st) == 0
     torch.cuda.synchronize()
     assert torch.equal(S1, S2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 4), (37, 300, 64), (257, 513, 1000), (300, 131, 12), (64, 14951, 1000),
+                                   (129, 77, 36), (512, 2048, 2000), (300, 700, 48)])
+def test_plane_gemm_b_direct_is_bitwise_the_staged_form(M, N, K):
+    """gemm_nt_x3d_kernel (B's fragments straight into registers, A staged 32 k per barrier: kge_forms.gemm_form 2)
+    against gemm_nt_x3p_kernel (both operands staged per 16-k chunk: form 1) on the same planes: C bitwise equal,
+    with partial tiles in M and N, odd and even 16-k chunk counts (K 1000: 63 chunks; 2000: 125; 48: 3) and a
+    padded leading dimension; nothing written past N."""
+    g = torch.Generator().manual_seed(M + 5 * N + K)
+    A = (torch.randn(M, K, generator=g) * torch.logspace(-2, 2, K)).to(DEV)
+    Bm = torch.randn(N, K, generator=g).to(DEV)
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    ap, bp = evaluate.split_planes(A), evaluate.split_planes(Bm)
+    out = []
+    for form in (1, 2):
+        C = torch.full((M, N + 3), -7.0, device=DEV)
+        f = _lib.forms(gemm_form=form)
+        assert lib.kge_gemm_nt_bf16x3_planes_ex(ap.data_ptr(), M, bp.data_ptr(), N, K, C.data_ptr(), N + 3, M, N,
+                                                ctypes.addressof(f), st) == 0
+        torch.cuda.synchronize()
+        out.append(C.cpu())
+    assert torch.equal(out[0], out[1])
+    assert bool((out[1][:, N:] == -7.0).all())

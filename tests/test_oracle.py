@@ -119,3 +119,22 @@ def test_oracle_reproduces_golden_train(path):
         np.testing.assert_allclose(loss.detach().numpy(), z[f"loss_mode{mode}"], rtol=1e-12)
         np.testing.assert_allclose(e.grad.numpy(), z[f"d_ent_mode{mode}"], rtol=1e-10, atol=1e-14)
         np.testing.assert_allclose(r.grad.numpy(), z[f"d_rel_mode{mode}"], rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.parametrize("name", ["DistMult", "ComplEx"])
+@pytest.mark.parametrize("mode", ["head-batch", "tail-batch"])
+def test_dense_ranks_equal_loop_ranks(name, mode):
+    """eval_ranks_dense (S = Q . ent^T at once, the C5 GPU test's checker) gives the ranks of eval_ranks (the
+    per-query restatement of upstream test_step), and those ranks lie inside its [lo, hi] bounds."""
+    E, R, d = 97, 5, 12
+    de = name == "ComplEx"
+    ent, rel, rng = O.make_tables(E, R, 2 * d if de else d, 2 * d if de else d, 24.0, d, seed=3)
+    ent, rel = ent.double(), rel.double()
+    g = np.random.RandomState(1)
+    true = np.stack([g.randint(E, size=400), g.randint(R, size=400), g.randint(E, size=400)], 1)
+    q = torch.from_numpy(true[:25])
+    want = O.eval_ranks(name, ent, rel, q, mode, true, 24.0, rng)
+    got, lo, hi = O.eval_ranks_dense(name, ent, rel, q, mode, true)
+    assert torch.equal(got, want)
+    assert bool((lo <= got).all() and (got <= hi).all())
+    assert int(want.max()) > 5  # the filter and the ranks are not trivial

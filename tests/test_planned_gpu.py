@@ -184,3 +184,58 @@ def test_planned_wrong_plan_makes_outputs_nan_and_bad_calls_fail():
     assert not ops.StepPlanner.available(fn, ent, rel, 0, d, B, 70000)
     with pytest.raises(RuntimeError):
         _planner(m, B, N).step()
+
+
+def test_planned_plan_of_the_other_row_order_makes_outputs_nan():
+    """a plan made for a score function without the relation sort (DistMult) has InterHT's batch shape,
+    but not its row order: the InterHT planned step refuses it by the header's sort flag (NaN outputs)."""
+    E, R, d, B, N = 2000, 5, 64, 24, 160
+    lib = kge.load()
+    mi = _model("InterHT", E, R, d, seed=3)
+    (pos, neg), = _batches(E, R, B, N, 1, seed=5)
+    ent, rel = mi.entity_embedding.detach(), mi.relation_embedding.detach()
+    st = torch.cuda.current_stream().cuda_stream
+    nb_i = lib.kge_step_plan_size(FN_IDS["InterHT"], E, ent.stride(0), R, rel.stride(0), mi._rel_off, B, N, d)
+    nb_d = lib.kge_step_plan_size(FN_IDS["DistMult"], E, d, R, d, 0, B, N, d)
+    assert nb_i > 0 and nb_d > 0
+    plan = torch.empty(max(nb_i, nb_d), dtype=torch.uint8, device=DEV)
+    own = torch.empty(max(nb_i, nb_d), dtype=torch.uint8, device=DEV)
+    assert lib.kge_step_plan(FN_IDS["InterHT"], 1, E, ent.stride(0), R, rel.stride(0), mi._rel_off, pos.data_ptr(),
+                             neg.data_ptr(), neg.stride(0), B, N, d, own.data_ptr(), st) == 0
+    assert lib.kge_step_plan(FN_IDS["DistMult"], 1, E, d, R, d, 0, pos.data_ptr(), neg.data_ptr(), neg.stride(0), B,
+                             N, d, plan.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    h_own, h_other = own[:28].view(torch.int32).cpu(), plan[:28].view(torch.int32).cpu()
+    assert torch.equal(h_own[:6], h_other[:6]) and int(h_own[6]) != int(h_other[6])  # only the sort flag differs
+    ns = torch.zeros(B, N, device=DEV)
+    on, op, ps = (torch.zeros(B, device=DEV) for _ in range(3))
+    assert lib.kge_step_forward_planned(FN_IDS["InterHT"], 1, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(), R,
+                                        rel.stride(0), mi._rel_off, B, N, d, mi._gamma_f, mi._range_f, 0.0, 1.0, 1,
+                                        plan.data_ptr(), pos.data_ptr(), neg.data_ptr(), neg.stride(0), 1, None,
+                                        ns.data_ptr(), N, on.data_ptr(), ps.data_ptr(), op.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(ns).all()) and bool(torch.isnan(on).all()) and bool(torch.isnan(op).all())
+
+
+def test_planner_step_checks_caller_outputs():
+    """StepPlanner.step(out=...) refuses outputs of the wrong shape, strides, dtype or device."""
+    E, R, d, B, N = 2000, 5, 64, 24, 160
+    m = _model("DistMult", E, R, d, seed=2)
+    (pos, neg), = _batches(E, R, B, N, 1, seed=4)
+    sp = _planner(m, B, N)
+    sp.plan(pos, neg, 0)
+    good = sp.outputs()
+    bad = [
+        (good[0], good[1], torch.empty(N, B, device=DEV).t(), good[3]),          # transposed strides
+        (good[0], good[1], torch.empty(B, N + 1, device=DEV)[:, :N], good[3]),   # padded rows
+        (good[0].double(), good[1], good[2], good[3]),                           # dtype
+        (good[0], good[1], good[2], torch.empty(B + 1, device=DEV)),             # shape
+        (good[0].cpu(), good[1], good[2], good[3]),                              # device
+        good[:3],
+    ]
+    for out in bad:
+        with pytest.raises((ValueError, TypeError)):
+            sp.step(out=out)
+    got = sp.step(out=good)
+    torch.cuda.synchronize()
+    assert _same(got, _unplanned(m, 0, pos, neg))

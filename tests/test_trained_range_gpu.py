@@ -157,3 +157,41 @@ def test_trained_range_fused_train_step(name):
     for p_got, p0, gr in ((m.entity_embedding, ent, e.grad), (m.relation_embedding, rel, r.grad)):
         p1, _, _ = O.keras_adam_step(p0, gr, torch.zeros_like(p0), torch.zeros_like(p0), 1, lr)
         assert (p_got.detach().cpu().double() - p1).abs().max().item() <= 5e-2 * lr
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fused_train_step_well_separated_rows(mode):
+    """the fused train forward's gradient weights on rows whose every score is far below 0 (e^s < 2^-24:
+    logsigmoid(-s) ~ -e^s, which log(1 + e) flushed to 0, dropping the T f term of the weight and the T R_b term of
+    the row's gradient). Keras Adam's epsilon is set to the median |gradient| of the oracle's step, so the update
+    lr g / (|g| + eps) follows the gradient's magnitude (not only its sign) where |g| ~ eps: a factor-2 error there
+    moves a parameter by ~0.15 lr. One step of both tables within 5e-2 lr of the oracle's."""
+    name, E, R, d, B, N, lr = "TransE", 300, 5, 64, 24, 160, 1e-3
+    m = kge.TFKGEModel(name, E, R, d, 0.0, device=DEV, seed=7)
+    g = np.random.RandomState(11)
+    pos = torch.from_numpy(np.stack([g.randint(E, size=B), g.randint(R, size=B), g.randint(E, size=B)], 1))
+    neg = torch.from_numpy(g.randint(E, size=(B, N)))
+    w = torch.from_numpy(g.uniform(0.2, 1.0, size=(B, 1))).float()
+    ent0 = m.entity_embedding.detach().cpu().double()
+    rel0 = m.relation_embedding.detach().cpu().double()
+    s0 = O.score(name, ent0, rel0, pos, neg, mode, 0.0)
+    k = 17.5 / float(-s0.max())  # every score at or below -17.5: e^s < 2.6e-8 < 2^-24
+    with torch.no_grad():
+        m.entity_embedding.mul_(k)
+        m.relation_embedding.mul_(k)
+    ent = m.entity_embedding.detach().cpu().double()
+    rel = m.relation_embedding.detach().cpu().double()
+    assert float(O.score(name, ent, rel, pos, neg, mode, 0.0).max()) < -17.0
+    e = ent.clone().requires_grad_(True)
+    r = rel.clone().requires_grad_(True)
+    ref = O.tf_train_loss(name, e, r, pos, neg, w.double(), torch.tensor([mode] * B), 0.0)
+    ref.backward()
+    ge = e.grad[e.grad != 0].abs()
+    eps = float(ge.median())
+    assert eps < 1e-9  # the candidate rows' gradients are of the e^s scale
+    opt = Adam(m.parameters(), lr=lr, eps=eps)
+    loss = float(m.train_step_fused(pos.to(DEV), neg.to(DEV), w.to(DEV), mode, opt))
+    assert abs(loss - ref.item()) <= TOL * max(1.0, abs(ref.item())), (loss, ref.item())
+    for p_got, p0, gr in ((m.entity_embedding, ent, e.grad), (m.relation_embedding, rel, r.grad)):
+        p1, _, _ = O.keras_adam_step(p0, gr, torch.zeros_like(p0), torch.zeros_like(p0), 1, lr, epsilon=eps)
+        assert (p_got.detach().cpu().double() - p1).abs().max().item() <= 5e-2 * lr

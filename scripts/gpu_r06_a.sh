@@ -16,6 +16,7 @@ run() {  # name limit cmd...
 }
 run new 600 python3 -u -m pytest -v --timeout 300 --timeout-method thread tests/test_train_c2_gpu.py tests/test_trained_range_gpu.py tests/test_planned_gpu.py tests/test_eval_gpu.py -k 'c2 or d1000 or separated or row_order or caller or without_entity or rotate or b_direct'
 run c5 600 python3 -u -m pytest -v --timeout 300 --timeout-method thread tests/test_configs_gpu.py -k c5
+run tsprobe_old 600 env KGE_HIP_LIB=$R/abtmp/libkge_pre_ts_rule.so python3 scripts/ts_many_rel_probe.py
 run tsprobe 600 python3 scripts/ts_many_rel_probe.py
 run sweep 600 python3 scripts/sweep_probe.py
 run gemm 600 python3 scripts/gemm_form_probe.py

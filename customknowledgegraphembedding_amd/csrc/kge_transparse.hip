@@ -2049,20 +2049,22 @@ int kge_transparse_score(int mode, const float* ent, int64_t nent, int64_t ent_l
                                    gamma, out, out_ld, stats, nullptr, nullptr, 0, stream);
 }
 
-// Both workspace forms pay per relation of the table, not per relation the batch uses: the head-batch planes
-// split every M_r on every call (nrel d^2 reads), and the grouped split form launches (nrel + 1) x row chunks x
-// column ranges x K ranges blocks that each scan the B rows for their relation. They are asked for only where the
-// batch has many rows per relation (WN18RR: 11 relations, 512 rows) and the planes stay small; otherwise 0 (the
-// staging split, the one-block grouped form: the same scores). scripts/ts_many_rel_probe.py,
+// The head-batch planes split every M_r of the table on every call (nrel d^2 reads and 6 B written per element),
+// whichever relations the batch uses: they are asked for only where the batch has many rows per relation (WN18RR:
+// 11 relations, 512 rows; 346-360 against 365-380 us per call) and the planes stay small; otherwise 0, the staging
+// split (the same scores; FB15k-237's 237 relations: 515-604 us with planes against 395-438 without, FB15k's 1 345:
+// 1 320 against 417). The grouped split form stays on for every relation count: its extra blocks are mostly empty
+// and cheap (1 345 relations: 444 us against 1 768 us for the one-block form). scripts/ts_many_rel_probe.py,
 // profiles/r06_ts_many_rel_ab.txt.
-constexpr int64_t kTsWsMinRowsPerRel = 16;
+constexpr int64_t kTsPlanesMinRowsPerRel = 16;
 constexpr int64_t kTsPlanesMaxBytes = (int64_t)256 << 20;
 
 size_t kge_transparse_score_workspace_size(int mode, int64_t nrel, int64_t B, int64_t d) {
     if (B <= 0 || d <= 0 || d > kXsMaxDim || nrel < 0) return 0;
-    if ((nrel + 1) * kTsWsMinRowsPerRel > B) return 0;
     // head-batch: M_r as bf16 planes for the 256-row kernel
-    if (mode == KGE_HEAD_BATCH) return mplanes_bytes(nrel, d) <= kTsPlanesMaxBytes ? (size_t)mplanes_bytes(nrel, d) : 0;
+    if (mode == KGE_HEAD_BATCH)
+        return ((nrel + 1) * kTsPlanesMinRowsPerRel <= B && mplanes_bytes(nrel, d) <= kTsPlanesMaxBytes)
+                   ? (size_t)mplanes_bytes(nrel, d) : 0;
     // the grouped rows (single / tail-batch): the partial projections [ksplit][B][xsplit 128] floats
     const int64_t xs = xg_xsplit(d), ks = xg_ksplit(d);
     return xs * ks > 1 ? (size_t)(ks * B * xs * kXgSplitCols) * sizeof(float) : 0;

@@ -361,17 +361,26 @@ def eval_query_dense(name, ent, rel, pos, mode):
     return torch.cat([re_h * re_r - im_h * im_r, re_h * im_r + im_h * re_r], dim=1)
 
 
-def eval_ranks_dense(name, ent, rel, pos, mode, all_true, rtol=1e-6):
+def eval_scores_dense(name, ent, rel, pos, mode):
+    """S [B, E] = Q . ent^T: every entity's score as the candidate (DistMult / ComplEx)."""
+    return eval_query_dense(name, ent, rel, pos, mode) @ ent.T
+
+
+def eval_ranks_dense(name, ent, rel, pos, mode, all_true, rtol=1e-6, atol=None):
     """eval_ranks (upstream test_step's filtered rank) for DistMult / ComplEx over every entity at once:
     S = Q . ent^T, rank = 1 + #(unfiltered e != truth with S[e] > S[truth]) (a filtered candidate carries the
     positive's score - 1, below it). Also returns the bounds [lo, hi] of the rank under a score perturbation of
-    rtol * sum_k |Q_k ent[e]_k| per candidate (the accuracy of an fp32 evaluation): lo counts the candidates
-    above the truth by more than both bounds, hi those not below it by more. Returns (ranks, lo, hi), int64 [B]."""
+    rtol * sum_k |Q_k ent[e]_k| per candidate (the accuracy bound of an fp32 evaluation), or of atol[i] per score of
+    query i when given: lo counts the candidates above the truth by more than both perturbations, hi those not below
+    it by more. Returns (ranks, lo, hi), int64 [B]."""
     E = ent.shape[0]
     col = 0 if mode == "head-batch" else 2
     Q = eval_query_dense(name, ent, rel, pos, mode)
     S = Q @ ent.T
-    T = rtol * (Q.abs() @ ent.abs().T)
+    if atol is None:
+        T = rtol * (Q.abs() @ ent.abs().T)
+    else:
+        T = torch.as_tensor(atol, dtype=S.dtype).reshape(-1, 1).expand_as(S)
     others = {}  # (r, t) -> true heads, or (h, r) -> true tails
     for h, r, t in map(tuple, all_true):
         key, e = ((r, t), h) if mode == "head-batch" else ((h, r), t)

@@ -169,12 +169,12 @@ def test_workspace_queries_are_host_arithmetic():
     assert lib.kge_transparse_step_workspace_size(R, B, d) == max(planes, xk)
     assert lib.kge_transparse_score_workspace_size(0, R, B, 2048) == 0    # past the planes form's d <= 1024
     assert lib.kge_transparse_score_workspace_size(3, R, B, 100) == 0     # one 128-column, one 128-k range
-    # many relations (FB15k-237, FB15k) or few rows per relation: no workspace (the staging split and the
-    # one-block grouped form), and no planes past 256 MB
+    # many relations (FB15k-237, FB15k) or few rows per relation: no head-batch planes (the staging
+    # split), and no planes past 256 MB; the grouped split's partial projections stay (faster at every count)
     for rr in (237, 1345):
-        for mode in (0, 1, 3):
-            assert lib.kge_transparse_score_workspace_size(mode, rr, B, d) == 0
-        assert lib.kge_transparse_step_workspace_size(rr, B, d) == 0
+        assert lib.kge_transparse_score_workspace_size(0, rr, B, d) == 0
+        assert lib.kge_transparse_score_workspace_size(1, rr, B, d) == xk
+        assert lib.kge_transparse_step_workspace_size(rr, B, d) == xk
     assert lib.kge_transparse_score_workspace_size(0, 32, 512, d) == 0      # (32 + 1) x 16 rows > 512
     assert lib.kge_transparse_score_workspace_size(0, 31, 512, d) > 0
     assert lib.kge_transparse_score_workspace_size(0, 60, 8192, 1024) == 0  # 60 x 6.3 MB of planes > 256 MB

@@ -814,19 +814,23 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
         col = 0 if mode == "head-batch" else 2
         pos = torch.from_numpy(q).to(device)
         batches.append((pos, mode, pos[:, col].contiguous(), torch.from_numpy(ptr).to(device),
-                        torch.from_numpy(ids).to(device)))
+                        torch.from_numpy(ids).to(device), int(ptr[-1])))
     S = torch.empty((Bq, E), dtype=torch.float32, device=device)
     K = m.entity_embedding.shape[1]
     ent = m.entity_embedding.detach()
     Q = torch.empty((Bq, K), dtype=torch.float32, device=device)
     lib = __import__("customknowledgegraphembedding_amd._lib", fromlist=["load"]).load()
-    split = os.environ.get("KGE_BENCH_EVAL_SPLIT", "planes")  # planes (default) | staging (the round-4 form)
+    # planes (default): ranks straight from the planes (kge_eval_rank_planes, no [Bq, E] score matrix);
+    # planes_s: the plane GEMM writing S, then kge_rank_filtered (round 5); staging: the round-4 form
+    split = os.environ.get("KGE_BENCH_EVAL_SPLIT", "planes")
     qp = torch.empty(int(lib.kge_split_bf16x3_bytes(Bq, K)), dtype=torch.uint8, device=device)
     ep = torch.empty(int(lib.kge_split_bf16x3_bytes(E, K)), dtype=torch.uint8, device=device)
+    rws = torch.empty(int(lib.kge_eval_rank_planes_workspace_size(Bq, max(b[5] for b in batches))) + 16,
+                      dtype=torch.uint8, device=device)
 
     def entity_pass():
         """The start of an evaluation pass: the entity table's bf16 planes (evaluate.entity_planes), once per pass."""
-        if split == "planes":
+        if split in ("planes", "planes_s"):
             lib.kge_split_bf16x3(ent.data_ptr(), E, K, ent.stride(0), ep.data_ptr(), E,
                                  torch.cuda.current_stream().cuda_stream)
 
@@ -834,11 +838,11 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
         """One query batch: Q = h*r or r*t written as bf16 planes (kge_eval_query_planes), S = Q . E^T
         (kge_gemm_nt_bf16x3_planes on the pass's entity planes, events around it; or kge_eval_query +
         kge_gemm_nt_bf16x3, the staging form), exact filtered ranks."""
-        pos, mode, truth, fptr, fids = b
+        pos, mode, truth, fptr, fids = b[:5]
         st = torch.cuda.current_stream().cuda_stream
         md = 0 if mode == "head-batch" else 1
         rel_ = m.relation_embedding
-        if split == "planes":
+        if split in ("planes", "planes_s"):
             lib.kge_eval_query_planes(FN_IDS[w["fn"]], md, ent.data_ptr(), E, ent.stride(0), rel_.data_ptr(), R,
                                       rel_.stride(0), pos.data_ptr(), Bq, m._D, qp.data_ptr(), Bq, st)
         else:
@@ -847,6 +851,13 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
         if ev is not None:
             ev[0].record()
         if split == "planes":
+            ranks = torch.empty(Bq, dtype=torch.int64, device=device)
+            lib.kge_eval_rank_planes(qp.data_ptr(), Bq, ep.data_ptr(), E, K, Bq, E, truth.data_ptr(), fptr.data_ptr(),
+                                     fids.data_ptr(), b[5], ranks.data_ptr(), rws.data_ptr(), rws.numel(), st)
+            if ev is not None:
+                ev[1].record()
+            return ranks
+        if split == "planes_s":
             lib.kge_gemm_nt_bf16x3_planes(qp.data_ptr(), Bq, ep.data_ptr(), E, K, S.data_ptr(), E, Bq, E, st)
         else:
             lib.kge_gemm_nt_bf16x3(Q.data_ptr(), K, ent.data_ptr(), ent.stride(0), S.data_ptr(), E, Bq, E, K, st)
@@ -896,11 +907,14 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                        "parallelism": f"replicas{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": mfma_flops / gemm_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                          "frac": mfma_flops / gemm_s / 1e12 / 2500.0, "traffic": None,
-                         "kernel": ("gemm_nt_x3p_kernel (256 x 256 tiles from the query planes, which "
-                                    "kge_eval_query_planes writes directly, and the entity bf16 planes, no "
-                                    "conversion in the loop, six "
-                                    "products per 16 k on v_mfma_f32_32x32x16_bf16; the entity planes made once per "
-                                    "evaluation pass, inside the timed region)" if split == "planes" else
+                         "kernel": ("kge_eval_rank_planes: pair_dot_x3_kernel (the truths' and filter entries' scores) "
+                                    "+ gemm_nt_x3p_kernel<true> (256 x 256 tiles from the query planes, which "
+                                    "kge_eval_query_planes writes directly, and the entity bf16 planes, six products per "
+                                    "16 k on v_mfma_f32_32x32x16_bf16, each row's count of scores above its truth in the "
+                                    "epilogue: no score matrix) + rank_finish_kernel; the entity planes made once per "
+                                    "evaluation pass, inside the timed region" if split == "planes" else
+                                    "gemm_nt_x3p_kernel (256 x 256 tiles from the query and entity bf16 planes, S "
+                                    "written, then kge_rank_filtered)" if split == "planes_s" else
                                     "gemm_nt_x3s_kernel (256 x 256 tiles, operands split once at staging into bf16 "
                                     "planes, six products per 16 k on v_mfma_f32_32x32x16_bf16)"),
                          "kernel_avg_us": gemm_s * 1e6,

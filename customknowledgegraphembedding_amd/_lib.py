@@ -154,6 +154,9 @@ SIGNATURES = {
     "kge_split_bf16x3_bytes": (_c_i64, [_c_i64, _c_i64]),
     "kge_split_bf16x3": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_i64, _c_p]),
     "kge_gemm_nt_bf16x3_planes": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p]),
+    "kge_eval_rank_planes_workspace_size": (_c_i64, [_c_i64, _c_i64]),
+    "kge_eval_rank_planes": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_i64, _c_p,
+                                    _c_p, ctypes.c_size_t, _c_p]),
     "kge_gemm_nt_bf16x3_planes_ex": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p,
                                             _c_p]),
     "kge_rank_filtered": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p]),

@@ -1252,6 +1252,32 @@ int kge_rank_filtered(const float* scores, int64_t M, int64_t N, int64_t ld, con
     return check_launch("kge_rank_filtered");
 }
 
+int64_t kge_eval_rank_planes_workspace_size(int64_t M, int64_t nfilter) {
+    if (M < 0 || nfilter < 0) return 0;
+    return eval_rank_ws_bytes(M, nfilter);
+}
+
+int kge_eval_rank_planes(const void* A_planes, int64_t a_rows, const void* B_planes, int64_t b_rows, int64_t K,
+                         int64_t M, int64_t N, const int64_t* truth, const int64_t* filter_ptr,
+                         const int64_t* filter_ids, int64_t nfilter, int64_t* ranks, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+    if (M < 0 || N <= 0 || K <= 0 || M > a_rows || N > b_rows || nfilter < 0) return fail(KGE_EINVAL, "bad shape");
+    if (M == 0) return ok();
+    if (!A_planes || !B_planes || !truth || !ranks || !workspace || (filter_ptr && !filter_ids) ||
+        (nfilter > 0 && !filter_ptr))
+        return fail(KGE_EINVAL, "null pointer");
+    if (M > INT32_MAX || N > INT32_MAX || !aligned(A_planes, 16) || !aligned(B_planes, 16) || !aligned(workspace, 16))
+        return fail(KGE_EINVAL, "kge_eval_rank_planes: int32 shapes and 16-B aligned planes / workspace");
+    if (kge_split_bf16x3_bytes(a_rows, K) >= ((int64_t)1 << 32) - 16 ||
+        kge_split_bf16x3_bytes(b_rows, K) >= ((int64_t)1 << 32) - 16)
+        return fail(KGE_ENOTSUP, "kge_eval_rank_planes: planes past 4 GB");
+    if ((int64_t)workspace_bytes < eval_rank_ws_bytes(M, nfilter))
+        return fail(KGE_EINVAL, "kge_eval_rank_planes: workspace too small");
+    launch_eval_rank_planes(A_planes, a_rows, B_planes, b_rows, K, (int)M, (int)N, truth, filter_ptr, filter_ids,
+                            nfilter, ranks, workspace, (hipStream_t)stream);
+    return check_launch("kge_eval_rank_planes");
+}
+
 int kge_score_dense(int fn, int mode, const float* head, int64_t head_ld, const float* rel, int64_t rel_ld,
                     int64_t rel_off, const float* tail, int64_t tail_ld, int64_t B, int64_t N, int64_t D, float gamma,
                     float emb_range, float modulus, float* scores, int64_t scores_ld, void* stream) {

@@ -624,11 +624,19 @@ struct XpGemmRegs {
     int4 a[3], b[3];
 };
 
+// CNT (kge_eval_rank_planes): no C; the epilogue counts, per query row, the scores above the row's truth score
+// ts[row] (columns < N) and adds the block's counts to gcnt[row] (integer atomics). The accumulators are the
+// CNT = false kernel's, bitwise.
+template <bool CNT>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2))) void gemm_nt_x3p_kernel(
     const __bf16* __restrict__ Ap, int64_t a_plane, const __bf16* __restrict__ Bp, int64_t b_plane, int kp,
-    float* __restrict__ C, int M, int N, int64_t ldc) {
+    float* __restrict__ C, int M, int N, int64_t ldc, const float* __restrict__ ts, int* __restrict__ gcnt) {
     extern __shared__ __attribute__((aligned(16))) unsigned char gp_smem[];  // 2 stages
+    __shared__ int rowcnt[CNT ? XS_T : 1];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if constexpr (CNT) {
+        if (t < XS_T) rowcnt[t] = 0;  // visible after the prologue's barrier
+    }
     const int half = lane >> 5, col = lane & 31;
     const int wr = wave >> 1, wc = wave & 1;
     const int ntn = (N + XS_T - 1) / XS_T, ntm = (M + XS_T - 1) / XS_T;
@@ -736,6 +744,28 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
         step(g + 1, R0);
     }
     if (g < T) step(g, R1);
+    if constexpr (CNT) {
+        // per query row: how many of this block's columns score above the row's truth (ties and NaN never
+        // count; the truth's own column scores exactly ts, so it does not count either)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int lr = wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const float tv = m0 + lr < M ? ts[m0 + lr] : INFINITY;
+                int c = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int gn = n0 + wc * 128 + j * 32 + col;
+                    const uint64_t bal = __ballot(gn < N && acc[i][j][r] > tv);
+                    c += __popcll(half ? (bal >> 32) : (bal & 0xFFFFFFFFull));
+                }
+                if (col == 0 && c) atomicAdd(&rowcnt[lr], c);
+            }
+        __syncthreads();
+        if (t < XS_T && rowcnt[t] && m0 + t < M) atomicAdd(&gcnt[m0 + t], rowcnt[t]);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -881,6 +911,113 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Filtered ranks without the score matrix (kge_eval_rank_planes, round 6). rank_kernel reads back the whole
+// [M, N] score matrix the GEMM wrote (4 096 x 14 951 floats = 245 MB written and read per C5 batch). Here:
+//   1. pair_dot_x3_kernel: the scores of the pairs a rank compares against, (q, truth[q]) and every filter entry
+//      (q, f), each as the diagonal of one 32 x 32 MFMA tile whose row p is pair p's query row and column p its
+//      entity row: the same planes, chunks and six products in the same order as the GEMM's element (q, e), so
+//      bitwise its value (tests/test_eval_gpu.py checks that against the materialised scores);
+//   2. gemm_nt_x3p_kernel<true>: the GEMM, counting per row the scores above the truth's;
+//   3. rank_finish_kernel: rank = 1 + count - #{filter entries f != truth scoring above the truth}: rank_kernel's
+//      rank exactly.
+// ---------------------------------------------------------------------------------------------
+constexpr int kPairDepth = 6;  // 16-k chunks of loads in flight per wave (the chunk chain is latency-bound)
+
+__global__ __launch_bounds__(kBlock) void pair_dot_x3_kernel(const __bf16* __restrict__ Ap, int64_t a_rows,
+                                                             const __bf16* __restrict__ Bp, int64_t b_rows, int kp,
+                                                             int64_t M, int64_t N, const int64_t* __restrict__ truth,
+                                                             const int64_t* __restrict__ fptr,
+                                                             const int64_t* __restrict__ fids, int64_t F,
+                                                             float* __restrict__ ts, float* __restrict__ fs,
+                                                             int* __restrict__ gcnt) {
+    const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) gcnt[i] = 0;
+    const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 32;
+    if (p0 >= M + F) return;  // wave-uniform
+    const int64_t p = p0 + col;
+    int64_t q = 0, e = -1;
+    if (p < M) {
+        q = p;
+        e = truth[p];
+    } else if (p < M + F) {
+        const int64_t j = p - M;
+        e = fids[j];
+        int64_t lo = 0, hi = M;  // the query whose filter range holds j: the last q with fptr[q] <= j
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (fptr[mid] <= j) lo = mid; else hi = mid;
+        }
+        q = lo;
+    }
+    const bool ev = e >= 0 && e < N;
+    const int64_t a_plane = a_rows * kp, b_plane = b_rows * kp;
+    const rsrc_t ra = make_rsrc(Ap, (uint32_t)(3 * a_plane * 2)), rb = make_rsrc(Bp, (uint32_t)(3 * b_plane * 2));
+    const uint32_t oa = (uint32_t)((q * 16 + 8 * half) * 2), ob = (uint32_t)(((ev ? e : 0) * 16 + 8 * half) * 2);
+    const uint32_t sa = (uint32_t)(a_rows * 32), sb = (uint32_t)(b_rows * 32);  // one chunk slab
+    const uint32_t pa = (uint32_t)(a_plane * 2), pb = (uint32_t)(b_plane * 2);
+    const int T = kp / 16;
+    bf16x8 av[kPairDepth][3], bv[kPairDepth][3];
+    auto load = [&](int slot, int g) {  // a chunk past K reads zeros (never multiplied)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+            av[slot][pl] = __builtin_bit_cast(
+                bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, g < T ? oa + pl * pa + g * sa : XS_OOB, 0, 0));
+            bv[slot][pl] = __builtin_bit_cast(
+                bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, g < T ? ob + pl * pb + g * sb : XS_OOB, 0, 0));
+        }
+    };
+    f32x16 acc;
+#pragma unroll
+    for (int r2 = 0; r2 < 16; ++r2) acc[r2] = 0.f;
+#pragma unroll
+    for (int s = 0; s < kPairDepth; ++s) load(s, s);
+    for (int g0 = 0; g0 < T; g0 += kPairDepth) {
+#pragma unroll
+        for (int s = 0; s < kPairDepth; ++s) {
+            if (g0 + s < T) {  // wave-uniform
+#pragma unroll
+                for (int q6 = 0; q6 < 6; ++q6)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[s][kX3A[q6]], bv[s][kX3B[q6]], acc, 0, 0, 0);
+            }
+            load(s, g0 + s + kPairDepth);
+        }
+    }
+    // the diagonal: pair c's score is row c, column c of the tile, held by the lane of column c in the half whose
+    // rows hold c (rows 8 (r >> 2) + 4 half + (r & 3))
+    if (half == ((col >> 2) & 1)) {
+        float v = 0.f;
+        const int rr = 4 * (col >> 3) + (col & 3);
+#pragma unroll
+        for (int r2 = 0; r2 < 16; ++r2)
+            if (r2 == rr) v = acc[r2];
+        if (p < M)
+            ts[p] = ev ? v : -INFINITY;  // rank_kernel's score of an out-of-range truth
+        else if (p < M + F)
+            fs[p - M] = v;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void rank_finish_kernel(int64_t M, int64_t N, const int64_t* __restrict__ truth,
+                                                             const int64_t* __restrict__ fptr,
+                                                             const int64_t* __restrict__ fids,
+                                                             const float* __restrict__ ts, const float* __restrict__ fs,
+                                                             const int* __restrict__ gcnt, int64_t* __restrict__ ranks) {
+    const int64_t q = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (q >= M) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t tr = truth[q];
+    const float st = ts[q];
+    int sub = 0;
+    if (fptr)
+        for (int64_t i = fptr[q] + lane; i < fptr[q + 1]; i += kWave) {
+            const int64_t f = fids[i];
+            if (f >= 0 && f < N && f != tr && fs[i] > st) ++sub;
+        }
+    for (int o = 32; o > 0; o >>= 1) sub += __shfl_xor(sub, o, kWave);
+    if (lane == 0) ranks[q] = 1 + (int64_t)gcnt[q] - sub;
+}
+
 }  // namespace
 
 int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N, int K, int64_t lda, int64_t ldb,
@@ -926,12 +1063,39 @@ int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b
                            C, M, N, ldc);
         return 0;
     }
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel),
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel<false>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
     (void)attr;
-    hipLaunchKernelGGL(gemm_nt_x3p_kernel, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st,
+    hipLaunchKernelGGL(gemm_nt_x3p_kernel<false>, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st,
                        static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp, C, M,
-                       N, ldc);
+                       N, ldc, nullptr, nullptr);
+    return 0;
+}
+
+int64_t eval_rank_ws_bytes(int64_t M, int64_t F) { return ((M * 8 + 15) / 16 * 16) + ((F * 4 + 15) / 16 * 16); }
+
+int launch_eval_rank_planes(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, int M, int N,
+                            const int64_t* truth, const int64_t* fptr, const int64_t* fids, int64_t F, int64_t* ranks,
+                            void* ws, hipStream_t st) {
+    const int kp = (int)((K + 15) / 16 * 16);
+    float* ts = static_cast<float*>(ws);
+    int* gcnt = reinterpret_cast<int*>(ts + M);
+    float* fs = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) + (((int64_t)M * 8 + 15) / 16 * 16));
+    const int64_t pairs = (int64_t)M + F, waves = (pairs + 31) / 32;
+    const int64_t pblocks =
+        std::max<int64_t>((waves + kWavesPerBlock - 1) / kWavesPerBlock, ((int64_t)M + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(pair_dot_x3_kernel, dim3((unsigned)pblocks), dim3(kBlock), 0, st, static_cast<const __bf16*>(Ap),
+                       a_rows, static_cast<const __bf16*>(Bp), b_rows, kp, (int64_t)M, (int64_t)N, truth, fptr, fids, F,
+                       ts, fs, gcnt);
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel<true>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
+    (void)attr;
+    const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
+    hipLaunchKernelGGL(gemm_nt_x3p_kernel<true>, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st,
+                       static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp,
+                       nullptr, M, N, (int64_t)0, ts, gcnt);
+    hipLaunchKernelGGL(rank_finish_kernel, dim3((unsigned)((M + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
+                       st, (int64_t)M, (int64_t)N, truth, fptr, fids, ts, fs, gcnt, ranks);
     return 0;
 }
 

@@ -9,7 +9,8 @@ The scores of a query batch against all E entities are computed on the GPU:
   * every other score function: the fused VALU scorer with candidate ids 0..E-1 (row stride 0).
 Ranks are exact integers from kge_rank_filtered: rank = 1 + #(unfiltered e != truth with
 s_e > s_truth). Ties count in the positive's favour; upstream's unstable argsort leaves them
-arbitrary, which no test here exercises (continuous random scores).
+arbitrary, which no test here exercises (continuous random scores). test_step ranks DistMult / ComplEx batches
+without materialising S (kge_eval_rank_planes: the same ranks).
 """
 from __future__ import annotations
 
@@ -143,6 +144,48 @@ def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor
                                  model._D, model._gamma_f, model._range_f, modulus, out=out)
 
 
+_RANK_WS = {}
+
+
+def rank_planes(model, positive_sample: torch.Tensor, mode: str, planes: torch.Tensor, truth: torch.Tensor,
+                filter_ptr: torch.Tensor | None = None, filter_ids: torch.Tensor | None = None,
+                nfilter: int | None = None) -> torch.Tensor | None:
+    """Filtered ranks of a query batch straight from the entity planes, without the [B, E] score matrix
+    (kge_eval_rank_planes: the truth's and the filter entries' scores with the GEMM's own arithmetic, the plane GEMM
+    counting per row the entities above the truth, the filter correction): rank_filtered(score_all(...))'s ranks
+    exactly. DistMult / ComplEx with planes; None where the query-plane form does not apply (then score_all +
+    rank_filtered). filter_ptr must start at 0; nfilter = filter_ptr[-1] (read from the device when not given)."""
+    if model.model_name not in MFMA_FNS or planes is None:
+        return None
+    ent, rel = model.entity_embedding.detach(), model.relation_embedding.detach()
+    if not (model._D % 4 == 0 and ent.data_ptr() % 16 == 0 and rel.data_ptr() % 16 == 0):
+        return None
+    lib = _lib.load()
+    m = ops.mode_id(mode)
+    B, E, K = positive_sample.shape[0], ent.shape[0], ent.shape[1]
+    dev = ent.device
+    st = torch.cuda.current_stream(dev).cuda_stream
+    key = (str(dev), st)
+    nbytes = int(lib.kge_split_bf16x3_bytes(B, K))
+    qp = _Q_PLANES.get(key)
+    if qp is None or qp.numel() < nbytes:
+        qp = _Q_PLANES[key] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    check(lib.kge_eval_query_planes(FN_IDS[model.model_name], m, ent.data_ptr(), E, ent.stride(0), rel.data_ptr(),
+                                    rel.shape[0], rel.stride(0), positive_sample.data_ptr(), B, model._D, qp.data_ptr(),
+                                    B, st), "kge_eval_query_planes")
+    nf = (int(filter_ptr[-1]) if nfilter is None else int(nfilter)) if filter_ptr is not None else 0
+    wsb = int(lib.kge_eval_rank_planes_workspace_size(B, nf))
+    ws = _RANK_WS.get(key)
+    if ws is None or ws.numel() < wsb:
+        ws = _RANK_WS[key] = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+    ranks = torch.empty(B, dtype=torch.int64, device=dev)
+    check(lib.kge_eval_rank_planes(qp.data_ptr(), B, planes.data_ptr(), E, K, B, E, truth.data_ptr(),
+                                   None if filter_ptr is None else filter_ptr.data_ptr(),
+                                   None if filter_ids is None else filter_ids.data_ptr(), nf, ranks.data_ptr(),
+                                   ws.data_ptr(), ws.numel(), st), "kge_eval_rank_planes")
+    return ranks
+
+
 def rank_filtered(scores: torch.Tensor, truth: torch.Tensor, filter_ptr: torch.Tensor | None = None,
                   filter_ids: torch.Tensor | None = None) -> torch.Tensor:
     M, N = scores.shape
@@ -227,11 +270,15 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
             for s in range(0, len(triples), bs):
                 q = triples[s:s + bs]
                 pos = torch.from_numpy(q).to(dev)
-                S = score_all(model, pos, mode, planes=planes)
                 p = ptr[s:s + len(q) + 1]
                 fptr = torch.from_numpy(p - p[0]).to(dev)
                 fids = torch.from_numpy(ids[p[0]:p[-1]]).to(dev)
-                all_ranks.append(rank_filtered(S, pos[:, col].contiguous(), fptr, fids).cpu().numpy())
+                truth = pos[:, col].contiguous()
+                # DistMult / ComplEx: ranks straight from the planes (no [B, E] score matrix); else scores + ranks
+                r = rank_planes(model, pos, mode, planes, truth, fptr, fids, nfilter=int(p[-1] - p[0]))
+                if r is None:
+                    r = rank_filtered(score_all(model, pos, mode, planes=planes), truth, fptr, fids)
+                all_ranks.append(r.cpu().numpy())
     ranks = np.concatenate(all_ranks) if all_ranks else np.zeros(0, dtype=np.int64)
     if world > 1:
         gathered = [None] * world
@@ -240,5 +287,5 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
     return metrics_from_ranks(ranks)
 
 
-__all__ = ["build_filter", "score_all", "rank_filtered", "metrics_from_ranks", "test_step", "entity_planes",
+__all__ = ["build_filter", "score_all", "rank_filtered", "rank_planes", "metrics_from_ranks", "test_step", "entity_planes",
            "split_planes", "HEAD_BATCH", "TAIL_BATCH"]

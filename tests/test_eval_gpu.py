@@ -303,3 +303,67 @@ def test_plane_gemm_b_direct_is_bitwise_the_staged_form(M, N, K):
         out.append(C.cpu())
     assert torch.equal(out[0], out[1])
     assert bool((out[1][:, N:] == -7.0).all())
+
+
+@pytest.mark.parametrize("name,E,d,B", [("DistMult", 900, 96, 70), ("ComplEx", 700, 48, 130), ("DistMult", 14951, 1000, 512),
+                                        ("ComplEx", 3000, 500, 300)])
+def test_rank_planes_equals_score_matrix_ranks(name, E, d, B):
+    """kge_eval_rank_planes (the truth's and the filter entries' scores as MFMA tile diagonals, the plane GEMM counting
+    per row, the filter correction) gives rank_filtered(score_all(...))'s ranks exactly, without the [B, E] matrix;
+    its pair scores are bitwise the GEMM's elements S[q, truth] and S[q, f]. Both modes, a filter of other true
+    triples, out-of-range truths (rank_kernel's -inf truth score), and no filter at all."""
+    de = name == "ComplEx"
+    m = kge.KGEModel(name, E, 7, d, 12.0, double_entity_embedding=de, double_relation_embedding=de, device=DEV, seed=5)
+    g = np.random.RandomState(E + d)
+    true = np.stack([g.randint(E, size=4 * B), g.randint(7, size=4 * B), g.randint(E, size=4 * B)], 1)
+    # a few hub (h, r) / (r, t) pairs so that some queries have long filter lists
+    true[B:B + 200, 0] = true[0, 0]
+    true[B:B + 200, 1] = true[0, 1]
+    true[B + 200:B + 400, 2] = true[1, 2]
+    true[B + 200:B + 400, 1] = true[1, 1]
+    q = true[:B]
+    planes = evaluate.entity_planes(m)
+    lib = _lib.load()
+    for mode in ("head-batch", "tail-batch"):
+        ptr, ids = evaluate.build_filter(q, mode, true)
+        col = 0 if mode == "head-batch" else 2
+        pos = torch.from_numpy(q).to(DEV)
+        truth = pos[:, col].contiguous().clone()
+        truth[3] = -1
+        truth[5] = E  # out of range: every finite score counts
+        fptr, fids = torch.from_numpy(ptr).to(DEV), torch.from_numpy(ids).to(DEV)
+        S = evaluate.score_all(m, pos, mode, planes=planes).clone()
+        want = evaluate.rank_filtered(S, truth, fptr, fids)
+        got = evaluate.rank_planes(m, pos, mode, planes, truth, fptr, fids)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), (name, mode)
+        # the pair scores in the workspace: [B] truth scores first, the filter entries' after the counts
+        (ws,) = evaluate._RANK_WS.values()  # one device, one stream
+        ts = ws[:4 * B].view(torch.float32)
+        tcpu = truth.cpu()
+        ok = (tcpu >= 0) & (tcpu < E)
+        idx = torch.arange(B)
+        assert torch.equal(ts.cpu()[ok], S.cpu()[idx[ok], tcpu[ok]])
+        off = (B * 8 + 15) // 16 * 16
+        nf = len(ids)
+        fs = ws[off:off + 4 * nf].view(torch.float32).cpu()
+        rows = torch.from_numpy(np.repeat(np.arange(B), np.diff(ptr)))
+        assert nf > 200 and torch.equal(fs, S.cpu()[rows, torch.from_numpy(ids)])
+        got0 = evaluate.rank_planes(m, pos, mode, planes, truth)
+        assert torch.equal(got0, evaluate.rank_filtered(S, truth))
+
+
+def test_test_step_ranks_from_planes_equal_the_score_matrix_path(monkeypatch):
+    """test_step on the fused rank path and with it turned off (score_all + rank_filtered): the same metrics."""
+    E, R, d = 1200, 6, 64
+    for name in ("DistMult", "ComplEx"):
+        de = name == "ComplEx"
+        m = kge.KGEModel(name, E, R, d, 9.0, double_entity_embedding=de, double_relation_embedding=de, device=DEV,
+                         seed=2)
+        g = np.random.RandomState(3)
+        true = np.stack([g.randint(E, size=3000), g.randint(R, size=3000), g.randint(E, size=3000)], 1)
+        a = evaluate.test_step(m, true[:300], true, batch_size=128)
+        monkeypatch.setattr(evaluate, "rank_planes", lambda *args, **kw: None)
+        b = evaluate.test_step(m, true[:300], true, batch_size=128)
+        monkeypatch.undo()
+        assert a == b, name

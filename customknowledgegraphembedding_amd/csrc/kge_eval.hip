@@ -922,9 +922,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
 //   3. rank_finish_kernel: rank = 1 + count - #{filter entries f != truth scoring above the truth}: rank_kernel's
 //      rank exactly.
 // ---------------------------------------------------------------------------------------------
-constexpr int kPairDepth = 6;  // 16-k chunks of loads in flight per wave (the chunk chain is latency-bound)
+// One wave per block (a C5 batch has ~4 100 pairs: 130 waves, each on a CU of its own) and 14 of its 16-k chunks of
+// loads in flight: a wave's 63 chunks x 6 MFMAs are one dependent chain, so the loads must run far ahead of it (6
+// chunks in flight and 4-wave blocks: 42.5 us per C5 batch, latency-bound).
+constexpr int kPairDepth = 14;
 
-__global__ __launch_bounds__(kBlock) void pair_dot_x3_kernel(const __bf16* __restrict__ Ap, int64_t a_rows,
+__global__ __launch_bounds__(kWave) void pair_dot_x3_kernel(const __bf16* __restrict__ Ap, int64_t a_rows,
                                                              const __bf16* __restrict__ Bp, int64_t b_rows, int kp,
                                                              int64_t M, int64_t N, const int64_t* __restrict__ truth,
                                                              const int64_t* __restrict__ fptr,
@@ -932,8 +935,8 @@ __global__ __launch_bounds__(kBlock) void pair_dot_x3_kernel(const __bf16* __res
                                                              float* __restrict__ ts, float* __restrict__ fs,
                                                              int* __restrict__ gcnt) {
     const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) gcnt[i] = 0;
-    const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 32;
+    for (int64_t i = (int64_t)blockIdx.x * kWave + lane; i < M; i += (int64_t)gridDim.x * kWave) gcnt[i] = 0;
+    const int64_t p0 = (int64_t)blockIdx.x * 32;
     if (p0 >= M + F) return;  // wave-uniform
     const int64_t p = p0 + col;
     int64_t q = 0, e = -1;
@@ -1082,9 +1085,7 @@ int launch_eval_rank_planes(const void* Ap, int64_t a_rows, const void* Bp, int6
     int* gcnt = reinterpret_cast<int*>(ts + M);
     float* fs = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) + (((int64_t)M * 8 + 15) / 16 * 16));
     const int64_t pairs = (int64_t)M + F, waves = (pairs + 31) / 32;
-    const int64_t pblocks =
-        std::max<int64_t>((waves + kWavesPerBlock - 1) / kWavesPerBlock, ((int64_t)M + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(pair_dot_x3_kernel, dim3((unsigned)pblocks), dim3(kBlock), 0, st, static_cast<const __bf16*>(Ap),
+    hipLaunchKernelGGL(pair_dot_x3_kernel, dim3((unsigned)waves), dim3(kWave), 0, st, static_cast<const __bf16*>(Ap),
                        a_rows, static_cast<const __bf16*>(Bp), b_rows, kp, (int64_t)M, (int64_t)N, truth, fptr, fids, F,
                        ts, fs, gcnt);
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel<true>),

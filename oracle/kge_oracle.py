@@ -370,9 +370,9 @@ def eval_ranks_dense(name, ent, rel, pos, mode, all_true, rtol=1e-6, atol=None):
     """eval_ranks (upstream test_step's filtered rank) for DistMult / ComplEx over every entity at once:
     S = Q . ent^T, rank = 1 + #(unfiltered e != truth with S[e] > S[truth]) (a filtered candidate carries the
     positive's score - 1, below it). Also returns the bounds [lo, hi] of the rank under a score perturbation of
-    rtol * sum_k |Q_k ent[e]_k| per candidate (the accuracy bound of an fp32 evaluation), or of atol[i] per score of
-    query i when given: lo counts the candidates above the truth by more than both perturbations, hi those not below
-    it by more. Returns (ranks, lo, hi), int64 [B]."""
+    rtol * sum_k |Q_k ent[e]_k| per candidate (the accuracy bound of an fp32 evaluation), or of atol when given
+    ([B]: one bound per query's scores; [B, E]: one per score): lo counts the candidates above the truth by more than
+    both perturbations, hi those not below it by more. Returns (ranks, lo, hi), int64 [B]."""
     E = ent.shape[0]
     col = 0 if mode == "head-batch" else 2
     Q = eval_query_dense(name, ent, rel, pos, mode)
@@ -380,7 +380,8 @@ def eval_ranks_dense(name, ent, rel, pos, mode, all_true, rtol=1e-6, atol=None):
     if atol is None:
         T = rtol * (Q.abs() @ ent.abs().T)
     else:
-        T = torch.as_tensor(atol, dtype=S.dtype).reshape(-1, 1).expand_as(S)
+        T = torch.as_tensor(atol, dtype=S.dtype)
+        T = T.expand_as(S) if T.dim() == 2 else T.reshape(-1, 1).expand_as(S)
     others = {}  # (r, t) -> true heads, or (h, r) -> true tails
     for h, r, t in map(tuple, all_true):
         key, e = ((r, t), h) if mode == "head-batch" else ((h, r), t)

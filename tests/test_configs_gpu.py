@@ -203,9 +203,10 @@ def test_c5_fb15k_filtered_ranks_512_queries(name):
     """C5 at the bench's query scale: 512 valid.txt queries per mode through test_step's own path (entity planes
     made once, query planes, the bf16x3 plane GEMM, kge_rank_filtered) against O.eval_ranks_dense (S = Q . E^T
     in fp64; pinned to the per-query eval_ranks in test_oracle.py). Every rank must lie in the oracle's [lo, hi]
-    under the GEMM's accuracy bound (1e-6 sum|q e| per score), and equal the oracle's rank exactly wherever no
-    candidate lies within twice this batch's measured score error (max |S - S64| of the query's row) of the
-    truth's score; at least 95 % of the queries must be decided that way."""
+    under the GEMM's accuracy bound (1e-6 sum|q e| per score: the GEMM's accuracy), and equal the oracle's rank
+    exactly wherever no candidate's fp64 margin to the truth is within the two scores' measured errors |S - S64|
+    (there the fp32 comparisons are the fp64 ones, so this checks the counting and the filter); at least 95 % of the
+    queries must be decided that way."""
     E, R, d = 14951, 1345, 1000
     de = name == "ComplEx"
     m = kge.KGEModel(name, E, R, d, 24.0, double_entity_embedding=de, double_relation_embedding=de, device=DEV,
@@ -226,8 +227,8 @@ def test_c5_fb15k_filtered_ranks_512_queries(name):
         qt = torch.from_numpy(q)
         want, lo, hi = O.eval_ranks_dense(name, ent, rel, qt, mode, true)
         assert bool(((lo <= got) & (got <= hi)).all()), (name, mode)
-        err = (S.detach().cpu().double() - O.eval_scores_dense(name, ent, rel, qt, mode)).abs().amax(dim=1)
-        want2, lo2, hi2 = O.eval_ranks_dense(name, ent, rel, qt, mode, true, atol=2 * err + 1e-30)
+        err = (S.detach().cpu().double() - O.eval_scores_dense(name, ent, rel, qt, mode)).abs()
+        want2, lo2, hi2 = O.eval_ranks_dense(name, ent, rel, qt, mode, true, atol=err + 1e-30)
         decided = lo2 == hi2
         assert torch.equal(want2, want)
         assert bool(((lo2 <= got) & (got <= hi2)).all()), (name, mode)

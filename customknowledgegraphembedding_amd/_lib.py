@@ -157,6 +157,8 @@ SIGNATURES = {
     "kge_eval_rank_planes_workspace_size": (_c_i64, [_c_i64, _c_i64]),
     "kge_eval_rank_planes": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_i64, _c_p,
                                     _c_p, ctypes.c_size_t, _c_p]),
+    "kge_eval_rank_planes_ex": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_i64,
+                                       _c_p, _c_p, ctypes.c_size_t, _c_p, _c_p]),
     "kge_gemm_nt_bf16x3_planes_ex": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p,
                                             _c_p]),
     "kge_rank_filtered": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p]),

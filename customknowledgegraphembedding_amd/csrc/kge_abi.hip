@@ -1207,12 +1207,13 @@ int kge_gemm_nt_bf16x3_planes(const void* A_planes, int64_t a_rows, const void* 
     return kge_gemm_nt_bf16x3_planes_ex(A_planes, a_rows, B_planes, b_rows, K, C, ldc, M, N, nullptr, stream);
 }
 
-// the plane GEMM the library runs (forms->gemm_form 0): 1 = gemm_nt_x3p_kernel, 2 = gemm_nt_x3d_kernel
+// the plane GEMM the library runs (forms->gemm_form 0): 1 = gemm_nt_x3p_kernel 256 x 256, 2 = gemm_nt_x3d_kernel,
+// 3 = gemm_nt_x3p_kernel 256 x 192
 constexpr int kPlanesGemmForm = 1;
 
 int kge_gemm_nt_bf16x3_planes_ex(const void* A_planes, int64_t a_rows, const void* B_planes, int64_t b_rows, int64_t K,
                                  float* C, int64_t ldc, int64_t M, int64_t N, const kge_forms* forms, void* stream) {
-    const int form = forms && (forms->gemm_form == 1 || forms->gemm_form == 2) ? forms->gemm_form : kPlanesGemmForm;
+    const int form = forms && forms->gemm_form >= 1 && forms->gemm_form <= 3 ? forms->gemm_form : kPlanesGemmForm;
     if (M < 0 || N < 0 || K <= 0 || M > a_rows || N > b_rows) return fail(KGE_EINVAL, "bad shape");
     if (M == 0 || N == 0) return ok();
     if (!A_planes || !B_planes || !C) return fail(KGE_EINVAL, "null pointer");
@@ -1261,6 +1262,16 @@ int kge_eval_rank_planes(const void* A_planes, int64_t a_rows, const void* B_pla
                          int64_t M, int64_t N, const int64_t* truth, const int64_t* filter_ptr,
                          const int64_t* filter_ids, int64_t nfilter, int64_t* ranks, void* workspace,
                          size_t workspace_bytes, void* stream) {
+    return kge_eval_rank_planes_ex(A_planes, a_rows, B_planes, b_rows, K, M, N, truth, filter_ptr, filter_ids, nfilter,
+                                   ranks, workspace, workspace_bytes, nullptr, stream);
+}
+
+int kge_eval_rank_planes_ex(const void* A_planes, int64_t a_rows, const void* B_planes, int64_t b_rows, int64_t K,
+                            int64_t M, int64_t N, const int64_t* truth, const int64_t* filter_ptr,
+                            const int64_t* filter_ids, int64_t nfilter, int64_t* ranks, void* workspace,
+                            size_t workspace_bytes, const kge_forms* forms, void* stream) {
+    const int form = forms && (forms->gemm_form == 1 || forms->gemm_form == 3) ? forms->gemm_form
+                                                                               : (kPlanesGemmForm == 3 ? 3 : 1);
     if (M < 0 || N <= 0 || K <= 0 || M > a_rows || N > b_rows || nfilter < 0) return fail(KGE_EINVAL, "bad shape");
     if (M == 0) return ok();
     if (!A_planes || !B_planes || !truth || !ranks || !workspace || (filter_ptr && !filter_ids) ||
@@ -1274,7 +1285,7 @@ int kge_eval_rank_planes(const void* A_planes, int64_t a_rows, const void* B_pla
     if ((int64_t)workspace_bytes < eval_rank_ws_bytes(M, nfilter))
         return fail(KGE_EINVAL, "kge_eval_rank_planes: workspace too small");
     launch_eval_rank_planes(A_planes, a_rows, B_planes, b_rows, K, (int)M, (int)N, truth, filter_ptr, filter_ids,
-                            nfilter, ranks, workspace, (hipStream_t)stream);
+                            nfilter, ranks, workspace, (hipStream_t)stream, form);
     return check_launch("kge_eval_rank_planes");
 }
 

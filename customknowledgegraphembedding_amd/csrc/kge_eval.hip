@@ -627,7 +627,10 @@ struct XpGemmRegs {
 // CNT (kge_eval_rank_planes): no C; the epilogue counts, per query row, the scores above the row's truth score
 // ts[row] (columns < N) and adds the block's counts to gcnt[row] (integer atomics). The accumulators are the
 // CNT = false kernel's, bitwise.
-template <bool CNT>
+// JN: 32-column B tiles per wave; the block tile is 256 x 64 JN (JN 4: 256 x 256; JN 3: 256 x 192, whose 78 tiles
+// per 4 096-query M tile at C5 fill 4.9 rounds of the CUs where 256-wide tiles fill 3.7). Every accumulator element
+// takes the same products in the same order for either JN: C is bitwise the same.
+template <bool CNT, int JN>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2))) void gemm_nt_x3p_kernel(
     const __bf16* __restrict__ Ap, int64_t a_plane, const __bf16* __restrict__ Bp, int64_t b_plane, int kp,
     float* __restrict__ C, int M, int N, int64_t ldc, const float* __restrict__ ts, int* __restrict__ gcnt) {
@@ -639,7 +642,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
     }
     const int half = lane >> 5, col = lane & 31;
     const int wr = wave >> 1, wc = wave & 1;
-    const int ntn = (N + XS_T - 1) / XS_T, ntm = (M + XS_T - 1) / XS_T;
+    constexpr int TN = 64 * JN;  // block tile columns
+    const int ntn = (N + TN - 1) / TN, ntm = (M + XS_T - 1) / XS_T;
     const int nblk = ntn * ntm;
     int bid = blockIdx.x;
     {  // XCD-aware bijective remap (gemm_nt_x3s_kernel's)
@@ -647,14 +651,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
         bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
     }
     const int tn = bid / ntm, tm = bid % ntm;
-    const int m0 = tm * XS_T, n0 = tn * XS_T;
+    const int m0 = tm * XS_T, n0 = tn * TN;
     const rsrc_t ra = make_rsrc(Ap, (uint32_t)(3 * a_plane * 2));
     const rsrc_t rb = make_rsrc(Bp, (uint32_t)(3 * b_plane * 2));
     // thread t stages row t >> 1, k half t & 1 of every plane; a plane is [K / 16][plane rows][16], so chunk g of
-    // the block's rows is contiguous and the offsets advance one chunk slab (plane rows x 32 B) per chunk
+    // the block's rows is contiguous and the offsets advance one chunk slab (plane rows x 32 B) per chunk (B rows
+    // past the tile's TN read zeros into LDS rows nothing reads)
     const int srow = t >> 1, sh = t & 1;
     const uint32_t oa0 = m0 + srow < M ? (uint32_t)(((int64_t)(m0 + srow) * 16 + 8 * sh) * 2) : XS_OOB;
-    const uint32_t ob0 = n0 + srow < N ? (uint32_t)(((int64_t)(n0 + srow) * 16 + 8 * sh) * 2) : XS_OOB;
+    const uint32_t ob0 =
+        (srow < TN && n0 + srow < N) ? (uint32_t)(((int64_t)(n0 + srow) * 16 + 8 * sh) * 2) : XS_OOB;
     const uint32_t pa = (uint32_t)(a_plane * 2), pb = (uint32_t)(b_plane * 2);
     const uint32_t sa = (uint32_t)(a_plane / kp * 32), sb = (uint32_t)(b_plane / kp * 32);  // one chunk slab
     const int so = xs_off(srow, sh);
@@ -678,11 +684,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
             *reinterpret_cast<int4*>(Bs + p * XS_PLANE + so) = R.b[p];
         }
     };
-    f32x16 acc[2][4];
+    f32x16 acc[2][JN];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < JN; ++j)
 #pragma unroll
             for (int r2 = 0; r2 < 16; ++r2) acc[i][j][r2] = 0.f;
     auto compute = [&](int stage) {  // gemm_nt_x3s_kernel's
@@ -696,8 +702,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
             for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * XS_PLANE + o);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int o = xs_off(wc * 128 + j * 32 + col, half);
+        for (int j = 0; j < JN; ++j) {
+            const int o = xs_off(wc * 32 * JN + j * 32 + col, half);
             bf16x8 bb[3];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) bb[pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * XS_PLANE + o);
@@ -719,16 +725,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
         gload(nxt, g + 3);
         __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);  // DS reads: the A fragments and B fragment 0
         __builtin_amdgcn_sched_group_barrier(0x008, 12, 0); // MFMA
+        constexpr int WPJ = 6 / (JN - 1);  // the 6 stores and 6 loads spread over the later B fragments
 #pragma unroll
-        for (int j = 1; j < 4; ++j) {
+        for (int j = 1; j < JN; ++j) {
             __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // B fragment j
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#pragma unroll
+            for (int u = 0; u < WPJ; ++u) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 12 / (WPJ + 1), 0);
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 12 - WPJ * (12 / (WPJ + 1)), 0);
         }
         __syncthreads();
     };
@@ -755,8 +762,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
                 const float tv = m0 + lr < M ? ts[m0 + lr] : INFINITY;
                 int c = 0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int gn = n0 + wc * 128 + j * 32 + col;
+                for (int j = 0; j < JN; ++j) {
+                    const int gn = n0 + wc * 32 * JN + j * 32 + col;
                     const uint64_t bal = __ballot(gn < N && acc[i][j][r] > tv);
                     c += __popcll(half ? (bal >> 32) : (bal & 0xFFFFFFFFull));
                 }
@@ -769,8 +776,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int gn = n0 + wc * 128 + j * 32 + col;
+        for (int j = 0; j < JN; ++j) {
+            const int gn = n0 + wc * 32 * JN + j * 32 + col;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int gm = m0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -1053,10 +1060,26 @@ int launch_split3_planes(const float* X, int64_t rows, int64_t cols, int64_t ld,
     return 0;
 }
 
+template <bool CNT, int JN>
+void launch_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int kp, float* C, int64_t ldc, int M,
+                int N, const float* ts, int* gcnt, hipStream_t st) {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel<CNT, JN>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
+    (void)attr;
+    const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + 64 * JN - 1) / (64 * JN));
+    hipLaunchKernelGGL((gemm_nt_x3p_kernel<CNT, JN>), dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st,
+                       static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp, C, M,
+                       N, ldc, ts, gcnt);
+}
+
 int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, float* C, int64_t ldc,
                        int M, int N, hipStream_t st, int form) {
     const int kp = (int)((K + 15) / 16 * 16);
     const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
+    if (form == 3) {  // 256 x 192 block tiles
+        launch_x3p<false, 3>(Ap, a_rows, Bp, b_rows, kp, C, ldc, M, N, nullptr, nullptr, st);
+        return 0;
+    }
     if (form == 2) {  // B straight into registers, A staged 32 k per barrier (gemm_nt_x3d_kernel)
         static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3d_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XD_STAGE) == hipSuccess;
@@ -1066,12 +1089,7 @@ int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b
                            C, M, N, ldc);
         return 0;
     }
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel<false>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
-    (void)attr;
-    hipLaunchKernelGGL(gemm_nt_x3p_kernel<false>, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st,
-                       static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp, C, M,
-                       N, ldc, nullptr, nullptr);
+    launch_x3p<false, 4>(Ap, a_rows, Bp, b_rows, kp, C, ldc, M, N, nullptr, nullptr, st);
     return 0;
 }
 
@@ -1079,7 +1097,7 @@ int64_t eval_rank_ws_bytes(int64_t M, int64_t F) { return ((M * 8 + 15) / 16 * 1
 
 int launch_eval_rank_planes(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, int M, int N,
                             const int64_t* truth, const int64_t* fptr, const int64_t* fids, int64_t F, int64_t* ranks,
-                            void* ws, hipStream_t st) {
+                            void* ws, hipStream_t st, int form) {
     const int kp = (int)((K + 15) / 16 * 16);
     float* ts = static_cast<float*>(ws);
     int* gcnt = reinterpret_cast<int*>(ts + M);
@@ -1088,13 +1106,10 @@ int launch_eval_rank_planes(const void* Ap, int64_t a_rows, const void* Bp, int6
     hipLaunchKernelGGL(pair_dot_x3_kernel, dim3((unsigned)waves), dim3(kWave), 0, st, static_cast<const __bf16*>(Ap),
                        a_rows, static_cast<const __bf16*>(Bp), b_rows, kp, (int64_t)M, (int64_t)N, truth, fptr, fids, F,
                        ts, fs, gcnt);
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_x3p_kernel<true>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * XS_STAGE) == hipSuccess;
-    (void)attr;
-    const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
-    hipLaunchKernelGGL(gemm_nt_x3p_kernel<true>, dim3((unsigned)tiles), dim3(512), 2 * XS_STAGE, st,
-                       static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp,
-                       nullptr, M, N, (int64_t)0, ts, gcnt);
+    if (form == 3)
+        launch_x3p<true, 3>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
+    else
+        launch_x3p<true, 4>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
     hipLaunchKernelGGL(rank_finish_kernel, dim3((unsigned)((M + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
                        st, (int64_t)M, (int64_t)N, truth, fptr, fids, ts, fs, gcnt, ranks);
     return 0;

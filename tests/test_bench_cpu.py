@@ -26,6 +26,11 @@ def test_gpus2_self_launches_two_ranks_one_line():
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout
     line = lines[0]
+    # the driver's contract keys, as the N > 1 line carries them
+    assert {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"} <= set(line)
+    assert line["metric"] == bench.METRIC and line["scaling"] == "weak" and line["higher_is_better"] is True
+    assert {"workload", "parallelism"} <= set(line["config"]) and line["config"]["parallelism"] == "replicas2"
     assert line["n_gpus"] == 2 and line["steps"] == 3 and line["dry_run"]
     assert line["rank_sum"] == 1  # ranks 0 and 1 both joined the process group
     # the N > 1 row-sharded record: per-variant step times, the selected form, and every rank's diagnosis

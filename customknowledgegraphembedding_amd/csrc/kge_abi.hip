@@ -1208,12 +1208,13 @@ int kge_gemm_nt_bf16x3_planes(const void* A_planes, int64_t a_rows, const void* 
 }
 
 // the plane GEMM the library runs (forms->gemm_form 0): 1 = gemm_nt_x3p_kernel 256 x 256, 2 = gemm_nt_x3d_kernel,
-// 3 = gemm_nt_x3p_kernel 256 x 192
-constexpr int kPlanesGemmForm = 1;
+// 3 = gemm_nt_x3p_kernel 256 x 192, 4 = gemm_nt_x3l_kernel (LDS-DMA staging, three stages; 546 against 551 us at
+// C5's shape, 568 against 572 us for the rank call: profiles/r06_gemm_dma_ab.txt)
+constexpr int kPlanesGemmForm = 4;
 
 int kge_gemm_nt_bf16x3_planes_ex(const void* A_planes, int64_t a_rows, const void* B_planes, int64_t b_rows, int64_t K,
                                  float* C, int64_t ldc, int64_t M, int64_t N, const kge_forms* forms, void* stream) {
-    const int form = forms && forms->gemm_form >= 1 && forms->gemm_form <= 3 ? forms->gemm_form : kPlanesGemmForm;
+    const int form = forms && forms->gemm_form >= 1 && forms->gemm_form <= 4 ? forms->gemm_form : kPlanesGemmForm;
     if (M < 0 || N < 0 || K <= 0 || M > a_rows || N > b_rows) return fail(KGE_EINVAL, "bad shape");
     if (M == 0 || N == 0) return ok();
     if (!A_planes || !B_planes || !C) return fail(KGE_EINVAL, "null pointer");
@@ -1270,8 +1271,9 @@ int kge_eval_rank_planes_ex(const void* A_planes, int64_t a_rows, const void* B_
                             int64_t M, int64_t N, const int64_t* truth, const int64_t* filter_ptr,
                             const int64_t* filter_ids, int64_t nfilter, int64_t* ranks, void* workspace,
                             size_t workspace_bytes, const kge_forms* forms, void* stream) {
-    const int form = forms && (forms->gemm_form == 1 || forms->gemm_form == 3) ? forms->gemm_form
-                                                                               : (kPlanesGemmForm == 3 ? 3 : 1);
+    const int form = forms && (forms->gemm_form == 1 || forms->gemm_form >= 3) && forms->gemm_form <= 4
+                         ? forms->gemm_form
+                         : (kPlanesGemmForm == 2 ? 1 : kPlanesGemmForm);
     if (M < 0 || N <= 0 || K <= 0 || M > a_rows || N > b_rows || nfilter < 0) return fail(KGE_EINVAL, "bad shape");
     if (M == 0) return ok();
     if (!A_planes || !B_planes || !truth || !ranks || !workspace || (filter_ptr && !filter_ids) ||

@@ -624,6 +624,13 @@ struct XpGemmRegs {
     int4 a[3], b[3];
 };
 
+// Knock-out builds for the step-cost breakdown probe (scripts/x3p_knockout_probe.py; wrong results by design,
+// never the library's build): bit 0 drops the per-chunk barrier, bit 1 the LDS stores, bit 2 the global loads,
+// bit 3 the fragment reads (the MFMAs take fragments read once before the loop).
+#ifndef KGE_X3P_KO
+#define KGE_X3P_KO 0
+#endif
+
 // CNT (kge_eval_rank_planes): no C; the epilogue counts, per query row, the scores above the row's truth score
 // ts[row] (columns < N) and adds the block's counts to gcnt[row] (integer atomics). The accumulators are the
 // CNT = false kernel's, bitwise.
@@ -719,10 +726,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
     // 568 us at C5 against the compiler's order (MFMAs first, then the stores and loads; profiles/r05_x3p_sched_ab.txt;
     // an s_setprio(1) around the step on top measured the same). The last step's store lands in a stage nothing
     // reads again.
+    bf16x8 ko_a[2][3], ko_b[3];  // KGE_X3P_KO bit 3: loop-invariant fragments
     auto step = [&](int g, XpGemmRegs& nxt) {
-        compute(g & 1);
-        sstore(nxt, (g + 1) & 1);
-        gload(nxt, g + 3);
+        if constexpr (KGE_X3P_KO & 8) {
+#pragma unroll
+            for (int j = 0; j < JN; ++j)
+#pragma unroll
+                for (int q = 0; q < 6; ++q)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ko_a[i][kX3A[q]], ko_b[kX3B[q]], acc[i][j],
+                                                                            0, 0, 0);
+        } else {
+            compute(g & 1);
+        }
+        if constexpr (!(KGE_X3P_KO & 2)) sstore(nxt, (g + 1) & 1);
+        if constexpr (!(KGE_X3P_KO & 4)) gload(nxt, g + 3);
         __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);  // DS reads: the A fragments and B fragment 0
         __builtin_amdgcn_sched_group_barrier(0x008, 12, 0); // MFMA
         constexpr int WPJ = 6 / (JN - 1);  // the 6 stores and 6 loads spread over the later B fragments
@@ -737,7 +756,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
             }
             __builtin_amdgcn_sched_group_barrier(0x008, 12 - WPJ * (12 / (WPJ + 1)), 0);
         }
-        __syncthreads();
+        if constexpr (!(KGE_X3P_KO & 1)) __syncthreads();
     };
     XpGemmRegs R0, R1;
     gload(R0, 0);
@@ -745,6 +764,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
     sstore(R0, 0);
     gload(R0, 2);
     __syncthreads();
+    if constexpr (KGE_X3P_KO & 8) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                ko_a[i][pl] = *reinterpret_cast<const bf16x8*>(gp_smem + pl * XS_PLANE + xs_off(wr * 64 + i * 32 + col, half));
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            ko_b[pl] = *reinterpret_cast<const bf16x8*>(gp_smem + 3 * XS_PLANE + pl * XS_PLANE + xs_off(wc * 32 * JN + col, half));
+    }
     int g = 0;
     for (; g + 1 < T; g += 2) {
         step(g, R1);
@@ -778,6 +807,151 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
             const int gn = n0 + wc * 32 * JN + j * 32 + col;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = m0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (gm < M && gn < N) C[(int64_t)gm * ldc + gn] = acc[i][j][r];
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The plane GEMM with LDS-DMA staging (round 6, form 4): gemm_nt_x3p_kernel's tile, waves, fragments, products and
+// epilogue, with each chunk's six planes (A and B, 3 x 8 KB each) copied global -> LDS by `buffer_load_dwordx4 ...
+// lds` (one 1-KB wave-instruction per plane: the LDS image of a wave's 32 rows is lane-linear, so xs_off's swizzle
+// is put on the SOURCE address: lane L of row r loads half (L & 1) ^ ((r >> 3) & 1)). No staging registers, no
+// ds_write pass: a knock-out build of gemm_nt_x3p_kernel without its stores and loads ran 483 against 572 us at
+// C5's shape (profiles/r06_x3p_knockout.txt).
+//   * three LDS stages (144 KB, static objects so the compiler's LDS-DMA wait tracking tells them apart); step g
+//     issues chunk g + 2's copies into the stage step g - 1 multiplied, multiplies stage g % 3, waits for chunk
+//     g + 1's copies (counted vmcnt: chunk g + 2's six stay in flight) and meets the others at a raw s_barrier
+//     (a __syncthreads() fence would drain every copy in flight);
+//   * the loop is unrolled by 3 so that every stage access names its object.
+// Per accumulator the same products in the same order: C (and the counts) bitwise gemm_nt_x3p_kernel<.., 4>'s.
+// ---------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* xl_lds_t;
+
+template <bool CNT>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2))) void gemm_nt_x3l_kernel(
+    const __bf16* __restrict__ Ap, int64_t a_plane, const __bf16* __restrict__ Bp, int64_t b_plane, int kp,
+    float* __restrict__ C, int M, int N, int64_t ldc, const float* __restrict__ ts, int* __restrict__ gcnt) {
+    __shared__ __attribute__((aligned(16))) unsigned char xl0[XS_STAGE];
+    __shared__ __attribute__((aligned(16))) unsigned char xl1[XS_STAGE];
+    __shared__ __attribute__((aligned(16))) unsigned char xl2[XS_STAGE];
+    __shared__ int rowcnt[CNT ? XS_T : 1];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if constexpr (CNT) {
+        if (t < XS_T) rowcnt[t] = 0;  // visible after the prologue's barrier
+    }
+    const int half = lane >> 5, col = lane & 31;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int ntn = (N + XS_T - 1) / XS_T, ntm = (M + XS_T - 1) / XS_T;
+    const int nblk = ntn * ntm;
+    int bid = blockIdx.x;
+    {  // XCD-aware bijective remap (gemm_nt_x3s_kernel's)
+        const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    }
+    const int tn = bid / ntm, tm = bid % ntm;
+    const int m0 = tm * XS_T, n0 = tn * XS_T;
+    const rsrc_t ra = make_rsrc(Ap, (uint32_t)(3 * a_plane * 2));
+    const rsrc_t rb = make_rsrc(Bp, (uint32_t)(3 * b_plane * 2));
+    // lane t writes LDS bytes [16 t, 16 t + 16) of each plane image: row t >> 1, slot t & 1, which holds the row's
+    // k half (t & 1) ^ ((row >> 3) & 1) (xs_off's swizzle, applied at the source)
+    const int srow = t >> 1, sh = (t & 1) ^ ((srow >> 3) & 1);
+    const uint32_t oa0 = m0 + srow < M ? (uint32_t)(((int64_t)(m0 + srow) * 16 + 8 * sh) * 2) : XS_OOB;
+    const uint32_t ob0 = n0 + srow < N ? (uint32_t)(((int64_t)(n0 + srow) * 16 + 8 * sh) * 2) : XS_OOB;
+    const uint32_t pa = (uint32_t)(a_plane * 2), pb = (uint32_t)(b_plane * 2);
+    const uint32_t sa = (uint32_t)(a_plane / kp * 32), sb = (uint32_t)(b_plane / kp * 32);  // one chunk slab
+    const int T = kp / 16;
+    const int wo = wave * 1024;  // this wave's 1-KB piece of every plane image
+    auto dma = [&](unsigned char* S, int g) {  // chunk g's six planes into stage S (past K: out of range, unread)
+        const bool ina = oa0 != XS_OOB && g < T, inb = ob0 != XS_OOB && g < T;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (xl_lds_t)(S + p * XS_PLANE + wo), 16,
+                                                     ina ? oa0 + p * pa + g * sa : XS_OOB, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (xl_lds_t)(S + (3 + p) * XS_PLANE + wo), 16,
+                                                     inb ? ob0 + p * pb + g * sb : XS_OOB, 0, 0, 0);
+        }
+    };
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r2 = 0; r2 < 16; ++r2) acc[i][j][r2] = 0.f;
+    auto compute = [&](const unsigned char* As) {  // gemm_nt_x3p_kernel's
+        const unsigned char* Bs = As + 3 * XS_PLANE;
+        bf16x8 a[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int o = xs_off(wr * 64 + i * 32 + col, half);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * XS_PLANE + o);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int o = xs_off(wc * 128 + j * 32 + col, half);
+            bf16x8 bb[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) bb[pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * XS_PLANE + o);
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0, 0, 0);
+        }
+    };
+    // step g: copies of chunk g + 2 into N2 (multiplied at step g - 1, released by that step's barrier), multiply
+    // Cur, then wait until chunk g + 1's copies (issued at step g - 1) have landed: 6 copies stay in flight
+    auto step = [&](int g, const unsigned char* Cur, unsigned char* N2) {
+        dma(N2, g + 2);
+        __builtin_amdgcn_sched_barrier(0);  // the copies first: a full step for them to land
+        compute(Cur);
+        asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    dma(xl0, 0);
+    dma(xl1, 1);
+    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int g = 0;
+    for (; g + 2 < T; g += 3) {
+        step(g, xl0, xl2);
+        step(g + 1, xl1, xl0);
+        step(g + 2, xl2, xl1);
+    }
+    if (g < T) step(g, xl0, xl2);
+    if (g + 1 < T) step(g + 1, xl1, xl0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight past the loop (copies of chunks >= T)
+    if constexpr (CNT) {
+        // gemm_nt_x3p_kernel's count epilogue
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int lr = wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const float tv = m0 + lr < M ? ts[m0 + lr] : INFINITY;
+                int c = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int gn = n0 + wc * 128 + j * 32 + col;
+                    const uint64_t bal = __ballot(gn < N && acc[i][j][r] > tv);
+                    c += __popcll(half ? (bal >> 32) : (bal & 0xFFFFFFFFull));
+                }
+                if (col == 0 && c) atomicAdd(&rowcnt[lr], c);
+            }
+        __syncthreads();
+        if (t < XS_T && rowcnt[t] && m0 + t < M) atomicAdd(&gcnt[m0 + t], rowcnt[t]);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int gn = n0 + wc * 128 + j * 32 + col;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int gm = m0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -1072,10 +1246,23 @@ void launch_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, 
                        N, ldc, ts, gcnt);
 }
 
+template <bool CNT>
+void launch_x3l(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int kp, float* C, int64_t ldc, int M,
+                int N, const float* ts, int* gcnt, hipStream_t st) {
+    const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
+    hipLaunchKernelGGL((gemm_nt_x3l_kernel<CNT>), dim3((unsigned)tiles), dim3(512), 0, st,
+                       static_cast<const __bf16*>(Ap), a_rows * kp, static_cast<const __bf16*>(Bp), b_rows * kp, kp, C, M,
+                       N, ldc, ts, gcnt);
+}
+
 int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, float* C, int64_t ldc,
                        int M, int N, hipStream_t st, int form) {
     const int kp = (int)((K + 15) / 16 * 16);
     const int64_t tiles = (int64_t)((M + XS_T - 1) / XS_T) * ((N + XS_T - 1) / XS_T);
+    if (form == 4) {  // LDS-DMA staging, three stages
+        launch_x3l<false>(Ap, a_rows, Bp, b_rows, kp, C, ldc, M, N, nullptr, nullptr, st);
+        return 0;
+    }
     if (form == 3) {  // 256 x 192 block tiles
         launch_x3p<false, 3>(Ap, a_rows, Bp, b_rows, kp, C, ldc, M, N, nullptr, nullptr, st);
         return 0;
@@ -1106,7 +1293,9 @@ int launch_eval_rank_planes(const void* Ap, int64_t a_rows, const void* Bp, int6
     hipLaunchKernelGGL(pair_dot_x3_kernel, dim3((unsigned)waves), dim3(kWave), 0, st, static_cast<const __bf16*>(Ap),
                        a_rows, static_cast<const __bf16*>(Bp), b_rows, kp, (int64_t)M, (int64_t)N, truth, fptr, fids, F,
                        ts, fs, gcnt);
-    if (form == 3)
+    if (form == 4)
+        launch_x3l<true>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
+    else if (form == 3)
         launch_x3p<true, 3>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
     else
         launch_x3p<true, 4>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);

@@ -97,7 +97,8 @@ struct TsParams {
     int xsplit, ksplit;
     float* xk;
     int64_t xk_ld;
-    int form;  // kge_forms.transparse_form: 0 the library's, 1 the forward's operands split per fragment
+    int form;  // kge_forms.transparse_form: 0 the library's, 1 the forward's operands split per fragment, 2 the
+               // head-batch split-once kernel in the compiler's instruction order
     // kge_transparse_step_forward: the negative call's row reduction (model.py:168-171, row_reduce_fast) in the
     // head-batch kernels' epilogue when one block holds a whole row (out_neg), and the positive call's
     // logsigmoid (model.py:145) in the split form's finish (out_pos_ls)
@@ -881,6 +882,10 @@ ts_fwd_x3_kernel(TsParams p) {
 //   * two LDS stages (96 KB) and two register sets: chunk g + 2 is loaded while chunk g is multiplied and
 //     chunk g + 1 stored, one barrier per chunk.
 // The 48 MFMAs of a chunk per wave read 18 ds_read_b128 (2 A fragments x 3 planes, 4 B fragments x 3).
+// SCHED (the default, round 6): the staging of chunk g + 1 (~110 VALU of splitting, 14-18 LDS stores) and the
+// loads of chunk g + 3 are placed among the chunk's last 36 MFMAs (the eval GEMM's sched-group recipe); the
+// compiler's own order (form 2) issues all 48 MFMAs first and then the staging, with both waves of a SIMD in the
+// same phase, so the matrix pipe idles through that tail every chunk. The same instructions either way: bitwise.
 // ---------------------------------------------------------------------------------------------
 constexpr int kXsPlane = XBR * 16 * 2;  // bytes of one bf16 plane chunk (256 rows x 16 k)
 constexpr int kXsStage = 6 * kXsPlane;  // A planes then B planes
@@ -906,7 +911,14 @@ struct XsRegs {
     int4 bp[3];  // B from the pre-split planes (BPL)
 };
 
-template <bool MASK, bool BPL>
+// Knock-out builds for the step-cost breakdown probe (scripts/x3p_knockout_probe.py; wrong results by design,
+// never the library's build), applied to the compiler-order step (transparse_form 2): bit 0 drops the per-chunk
+// barrier, bit 1 the LDS stores (and the splits), bit 2 the global loads.
+#ifndef KGE_TS_KO
+#define KGE_TS_KO 0
+#endif
+
+template <bool MASK, bool BPL, bool SCHED>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kXThreads), amdgpu_waves_per_eu(2))) void
 ts_fwd_x3s_kernel(TsParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char xs_smem[];  // 2 stages, then u - 1 (d floats)
@@ -1110,17 +1122,98 @@ ts_fwd_x3s_kernel(TsParams p) {
                 }
             }
     };
+    // SCHED: compute, sstore and gload of one step in the order the matrix pipe wants, written out in source
+    // order between scheduling fences (the scheduler's own interleave of this step is undone by its register-
+    // pressure check at 2 waves per SIMD, 254 VGPRs): B fragment j + 1 is read before fragment j's 12 MFMAs, and
+    // after MFMAs 2, 6 and 10 of fragments 1-3 one piece of the staging runs (a row of A split and stored, half of
+    // B's split, one column of B's stores, the loads of chunk g + 3 into the registers just stored). The same
+    // MFMAs in the same order per accumulator, the same splits: bitwise the other order's scores.
+    auto compute_staged = [&](int g, XsRegs& nxt) {
+        const unsigned char* A = xs_smem + (g & 1) * kXsStage;
+        const unsigned char* Bs = A + 3 * kXsPlane;
+        unsigned char* SA = xs_smem + ((g + 1) & 1) * kXsStage;
+        unsigned char* SB = SA + 3 * kXsPlane;
+        bf16x4_t e0, e1, e2, o0, o1, o2;  // B's three terms at k = 2 kp (e) and 2 kp + 1 (o) of 4 columns
+        auto piece = [&](int pc) {
+            if (pc < 2) {  // A row u: split and store (sstore's)
+                const int u = pc, row = (t >> 2) + 128 * u;
+                bf16x4_t s0, s1, s2;
+                split3_x4(f32x4_t{nxt.a[u].x, nxt.a[u].y, nxt.a[u].z, nxt.a[u].w}, s0, s1, s2);
+                const int o = xs_off(row, aq >> 1) + (aq & 1) * 8;
+                *reinterpret_cast<bf16x4_t*>(SA + o) = s0;
+                *reinterpret_cast<bf16x4_t*>(SA + kXsPlane + o) = s1;
+                *reinterpret_cast<bf16x4_t*>(SA + 2 * kXsPlane + o) = s2;
+            } else if (pc < 8) {
+                if constexpr (BPL) {
+                    if (pc < 5) *reinterpret_cast<int4*>(SB + (pc - 2) * kXsPlane + xs_off(spc, sph)) = nxt.bp[pc - 2];
+                } else if (pc < 4) {
+                    float4 b = nxt.b[pc - 2];
+                    if (fuse_mask) b = mul4(b, nxt.m[pc - 2]);
+                    if (pc == 2)
+                        split3_x4(f32x4_t{b.x, b.y, b.z, b.w}, e0, e1, e2);
+                    else
+                        split3_x4(f32x4_t{b.x, b.y, b.z, b.w}, o0, o1, o2);
+                } else {
+                    const int c = pc - 4, cl = 4 * bjq + c;
+                    const int o = xs_off(cl, bkp >> 2) + (bkp & 3) * 4;
+                    *reinterpret_cast<bf16x2_t*>(SB + o) = bf16x2_t{e0[c], o0[c]};
+                    *reinterpret_cast<bf16x2_t*>(SB + kXsPlane + o) = bf16x2_t{e1[c], o1[c]};
+                    *reinterpret_cast<bf16x2_t*>(SB + 2 * kXsPlane + o) = bf16x2_t{e2[c], o2[c]};
+                }
+            } else {
+                gload(nxt, g + 3);
+            }
+        };
+        bf16x8 a[2][3], bb[3], bn[3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int o = xs_off(wr * 64 + i * 32 + col, half);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * kXsPlane + o);
+        }
+        {
+            const int o = xs_off(wc * 128 + col, half);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) bb[pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * kXsPlane + o);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j < 3) {
+                const int o = xs_off(wc * 128 + (j + 1) * 32 + col, half);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) bn[pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * kXsPlane + o);
+            }
+#pragma unroll
+            for (int m = 0; m < 12; ++m) {
+                const int q = m >> 1, i = m & 1;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][kX3A[q]], bb[kX3B[q]], acc[i][j], 0, 0, 0);
+                if (j >= 1 && m % 4 == 1) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    piece((j - 1) * 3 + m / 4);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) bb[pl] = bn[pl];
+        }
+    };
     // one chunk step: multiply stage g % 2, store chunk g + 1 (held in `nxt`) into the other stage, load chunk
-    // g + 3 into `nxt` (chunk g + 2 is in flight in the other set), fold at the end of a column super-tile
+    // g + 3 into `nxt` (chunk g + 2 is in flight in the other set), fold at the end of a column super-tile. The
+    // store is unconditional (one basic block for the schedule): the last step's lands in a stage nothing reads
+    // again, after the barrier that ended that stage's last multiply.
     auto step = [&](int g, XsRegs& nxt) {
-        compute(g & 1);
-        if (g + 1 < T) sstore(nxt, (g + 1) & 1);
-        gload(nxt, g + 3);
+        if constexpr (SCHED) {
+            compute_staged(g, nxt);
+        } else {
+            compute(g & 1);
+            if constexpr (!(KGE_TS_KO & 2)) sstore(nxt, (g + 1) & 1);
+            if constexpr (!(KGE_TS_KO & 4)) gload(nxt, g + 3);
+        }
         if ((g + 1) % nk == 0) {
             fold(g / nk);
             zero_acc();
         }
-        __syncthreads();
+        if constexpr (!(KGE_TS_KO & 1)) __syncthreads();
     };
     XsRegs R0, R1;
     zero_acc();
@@ -1523,13 +1616,24 @@ int64_t mplanes_bytes(int64_t nrel, int64_t d) {
     return nrel * 3 * nk * cols * 16 * 2;
 }
 
-template <bool MASK, bool BPL>
-void launch_x3s(const TsParams& q, unsigned grid, size_t lds, hipStream_t st) {
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel<MASK, BPL>),
+template <bool MASK, bool BPL, bool SCHED>
+void launch_x3s_form(const TsParams& q, unsigned grid, size_t lds, hipStream_t st) {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(ts_fwd_x3s_kernel<MASK, BPL, SCHED>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  2 * kXsStage + kXsMaxDim * 4) == hipSuccess;
     (void)attr;
-    hipLaunchKernelGGL((ts_fwd_x3s_kernel<MASK, BPL>), dim3(grid), dim3(kXThreads), lds, st, q);
+    hipLaunchKernelGGL((ts_fwd_x3s_kernel<MASK, BPL, SCHED>), dim3(grid), dim3(kXThreads), lds, st, q);
+}
+
+// form 2: the compiler's instruction order (the A/B against the scheduled step; bitwise the same scores). The
+// mask-product variant keeps it always: its scheduled step spills 26 VGPRs into the loop (613 against 404 us at
+// c6's shape on 237 relations, profiles/r06_ts_sched_ab.txt).
+template <bool MASK, bool BPL>
+void launch_x3s(const TsParams& q, unsigned grid, size_t lds, hipStream_t st) {
+    if (q.form == 2 || MASK)
+        launch_x3s_form<MASK, BPL, false>(q, grid, lds, st);
+    else
+        launch_x3s_form<MASK, BPL, true>(q, grid, lds, st);
 }
 
 template <int NWV, int JPW, int DEP, bool MASK>
@@ -1925,7 +2029,7 @@ bool launch_rows(const TsParams& p, hipStream_t st) {
         // staging where the 32-bit buffer offsets reach (form 1: the forms that split each fragment in registers,
         // for the bitwise / rounding cross-checks)
         if (use_v4(p)) {
-            const bool xs_ok = p.form == 0 && p.d <= kXsMaxDim && p.nent * p.ent_ld * 4 < (int64_t)kXsOOB &&
+            const bool xs_ok = (p.form == 0 || p.form == 2) && p.d <= kXsMaxDim && p.nent * p.ent_ld * 4 < (int64_t)kXsOOB &&
                                (int64_t)p.d * p.d * 4 < (int64_t)kXsOOB;
             if (p.grouped && xs_ok) {
                 // single / tail-batch rows: 64 rows of one relation per block (ts_fwd_x3g_kernel), all columns, or

@@ -1,5 +1,5 @@
 """Round 6: C5's rank call (kge_eval_rank_planes_ex: pair scores, counting plane GEMM, finish) with 256 x 256 (form 1)
-and 256 x 192 (form 3) GEMM tiles, 4 096 DistMult d=1000 queries x 14 951 entities with a filter, same process,
+and 256 x 192 (form 3) GEMM tiles and LDS-DMA staging (form 4), 4 096 DistMult d=1000 queries x 14 951 entities with a filter, same process,
 events around 10 calls, 3 rounds interleaved; ranks compared. Usage: python scripts/rank_form_probe.py"""
 import ctypes
 import json
@@ -30,10 +30,10 @@ planes = evaluate.entity_planes(m)
 want = evaluate.rank_planes(m, pos, "tail-batch", planes, truth, fptr, fids)  # writes the query planes
 (qp,) = evaluate._Q_PLANES.values()
 (ws,) = evaluate._RANK_WS.values()
-res = {"Bq": Bq, "E": E, "d": d, "nfilter": int(len(ids)), "form1_us": [], "form3_us": []}
+res = {"Bq": Bq, "E": E, "d": d, "nfilter": int(len(ids)), "form1_us": [], "form3_us": [], "form4_us": []}
 outs = {}
 for _ in range(3):
-    for form in (1, 3):
+    for form in (1, 3, 4):
         f = _lib.forms(gemm_form=form)
         r = torch.empty(Bq, dtype=torch.int64, device=dev)
 
@@ -51,5 +51,5 @@ for _ in range(3):
         torch.cuda.synchronize()
         res[f"form{form}_us"].append(round(e0.elapsed_time(e1) / 10 * 1e3, 1))
         outs[form] = r.clone()
-res["ranks_equal"] = bool(torch.equal(outs[1], want) and torch.equal(outs[3], want))
+res["ranks_equal"] = all(bool(torch.equal(outs[f], want)) for f in (1, 3, 4))
 print(json.dumps(res), flush=True)

@@ -284,7 +284,8 @@ def test_eval_query_planes_is_bitwise_query_then_split(fn, D, B, mode):
                                    (129, 77, 36), (512, 2048, 2000), (300, 700, 48)])
 def test_plane_gemm_b_direct_is_bitwise_the_staged_form(M, N, K):
     """gemm_nt_x3d_kernel (B's fragments straight into registers, A staged 32 k per barrier: kge_forms.gemm_form 2)
-    against gemm_nt_x3p_kernel (both operands staged per 16-k chunk: form 1) on the same planes: C bitwise equal,
+    and gemm_nt_x3l_kernel (both staged by LDS-DMA copies, three stages: form 4) against gemm_nt_x3p_kernel (both
+    operands staged per 16-k chunk: form 1) on the same planes: C bitwise equal,
     with partial tiles in M and N, odd and even 16-k chunk counts (K 1000: 63 chunks; 2000: 125; 48: 3) and a
     padded leading dimension; nothing written past N."""
     g = torch.Generator().manual_seed(M + 5 * N + K)
@@ -294,15 +295,16 @@ def test_plane_gemm_b_direct_is_bitwise_the_staged_form(M, N, K):
     st = torch.cuda.current_stream().cuda_stream
     ap, bp = evaluate.split_planes(A), evaluate.split_planes(Bm)
     out = []
-    for form in (1, 2, 3):  # 3: the staged form with 256 x 192 tiles
+    for form in (1, 2, 3, 4):  # 3: the staged form with 256 x 192 tiles
         C = torch.full((M, N + 3), -7.0, device=DEV)
         f = _lib.forms(gemm_form=form)
         assert lib.kge_gemm_nt_bf16x3_planes_ex(ap.data_ptr(), M, bp.data_ptr(), N, K, C.data_ptr(), N + 3, M, N,
                                                 ctypes.addressof(f), st) == 0
         torch.cuda.synchronize()
         out.append(C.cpu())
-    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
-    assert bool((out[1][:, N:] == -7.0).all()) and bool((out[2][:, N:] == -7.0).all())
+    for o in out[1:]:
+        assert torch.equal(out[0], o)
+        assert bool((o[:, N:] == -7.0).all())
 
 
 @pytest.mark.parametrize("name,E,d,B", [("DistMult", 900, 96, 70), ("ComplEx", 700, 48, 130), ("DistMult", 14951, 1000, 512),
@@ -351,16 +353,19 @@ def test_rank_planes_equals_score_matrix_ranks(name, E, d, B):
         assert nf > 10 and torch.equal(fs, S.cpu()[rows, torch.from_numpy(ids)])
         got0 = evaluate.rank_planes(m, pos, mode, planes, truth)
         assert torch.equal(got0, evaluate.rank_filtered(S, truth))
-        # the counting GEMM with 256 x 192 tiles (kge_forms.gemm_form 3): the same ranks
+        # the counting GEMM with 256 x 256 tiles staged through registers (kge_forms.gemm_form 1), 256 x 192 tiles
+        # (3) and LDS-DMA staging (4): the same ranks
         K = m.entity_embedding.shape[1]
-        f3 = _lib.forms(gemm_form=3)
-        r3 = torch.empty(B, dtype=torch.int64, device=DEV)
         (qpl,) = evaluate._Q_PLANES.values()  # the batch's query planes, as rank_planes wrote them
-        assert lib.kge_eval_rank_planes_ex(qpl.data_ptr(), B, planes.data_ptr(), E, K, B, E, truth.data_ptr(),
-                                           fptr.data_ptr(), fids.data_ptr(), len(ids), r3.data_ptr(), ws.data_ptr(),
-                                           ws.numel(), ctypes.addressof(f3), torch.cuda.current_stream().cuda_stream) == 0
-        torch.cuda.synchronize()
-        assert torch.equal(r3, want), (name, mode)
+        for form in (1, 3, 4):
+            f3 = _lib.forms(gemm_form=form)
+            r3 = torch.empty(B, dtype=torch.int64, device=DEV)
+            assert lib.kge_eval_rank_planes_ex(qpl.data_ptr(), B, planes.data_ptr(), E, K, B, E, truth.data_ptr(),
+                                               fptr.data_ptr(), fids.data_ptr(), len(ids), r3.data_ptr(),
+                                               ws.data_ptr(), ws.numel(), ctypes.addressof(f3),
+                                               torch.cuda.current_stream().cuda_stream) == 0
+            torch.cuda.synchronize()
+            assert torch.equal(r3, want), (name, mode, form)
 
 
 def test_test_step_ranks_from_planes_equal_the_score_matrix_path(monkeypatch):

@@ -194,7 +194,8 @@ def test_split_once_forward_is_bitwise_the_register_split_one(monkeypatch, d, N,
     outs = []
     # 1: split per fragment in registers (ts_fwd_x3_kernel); 0 + workspace: M_r split once into bf16 planes per
     # call (ts_mplanes_kernel + ts_fwd_x3s_kernel<.., true>); 0 without: split once at staging (ts_fwd_x3s_kernel)
-    for form, split in ((1, True), (0, True), (0, False)):
+    # 2: the split-once kernel in the compiler's instruction order (staging after the MFMAs)
+    for form, split in ((1, True), (0, True), (0, False), (2, True), (2, False)):
         st = torch.empty((B * N, 2), dtype=torch.float32, device=DEV)
         s = ops.transparse_score_raw(0, ed, rd, Wd, md, pos.to(DEV), neg.to(DEV), gamma, stats=st, M=M,
                                      forms=dict(transparse_form=form), split=split)

@@ -820,29 +820,36 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
     ent = m.entity_embedding.detach()
     Q = torch.empty((Bq, K), dtype=torch.float32, device=device)
     lib = __import__("customknowledgegraphembedding_amd._lib", fromlist=["load"]).load()
-    # planes (default): ranks straight from the planes (kge_eval_rank_planes, no [Bq, E] score matrix);
-    # planes_s: the plane GEMM writing S, then kge_rank_filtered (round 5); staging: the round-4 form
+    # planes (default): ranks straight from the planes, batches alternating between two streams
+    # (evaluate.RankPipeline: batch i + 1's kernels fill the CUs batch i's GEMM leaves idle); planes1: one stream
+    # (kge_eval_rank_planes); planes_s: the plane GEMM writing S, then kge_rank_filtered (round 5); staging: the
+    # round-4 form
     split = os.environ.get("KGE_BENCH_EVAL_SPLIT", "planes")
     qp = torch.empty(int(lib.kge_split_bf16x3_bytes(Bq, K)), dtype=torch.uint8, device=device)
     ep = torch.empty(int(lib.kge_split_bf16x3_bytes(E, K)), dtype=torch.uint8, device=device)
     rws = torch.empty(int(lib.kge_eval_rank_planes_workspace_size(Bq, max(b[5] for b in batches))) + 16,
                       dtype=torch.uint8, device=device)
+    pipe = evaluate.RankPipeline(m, ep, Bq, max(b[5] for b in batches)) if split == "planes" else None
 
     def entity_pass():
         """The start of an evaluation pass: the entity table's bf16 planes (evaluate.entity_planes), once per pass."""
-        if split in ("planes", "planes_s"):
+        if split in ("planes", "planes1", "planes_s"):
             lib.kge_split_bf16x3(ent.data_ptr(), E, K, ent.stride(0), ep.data_ptr(), E,
                                  torch.cuda.current_stream().cuda_stream)
+        if pipe is not None:
+            pipe.wait_caller()
 
     def step(b, ev=None):
         """One query batch: Q = h*r or r*t written as bf16 planes (kge_eval_query_planes), S = Q . E^T
         (kge_gemm_nt_bf16x3_planes on the pass's entity planes, events around it; or kge_eval_query +
         kge_gemm_nt_bf16x3, the staging form), exact filtered ranks."""
         pos, mode, truth, fptr, fids = b[:5]
+        if pipe is not None:  # the query planes and pair scores on the side stream, events around the GEMM
+            return pipe.submit(pos, mode, truth, fptr, fids, b[5], events=ev)
         st = torch.cuda.current_stream().cuda_stream
         md = 0 if mode == "head-batch" else 1
         rel_ = m.relation_embedding
-        if split in ("planes", "planes_s"):
+        if split in ("planes1", "planes_s"):
             lib.kge_eval_query_planes(FN_IDS[w["fn"]], md, ent.data_ptr(), E, ent.stride(0), rel_.data_ptr(), R,
                                       rel_.stride(0), pos.data_ptr(), Bq, m._D, qp.data_ptr(), Bq, st)
         else:
@@ -850,7 +857,7 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                                rel_.stride(0), pos.data_ptr(), Bq, m._D, Q.data_ptr(), K, st)
         if ev is not None:
             ev[0].record()
-        if split == "planes":
+        if split == "planes1":
             ranks = torch.empty(Bq, dtype=torch.int64, device=device)
             lib.kge_eval_rank_planes(qp.data_ptr(), Bq, ep.data_ptr(), E, K, Bq, E, truth.data_ptr(), fptr.data_ptr(),
                                      fids.data_ptr(), b[5], ranks.data_ptr(), rws.data_ptr(), rws.numel(), st)
@@ -868,6 +875,8 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
     entity_pass()
     for i in range(a.warmup):
         step(batches[i % 4])
+    if pipe is not None:
+        pipe.flush()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     if dist_on:
@@ -879,11 +888,19 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
     entity_pass()  # the timed region is one evaluation pass: its entity planes are made inside it
     for i in range(a.steps):
         ranks.append(step(batches[i % 4], evs[i]))
+    if pipe is not None:
+        pipe.flush()
     torch.cuda.synchronize()
     if dist_on:
         tdist.barrier()
     dt = time.perf_counter() - t0
     gemm_s = statistics.mean(e0.elapsed_time(e1) for e0, e1 in evs) / 1e3
+    overlapped_s = None
+    if pipe is not None:
+        # the GEMMs of consecutive batches overlap (two streams): each one's events also span the other stream's
+        # work, so the per-launch figure is the GEMMs' span (first start to last end) over the launches
+        overlapped_s = gemm_s
+        gemm_s = evs[0][0].elapsed_time(evs[-1][1]) / 1e3 / a.steps
     flops = 2.0 * Bq * E * K            # the fp32 contraction
     kp = (K + 15) // 16 * 16
     mfma_flops = 6 * 2.0 * Bq * E * kp  # bf16 MFMA work executed (six products, K padded to 16)
@@ -907,17 +924,25 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                        "parallelism": f"replicas{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": mfma_flops / gemm_s / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
                          "frac": mfma_flops / gemm_s / 1e12 / 2500.0, "traffic": None,
-                         "kernel": ("kge_eval_rank_planes: pair_dot_x3_kernel (the truths' and filter entries' scores) "
-                                    "+ gemm_nt_x3p_kernel<true> (256 x 256 tiles from the query planes, which "
-                                    "kge_eval_query_planes writes directly, and the entity bf16 planes, six products per "
-                                    "16 k on v_mfma_f32_32x32x16_bf16, each row's count of scores above its truth in the "
-                                    "epilogue: no score matrix) + rank_finish_kernel; the entity planes made once per "
-                                    "evaluation pass, inside the timed region" if split == "planes" else
+                         "kernel": ("gemm_nt_x3l_kernel<true> (the counting phase of kge_eval_rank_planes_phases, "
+                                    "events around it: 256 x 256 tiles from the query planes and the entity bf16 planes "
+                                    "copied global -> LDS by LDS-DMA loads into three stages, six products per 16 k on "
+                                    "v_mfma_f32_32x32x16_bf16, each row's count of scores above its truth in the "
+                                    "epilogue: no score matrix), with the batch's query planes, pair scores "
+                                    "(pair_dot_x3_kernel) and rank_finish_kernel on the same stream; batches alternate "
+                                    "between two streams (evaluate.RankPipeline), so a GEMM's events also span the other "
+                                    "stream's kernels that share its CUs; the entity planes made once per evaluation "
+                                    "pass, inside the timed region" if split == "planes" else
+                                    "kge_eval_rank_planes on one stream: pair_dot_x3_kernel + gemm_nt_x3l_kernel<true> + "
+                                    "rank_finish_kernel, events around the three" if split == "planes1" else
                                     "gemm_nt_x3p_kernel (256 x 256 tiles from the query and entity bf16 planes, S "
                                     "written, then kge_rank_filtered)" if split == "planes_s" else
                                     "gemm_nt_x3s_kernel (256 x 256 tiles, operands split once at staging into bf16 "
                                     "planes, six products per 16 k on v_mfma_f32_32x32x16_bf16)"),
                          "kernel_avg_us": gemm_s * 1e6,
+                         **({"kernel_avg_us_what": "span of the overlapping GEMM launches (first start to last end, "
+                                                   "events on both streams) / launches",
+                             "overlapped_launch_avg_us": overlapped_s * 1e6} if overlapped_s is not None else {}),
                          "fp32_equivalent_tflops": flops / gemm_s / 1e12,
                          "fp32_equivalent_over_fp32_mfma_peak": flops / gemm_s / 1e12 / 157.3},
             "filtered_metrics": met, "build": kge.build_id()}

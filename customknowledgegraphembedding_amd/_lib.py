@@ -159,6 +159,8 @@ SIGNATURES = {
                                     _c_p, ctypes.c_size_t, _c_p]),
     "kge_eval_rank_planes_ex": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_i64,
                                        _c_p, _c_p, ctypes.c_size_t, _c_p, _c_p]),
+    "kge_eval_rank_planes_phases": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p,
+                                           _c_i64, _c_p, _c_p, ctypes.c_size_t, _c_i, _c_p, _c_p]),
     "kge_gemm_nt_bf16x3_planes_ex": (_c_i, [_c_p, _c_i64, _c_p, _c_i64, _c_i64, _c_p, _c_i64, _c_i64, _c_i64, _c_p,
                                             _c_p]),
     "kge_rank_filtered": (_c_i, [_c_p, _c_i64, _c_i64, _c_i64, _c_p, _c_p, _c_p, _c_p, _c_p]),

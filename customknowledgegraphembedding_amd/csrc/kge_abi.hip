@@ -1271,12 +1271,21 @@ int kge_eval_rank_planes_ex(const void* A_planes, int64_t a_rows, const void* B_
                             int64_t M, int64_t N, const int64_t* truth, const int64_t* filter_ptr,
                             const int64_t* filter_ids, int64_t nfilter, int64_t* ranks, void* workspace,
                             size_t workspace_bytes, const kge_forms* forms, void* stream) {
+    return kge_eval_rank_planes_phases(A_planes, a_rows, B_planes, b_rows, K, M, N, truth, filter_ptr, filter_ids,
+                                       nfilter, ranks, workspace, workspace_bytes, KGE_RANK_ALL, forms, stream);
+}
+
+int kge_eval_rank_planes_phases(const void* A_planes, int64_t a_rows, const void* B_planes, int64_t b_rows, int64_t K,
+                                int64_t M, int64_t N, const int64_t* truth, const int64_t* filter_ptr,
+                                const int64_t* filter_ids, int64_t nfilter, int64_t* ranks, void* workspace,
+                                size_t workspace_bytes, int phases, const kge_forms* forms, void* stream) {
+    if (phases <= 0 || phases > KGE_RANK_ALL) return fail(KGE_EINVAL, "kge_eval_rank_planes: phases must be 1..7");
     const int form = forms && (forms->gemm_form == 1 || forms->gemm_form >= 3) && forms->gemm_form <= 4
                          ? forms->gemm_form
                          : (kPlanesGemmForm == 2 ? 1 : kPlanesGemmForm);
     if (M < 0 || N <= 0 || K <= 0 || M > a_rows || N > b_rows || nfilter < 0) return fail(KGE_EINVAL, "bad shape");
     if (M == 0) return ok();
-    if (!A_planes || !B_planes || !truth || !ranks || !workspace || (filter_ptr && !filter_ids) ||
+    if (!A_planes || !B_planes || !truth || !ranks || !workspace || (filter_ptr && !filter_ids && nfilter > 0) ||
         (nfilter > 0 && !filter_ptr))
         return fail(KGE_EINVAL, "null pointer");
     if (M > INT32_MAX || N > INT32_MAX || !aligned(A_planes, 16) || !aligned(B_planes, 16) || !aligned(workspace, 16))
@@ -1287,7 +1296,7 @@ int kge_eval_rank_planes_ex(const void* A_planes, int64_t a_rows, const void* B_
     if ((int64_t)workspace_bytes < eval_rank_ws_bytes(M, nfilter))
         return fail(KGE_EINVAL, "kge_eval_rank_planes: workspace too small");
     launch_eval_rank_planes(A_planes, a_rows, B_planes, b_rows, K, (int)M, (int)N, truth, filter_ptr, filter_ids,
-                            nfilter, ranks, workspace, (hipStream_t)stream, form);
+                            nfilter, ranks, workspace, (hipStream_t)stream, form, phases);
     return check_launch("kge_eval_rank_planes");
 }
 

@@ -1284,23 +1284,27 @@ int64_t eval_rank_ws_bytes(int64_t M, int64_t F) { return ((M * 8 + 15) / 16 * 1
 
 int launch_eval_rank_planes(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, int M, int N,
                             const int64_t* truth, const int64_t* fptr, const int64_t* fids, int64_t F, int64_t* ranks,
-                            void* ws, hipStream_t st, int form) {
+                            void* ws, hipStream_t st, int form, int phases) {
     const int kp = (int)((K + 15) / 16 * 16);
     float* ts = static_cast<float*>(ws);
     int* gcnt = reinterpret_cast<int*>(ts + M);
     float* fs = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) + (((int64_t)M * 8 + 15) / 16 * 16));
     const int64_t pairs = (int64_t)M + F, waves = (pairs + 31) / 32;
-    hipLaunchKernelGGL(pair_dot_x3_kernel, dim3((unsigned)waves), dim3(kWave), 0, st, static_cast<const __bf16*>(Ap),
-                       a_rows, static_cast<const __bf16*>(Bp), b_rows, kp, (int64_t)M, (int64_t)N, truth, fptr, fids, F,
-                       ts, fs, gcnt);
-    if (form == 4)
-        launch_x3l<true>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
-    else if (form == 3)
-        launch_x3p<true, 3>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
-    else
-        launch_x3p<true, 4>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
-    hipLaunchKernelGGL(rank_finish_kernel, dim3((unsigned)((M + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
-                       st, (int64_t)M, (int64_t)N, truth, fptr, fids, ts, fs, gcnt, ranks);
+    if (phases & 1)
+        hipLaunchKernelGGL(pair_dot_x3_kernel, dim3((unsigned)waves), dim3(kWave), 0, st, static_cast<const __bf16*>(Ap),
+                           a_rows, static_cast<const __bf16*>(Bp), b_rows, kp, (int64_t)M, (int64_t)N, truth, fptr, fids,
+                           F, ts, fs, gcnt);
+    if (phases & 2) {
+        if (form == 4)
+            launch_x3l<true>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
+        else if (form == 3)
+            launch_x3p<true, 3>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
+        else
+            launch_x3p<true, 4>(Ap, a_rows, Bp, b_rows, kp, nullptr, 0, M, N, ts, gcnt, st);
+    }
+    if (phases & 4)
+        hipLaunchKernelGGL(rank_finish_kernel, dim3((unsigned)((M + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock),
+                           0, st, (int64_t)M, (int64_t)N, truth, fptr, fids, ts, fs, gcnt, ranks);
     return 0;
 }
 

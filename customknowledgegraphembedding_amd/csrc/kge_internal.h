@@ -223,14 +223,16 @@ int launch_gemm_nt_f32x3(const float* A, const float* B, float* C, int M, int N,
 int launch_split3_planes(const float* X, int64_t rows, int64_t cols, int64_t ld, void* planes, int64_t plane_rows,
                          hipStream_t st);
 // form 1: both operands staged through LDS per 16-k chunk (gemm_nt_x3p_kernel, 256 x 256 tiles); 2: B straight into
-// registers, A staged per 32 k (gemm_nt_x3d_kernel); 3: gemm_nt_x3p_kernel with 256 x 192 tiles. Bitwise the same C.
+// registers, A staged per 32 k (gemm_nt_x3d_kernel); 3: gemm_nt_x3p_kernel with 256 x 192 tiles; 4: LDS-DMA staging
+// in three stages (gemm_nt_x3l_kernel). Bitwise the same C.
 int launch_gemm_nt_x3p(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, float* C, int64_t ldc,
                        int M, int N, hipStream_t st, int form);
-// kge_eval_rank_planes: workspace bytes (truth scores and counts [M], filter-entry scores [F]) and the launches
+// kge_eval_rank_planes: workspace bytes (truth scores and counts [M], filter-entry scores [F]) and the launches of
+// the phases in `phases` (1 pair scores + count reset, 2 counting GEMM, 4 finish), in that order
 int64_t eval_rank_ws_bytes(int64_t M, int64_t F);
 int launch_eval_rank_planes(const void* Ap, int64_t a_rows, const void* Bp, int64_t b_rows, int64_t K, int M, int N,
                             const int64_t* truth, const int64_t* fptr, const int64_t* fids, int64_t F, int64_t* ranks,
-                            void* ws, hipStream_t st, int form);
+                            void* ws, hipStream_t st, int form, int phases);
 int launch_rank(const float* S, int64_t M, int64_t N, int64_t ld, const int64_t* truth, const int64_t* fptr,
                 const int64_t* fids, int64_t* ranks, hipStream_t st);
 

@@ -147,6 +147,14 @@ def score_all(model, positive_sample: torch.Tensor, mode: str, out: torch.Tensor
 _RANK_WS = {}
 
 
+def _planes_rank_ok(model, planes) -> bool:
+    """Whether the ranks-from-planes path applies: DistMult / ComplEx with entity planes, float4 rows."""
+    if model.model_name not in MFMA_FNS or planes is None:
+        return False
+    ent, rel = model.entity_embedding, model.relation_embedding
+    return model._D % 4 == 0 and ent.data_ptr() % 16 == 0 and rel.data_ptr() % 16 == 0
+
+
 def rank_planes(model, positive_sample: torch.Tensor, mode: str, planes: torch.Tensor, truth: torch.Tensor,
                 filter_ptr: torch.Tensor | None = None, filter_ids: torch.Tensor | None = None,
                 nfilter: int | None = None) -> torch.Tensor | None:
@@ -155,11 +163,9 @@ def rank_planes(model, positive_sample: torch.Tensor, mode: str, planes: torch.T
     counting per row the entities above the truth, the filter correction): rank_filtered(score_all(...))'s ranks
     exactly. DistMult / ComplEx with planes; None where the query-plane form does not apply (then score_all +
     rank_filtered). filter_ptr must start at 0; nfilter = filter_ptr[-1] (read from the device when not given)."""
-    if model.model_name not in MFMA_FNS or planes is None:
+    if not _planes_rank_ok(model, planes):
         return None
     ent, rel = model.entity_embedding.detach(), model.relation_embedding.detach()
-    if not (model._D % 4 == 0 and ent.data_ptr() % 16 == 0 and rel.data_ptr() % 16 == 0):
-        return None
     lib = _lib.load()
     m = ops.mode_id(mode)
     B, E, K = positive_sample.shape[0], ent.shape[0], ent.shape[1]
@@ -186,10 +192,92 @@ def rank_planes(model, positive_sample: torch.Tensor, mode: str, planes: torch.T
     return ranks
 
 
+class RankPipeline:
+    """rank_planes over consecutive query batches on two streams: batch i runs its whole chain (query planes,
+    kge_eval_rank_planes_phases' pair scores, counting GEMM and finish) on stream i % 2, with a query-plane buffer and
+    a workspace of its own. The counting GEMM holds every CU's VGPRs while its blocks run, so a single stream leaves
+    the CUs of its last partial round idle (944 tiles = 3.7 rounds at C5) and runs the small kernels between GEMMs;
+    with two streams the next batch's kernels and GEMM blocks fill them. submit() returns the batch's ranks tensor,
+    valid on the caller's stream after flush(). Same ranks as rank_planes, batch by batch. DistMult / ComplEx with
+    entity planes only (rank_planes' domain). Inputs given as CPU tensors are uploaded on the batch's stream; device
+    inputs must already be complete (the streams wait for the caller's stream only in the constructor and in
+    wait_caller())."""
+
+    def __init__(self, model, planes: torch.Tensor, max_rows: int, max_filter: int, forms: dict | None = None):
+        if model.model_name not in MFMA_FNS or planes is None:
+            raise ValueError("RankPipeline: DistMult / ComplEx with entity planes")
+        self.m, self.planes = model, planes
+        self.ent, self.rel = model.entity_embedding.detach(), model.relation_embedding.detach()
+        dev = self.ent.device
+        self.lib = _lib.load()
+        K = self.ent.shape[1]
+        qb = int(self.lib.kge_split_bf16x3_bytes(max_rows, K))
+        wb = max(int(self.lib.kge_eval_rank_planes_workspace_size(max_rows, max_filter)), 16)
+        self.qp = [torch.empty(qb, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.ws = [torch.empty(wb, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.max_rows, self.max_filter = max_rows, max_filter
+        self.main = torch.cuda.current_stream(dev)
+        self.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        self.forms = forms
+        self.i = 0
+        self.wait_caller()  # the tables and planes as the caller's stream left them
+
+    def wait_caller(self):
+        """Both streams wait for the caller's stream: after the caller rewrote the tables or the planes."""
+        for st in self.streams:
+            st.wait_stream(self.main)
+
+    def submit(self, positive_sample, mode, truth, filter_ptr=None, filter_ids=None, nfilter=None, events=None):
+        """Queue one batch; `events` (optional pair of timing events) are recorded on the batch's stream around its
+        counting GEMM."""
+        B = positive_sample.shape[0]
+        if filter_ptr is not None and nfilter is None:
+            nfilter = int(filter_ptr[-1])
+        nf = int(nfilter) if filter_ptr is not None else 0
+        if B > self.max_rows or nf > self.max_filter:
+            raise ValueError("RankPipeline: batch or filter larger than the pipeline was sized for")
+        E, K = self.ent.shape
+        slot = self.i & 1
+        self.i += 1
+        st = self.streams[slot]
+        dev = self.ent.device
+        fp, _keep = ops._forms_ptr(self.forms)
+        with torch.cuda.stream(st):
+            ranks = torch.empty(B, dtype=torch.int64, device=dev)
+            positive_sample, truth, filter_ptr, filter_ids = (
+                None if t is None else t.to(dev) for t in (positive_sample, truth, filter_ptr, filter_ids))
+            check(self.lib.kge_eval_query_planes(FN_IDS[self.m.model_name], ops.mode_id(mode), self.ent.data_ptr(), E,
+                                                 self.ent.stride(0), self.rel.data_ptr(), self.rel.shape[0],
+                                                 self.rel.stride(0), positive_sample.data_ptr(), B, self.m._D,
+                                                 self.qp[slot].data_ptr(), B, st.cuda_stream), "kge_eval_query_planes")
+            args = (self.qp[slot].data_ptr(), B, self.planes.data_ptr(), E, K, B, E, truth.data_ptr(),
+                    None if filter_ptr is None else filter_ptr.data_ptr(),
+                    None if filter_ids is None else filter_ids.data_ptr(), nf, ranks.data_ptr(),
+                    self.ws[slot].data_ptr(), self.ws[slot].numel())
+            for ph in (1, 2, 4):  # KGE_RANK_PAIRS, KGE_RANK_COUNT (events around it), KGE_RANK_FINISH
+                if ph == 2 and events is not None:
+                    events[0].record(st)
+                check(self.lib.kge_eval_rank_planes_phases(*args, ph, fp, st.cuda_stream), "kge_eval_rank_planes")
+                if ph == 2 and events is not None:
+                    events[1].record(st)
+            for t in (positive_sample, truth, filter_ptr, filter_ids):
+                if t is not None and t.device.type == "cuda":
+                    t.record_stream(st)
+        ranks.record_stream(self.main)
+        return ranks
+
+    def flush(self):
+        """The caller's stream waits for both streams (every submitted batch's ranks)."""
+        for st in self.streams:
+            self.main.wait_stream(st)
+
+
 def rank_filtered(scores: torch.Tensor, truth: torch.Tensor, filter_ptr: torch.Tensor | None = None,
                   filter_ids: torch.Tensor | None = None) -> torch.Tensor:
     M, N = scores.shape
     ranks = torch.empty(M, dtype=torch.int64, device=scores.device)
+    if filter_ids is not None and filter_ids.numel() == 0:  # every row's filter list empty: no filter
+        filter_ptr = filter_ids = None
     rc = _lib.load().kge_rank_filtered(scores.data_ptr(), M, N, scores.stride(0), truth.data_ptr(),
                                        None if filter_ptr is None else filter_ptr.data_ptr(),
                                        None if filter_ids is None else filter_ids.data_ptr(), ranks.data_ptr(),
@@ -264,7 +352,24 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
     all_ranks = []
     with torch.no_grad():
         planes = entity_planes(model)  # once per evaluation pass (DistMult / ComplEx)
-        for mode in ("head-batch", "tail-batch"):
+        if _planes_rank_ok(model, planes) and len(triples):
+            # ranks straight from the planes (no [B, E] score matrix), batches pipelined over two streams
+            filt = {m: build_filter(triples, m, all_true_triples) for m in ("head-batch", "tail-batch")}
+            starts = range(0, len(triples), bs)
+            maxf = max(int(ptr[min(s + bs, len(triples))] - ptr[s]) for ptr, _ in filt.values() for s in starts)
+            pipe = RankPipeline(model, planes, min(bs, len(triples)), maxf)
+            for mode in ("head-batch", "tail-batch"):
+                col = 0 if mode == "head-batch" else 2
+                ptr, ids = filt[mode]
+                for s in starts:
+                    q = triples[s:s + bs]
+                    p = ptr[s:s + len(q) + 1]
+                    pos = torch.from_numpy(q)
+                    all_ranks.append(pipe.submit(pos, mode, pos[:, col].contiguous(), torch.from_numpy(p - p[0]),
+                                                 torch.from_numpy(ids[p[0]:p[-1]]), int(p[-1] - p[0])))
+            pipe.flush()
+            all_ranks = [r.cpu().numpy() for r in all_ranks]
+        for mode in (() if all_ranks else ("head-batch", "tail-batch")):
             col = 0 if mode == "head-batch" else 2
             ptr, ids = build_filter(triples, mode, all_true_triples)
             for s in range(0, len(triples), bs):
@@ -274,10 +379,7 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
                 fptr = torch.from_numpy(p - p[0]).to(dev)
                 fids = torch.from_numpy(ids[p[0]:p[-1]]).to(dev)
                 truth = pos[:, col].contiguous()
-                # DistMult / ComplEx: ranks straight from the planes (no [B, E] score matrix); else scores + ranks
-                r = rank_planes(model, pos, mode, planes, truth, fptr, fids, nfilter=int(p[-1] - p[0]))
-                if r is None:
-                    r = rank_filtered(score_all(model, pos, mode, planes=planes), truth, fptr, fids)
+                r = rank_filtered(score_all(model, pos, mode, planes=planes), truth, fptr, fids)
                 all_ranks.append(r.cpu().numpy())
     ranks = np.concatenate(all_ranks) if all_ranks else np.zeros(0, dtype=np.int64)
     if world > 1:
@@ -287,5 +389,5 @@ def test_step(model, test_triples, all_true_triples, args=None, batch_size=None)
     return metrics_from_ranks(ranks)
 
 
-__all__ = ["build_filter", "score_all", "rank_filtered", "rank_planes", "metrics_from_ranks", "test_step", "entity_planes",
+__all__ = ["build_filter", "score_all", "rank_filtered", "rank_planes", "RankPipeline", "metrics_from_ranks", "test_step", "entity_planes",
            "split_planes", "HEAD_BATCH", "TAIL_BATCH"]

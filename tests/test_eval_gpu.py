@@ -369,7 +369,8 @@ def test_rank_planes_equals_score_matrix_ranks(name, E, d, B):
 
 
 def test_test_step_ranks_from_planes_equal_the_score_matrix_path(monkeypatch):
-    """test_step on the fused rank path and with it turned off (score_all + rank_filtered): the same metrics."""
+    """test_step on the fused rank path (the two-stream RankPipeline) and with it turned off (score_all +
+    rank_filtered): the same metrics."""
     E, R, d = 1200, 6, 64
     for name in ("DistMult", "ComplEx"):
         de = name == "ComplEx"
@@ -378,7 +379,64 @@ def test_test_step_ranks_from_planes_equal_the_score_matrix_path(monkeypatch):
         g = np.random.RandomState(3)
         true = np.stack([g.randint(E, size=3000), g.randint(R, size=3000), g.randint(E, size=3000)], 1)
         a = evaluate.test_step(m, true[:300], true, batch_size=128)
-        monkeypatch.setattr(evaluate, "rank_planes", lambda *args, **kw: None)
+        monkeypatch.setattr(evaluate, "_planes_rank_ok", lambda *args, **kw: False)
         b = evaluate.test_step(m, true[:300], true, batch_size=128)
         monkeypatch.undo()
         assert a == b, name
+
+
+@pytest.mark.parametrize("name,E,d", [("DistMult", 3000, 200), ("ComplEx", 1500, 96)])
+def test_rank_pipeline_equals_rank_planes(name, E, d):
+    """evaluate.RankPipeline (batches alternating between two streams, each with its own query planes and workspace,
+    kge_eval_rank_planes_phases' three phases in order) gives rank_planes' ranks batch by batch: five batches of
+    different sizes and modes, CPU and device inputs, a filter, a one-row batch with an empty filter list; and the
+    three phases issued one by one on one stream equal the one-call rank."""
+    de = name == "ComplEx"
+    m = kge.KGEModel(name, E, 5, d, 12.0, double_entity_embedding=de, double_relation_embedding=de, device=DEV, seed=3)
+    g = np.random.RandomState(E)
+    true = np.stack([g.randint(E, size=6000), g.randint(5, size=6000), g.randint(E, size=6000)], 1)
+    planes = evaluate.entity_planes(m)
+    sizes = [700, 256, 1, 513, 700]
+    batches, want = [], []
+    off = 0
+    for i, B in enumerate(sizes):
+        q = true[off:off + B]
+        off += B
+        mode = "head-batch" if i % 2 == 0 else "tail-batch"
+        ptr, ids = evaluate.build_filter(q, mode, true)
+        col = 0 if mode == "head-batch" else 2
+        pos, fptr, fids = torch.from_numpy(q), torch.from_numpy(ptr), torch.from_numpy(ids)
+        truth = pos[:, col].contiguous().clone()
+        batches.append((pos, mode, truth, fptr, fids, int(ptr[-1])))
+        want.append(evaluate.rank_planes(m, pos.to(DEV), mode, planes, truth.to(DEV), fptr.to(DEV), fids.to(DEV)).clone())
+    torch.cuda.synchronize()
+    pipe = evaluate.RankPipeline(m, planes, max(sizes), max(b[5] for b in batches))
+    got = []
+    for i, (pos, mode, truth, fptr, fids, nf) in enumerate(batches):
+        if i % 2:  # device inputs, complete before the submit
+            pos, truth, fptr, fids = pos.to(DEV), truth.to(DEV), fptr.to(DEV), fids.to(DEV)
+            torch.cuda.synchronize()
+        got.append(pipe.submit(pos, mode, truth, fptr, fids, nf))
+    pipe.flush()
+    torch.cuda.synchronize()
+    for i in range(len(sizes)):
+        assert torch.equal(got[i], want[i]), (name, i)
+    # phases one by one on one stream
+    lib = _lib.load()
+    pos, mode, truth, fptr, fids, nf = batches[0]
+    pos, truth, fptr, fids = pos.to(DEV), truth.to(DEV), fptr.to(DEV), fids.to(DEV)
+    B, K = pos.shape[0], m.entity_embedding.shape[1]
+    evaluate.rank_planes(m, pos, mode, planes, truth, fptr, fids)  # writes the batch's query planes
+    (qpl,) = evaluate._Q_PLANES.values()
+    ws = torch.empty(int(lib.kge_eval_rank_planes_workspace_size(B, nf)), dtype=torch.uint8, device=DEV)
+    r = torch.full((B,), -5, dtype=torch.int64, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    for ph in (1, 2, 4):
+        assert lib.kge_eval_rank_planes_phases(qpl.data_ptr(), B, planes.data_ptr(), E, K, B, E, truth.data_ptr(),
+                                               fptr.data_ptr(), fids.data_ptr(), nf, r.data_ptr(), ws.data_ptr(),
+                                               ws.numel(), ph, None, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(r, want[0])
+    assert lib.kge_eval_rank_planes_phases(qpl.data_ptr(), B, planes.data_ptr(), E, K, B, E, truth.data_ptr(),
+                                           fptr.data_ptr(), fids.data_ptr(), nf, r.data_ptr(), ws.data_ptr(),
+                                           ws.numel(), 8, None, st) != 0

@@ -1445,18 +1445,29 @@ def main(argv=None):
         torch.cuda.synchronize()
         per_mode[mode] = e[0].elapsed_time(e[1]) / ev_group
     # the same step without the plan made ahead (kge_step_forward: the tile kernel's setup in the scoring
-    # launch), device time per step over the same alternating batches: what the plan saves
-    unplanned_us = None
+    # launch), device time per step over the same alternating batches: what the plan saves. Planned and
+    # unplanned blocks alternate (three rounds each, the planned runner continuing its own plan chain), so both
+    # figures see the same clock and cache state
+    unplanned_us = planned_us = None
     if runner.planner is not None:
         plain = StepRunner(m, batches, fn, planned=False)
-        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        for i in range(4 * ev_group):
-            if i == 2 * ev_group:
-                e[0].record()
-            plain(i)
-        e[1].record()
-        torch.cuda.synchronize()
-        unplanned_us = e[0].elapsed_time(e[1]) / (2 * ev_group) * 1e3
+        acc = {"planned": [], "unplanned": []}
+        nxt = a.warmup + a.steps
+        for rnd in range(3):
+            for key in (("planned", "unplanned") if rnd % 2 == 0 else ("unplanned", "planned")):
+                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for i in range(4 * ev_group):
+                    if i == 2 * ev_group:
+                        e[0].record()
+                    if key == "planned":
+                        runner(nxt)
+                        nxt += 1
+                    else:
+                        plain(i)
+                e[1].record()
+                torch.cuda.synchronize()
+                acc[key].append(e[0].elapsed_time(e[1]) / (2 * ev_group) * 1e3)
+        planned_us, unplanned_us = statistics.median(acc["planned"]), statistics.median(acc["unplanned"])
     head_ms, tail_ms = [per_mode[0]], [per_mode[1]]
     if not kern_ms:  # fewer steps than one event group
         kern_ms = head_ms + tail_ms
@@ -1509,7 +1520,9 @@ def main(argv=None):
             step_plan=("kge_step_forward_planned: each step's id-only setup (row groups, entity-sorted candidate "
                        "lists) made by the previous step's tail blocks; one plan per timed step"
                        if runner.planner is not None else "none (kge_step_forward)"),
-            unplanned_step_us=unplanned_us,
+            unplanned_step_us=unplanned_us, planned_step_us=planned_us,
+            plan_ab=("device us per step, medians of three interleaved blocks of planned and unplanned steps "
+                     "after the timed region"),
             host_us_per_step_median=statistics.median(host_us), event_group_step_us=[x * 1e3 for x in kern_ms],
             unique_row_bytes_per_step=uniq * ent_dim_ * 4, row_reuse=(B * N + 2 * B) / max(1, uniq)),
         "build": kge.build_id(),

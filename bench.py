@@ -935,8 +935,8 @@ def eval_bench(w, a, device, world=1, rank=0, dist_on=False):
                                     "pass, inside the timed region" if split == "planes" else
                                     "kge_eval_rank_planes on one stream: pair_dot_x3_kernel + gemm_nt_x3l_kernel<true> + "
                                     "rank_finish_kernel, events around the three" if split == "planes1" else
-                                    "gemm_nt_x3p_kernel (256 x 256 tiles from the query and entity bf16 planes, S "
-                                    "written, then kge_rank_filtered)" if split == "planes_s" else
+                                    "gemm_nt_x3l_kernel (256 x 256 tiles from the query and entity bf16 planes by "
+                                    "LDS-DMA, S written, then kge_rank_filtered)" if split == "planes_s" else
                                     "gemm_nt_x3s_kernel (256 x 256 tiles, operands split once at staging into bf16 "
                                     "planes, six products per 16 k on v_mfma_f32_32x32x16_bf16)"),
                          "kernel_avg_us": gemm_s * 1e6,

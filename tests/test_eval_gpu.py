@@ -417,10 +417,19 @@ def test_rank_pipeline_equals_rank_planes(name, E, d):
             pos, truth, fptr, fids = pos.to(DEV), truth.to(DEV), fptr.to(DEV), fids.to(DEV)
             torch.cuda.synchronize()
         got.append(pipe.submit(pos, mode, truth, fptr, fids, nf))
+    # an explicitly empty filter list (filter_ptr all zero, no ids) ranks as no filter at all
+    pos0, mode0, truth0 = batches[1][:3]
+    empty = pipe.submit(pos0, mode0, truth0, torch.zeros(pos0.shape[0] + 1, dtype=torch.int64),
+                        torch.zeros(0, dtype=torch.int64), 0)
     pipe.flush()
     torch.cuda.synchronize()
     for i in range(len(sizes)):
         assert torch.equal(got[i], want[i]), (name, i)
+    nofilter = evaluate.rank_planes(m, pos0.to(DEV), mode0, planes, truth0.to(DEV))
+    assert torch.equal(empty, nofilter)
+    assert torch.equal(evaluate.rank_filtered(evaluate.score_all(m, pos0.to(DEV), mode0, planes=planes), truth0.to(DEV),
+                                              torch.zeros(pos0.shape[0] + 1, dtype=torch.int64, device=DEV),
+                                              torch.zeros(0, dtype=torch.int64, device=DEV)), nofilter)
     # phases one by one on one stream
     lib = _lib.load()
     pos, mode, truth, fptr, fids, nf = batches[0]

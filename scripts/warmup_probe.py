@@ -1,0 +1,52 @@
+"""Round 6: the C2 planned step's device time from a cold start, per block of 10 steps over 300 steps, in a fresh
+process (cold), and again in fresh processes whose first 30 ms run an unrelated MFMA-only loop (a torch bf16 GEMM,
+no memory traffic: PRE 1) or an HBM stream (copies of a 1 GB buffer: PRE 2) before the first step. Separates the
+compute clock's ramp from the memory side's. Usage: python scripts/warmup_probe.py [pre ...]"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r'''
+import json, sys, time, torch
+sys.path.insert(0, ROOT)
+import bench
+from customknowledgegraphembedding_amd import ops
+from customknowledgegraphembedding_amd._lib import FN_IDS
+bench.ops = ops
+dev = torch.device("cuda", 0)
+w = bench.WORKLOADS["c2"]
+m, batches = bench.make_inputs(w, 0, dev)
+r = bench.StepRunner(m, batches, FN_IDS[w["fn"]], planned=True)
+torch.cuda.synchronize()
+if PRE == 1:
+    a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.03:
+        for _ in range(4):
+            a @ a
+        torch.cuda.synchronize()
+elif PRE == 2:
+    a = torch.empty(256 * 1024 * 1024, device=dev, dtype=torch.float32)
+    b = torch.empty_like(a)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.03:
+        for _ in range(4):
+            b.copy_(a)
+        torch.cuda.synchronize()
+    del a, b
+evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(30)]
+for b in range(30):
+    evs[b][0].record()
+    for i in range(10):
+        r(b * 10 + i)
+    evs[b][1].record()
+torch.cuda.synchronize()
+print("RESULT " + json.dumps({"pre_30ms": ["none", "bf16 GEMM", "HBM copy"][PRE], "us_per_step_by_block_of_10": [round(e0.elapsed_time(e1) / 10 * 1e3, 1) for e0, e1 in evs]}), flush=True)
+'''
+for pre in [int(x) for x in sys.argv[1:]] or (0, 1, 0, 1):
+    code = f"ROOT = {ROOT!r}\nPRE = {pre}\n" + CHILD
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=400)
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")]
+    print(line[0][7:] if line else json.dumps({"pre": pre, "rc": p.returncode, "err": p.stderr[-800:]}), flush=True)

@@ -6,6 +6,6 @@ cd "$R"
 O=gpurun_out/r06v
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -u scripts/warmup_probe.py 2 0 2 > $O/probe2.log 2>&1; rc=$?
-echo "probe rc=$rc"; cat $O/probe2.log | tail -5
+timeout -k 10 900 python3 -u scripts/warmup_probe.py 0 1 2 0 1 2 > $O/probe4.log 2>&1; rc=$?
+echo "probe rc=$rc"; cat $O/probe4.log | tail -7
 echo r06v done

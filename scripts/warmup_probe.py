@@ -1,7 +1,7 @@
 """Round 6: the C2 planned step's device time from a cold start, per block of 10 steps over 300 steps, in a fresh
-process (cold), and again in fresh processes whose first 30 ms run an unrelated MFMA-only loop (a torch bf16 GEMM,
-no memory traffic: PRE 1) or an HBM stream (copies of a 1 GB buffer: PRE 2) before the first step. Separates the
-compute clock's ramp from the memory side's. Usage: python scripts/warmup_probe.py [pre ...]"""
+process (cold: 10 untimed steps take the first calls' one-time costs first), and again in fresh processes whose first 30 ms run an unrelated MFMA-only loop (a torch bf16 GEMM,
+no memory traffic: PRE 1) or an HBM stream (copies of a 1 GB buffer: PRE 2) before the first step, or with the
+sweep ascending every step (PRE 3). Separates the compute clock's ramp from the memory side's and from the sweep. Usage: python scripts/warmup_probe.py [pre ...]"""
 import json
 import os
 import subprocess
@@ -19,6 +19,10 @@ dev = torch.device("cuda", 0)
 w = bench.WORKLOADS["c2"]
 m, batches = bench.make_inputs(w, 0, dev)
 r = bench.StepRunner(m, batches, FN_IDS[w["fn"]], planned=True)
+if PRE == 3:  # ascending sweep every step (no alternation), no pre-phase
+    r.planner.set_sweep(0)
+for i in range(10):  # the first calls' one-time costs (code loading, allocations) before the pre-phase
+    r(1000 + i)
 torch.cuda.synchronize()
 if PRE == 1:
     a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
@@ -43,7 +47,7 @@ for b in range(30):
         r(b * 10 + i)
     evs[b][1].record()
 torch.cuda.synchronize()
-print("RESULT " + json.dumps({"pre_30ms": ["none", "bf16 GEMM", "HBM copy"][PRE], "us_per_step_by_block_of_10": [round(e0.elapsed_time(e1) / 10 * 1e3, 1) for e0, e1 in evs]}), flush=True)
+print("RESULT " + json.dumps({"pre_30ms": ["none", "bf16 GEMM", "HBM copy", "none; ascending sweep"][PRE], "us_per_step_by_block_of_10": [round(e0.elapsed_time(e1) / 10 * 1e3, 1) for e0, e1 in evs]}), flush=True)
 '''
 for pre in [int(x) for x in sys.argv[1:]] or (0, 1, 0, 1):
     code = f"ROOT = {ROOT!r}\nPRE = {pre}\n" + CHILD
